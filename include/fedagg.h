@@ -1,0 +1,161 @@
+/*
+ * fedagg.h — C ABI of libfedagg.so, the MI355X (gfx950) server-side federated
+ * aggregation kernels.
+ *
+ * This is the drop-in boundary for FedML's server-side FedAvg reduction.  Every
+ * entry point below replaces one arithmetic loop of the reference:
+ *
+ *   FedMLAggOperator.agg -> model_aggregator -> torch_aggregator
+ *     python/fedml/ml/aggregator/agg_operator.py:10-30, :223-234, :33-134
+ *
+ * Conventions (all entry points):
+ *   - Every pointer argument is a DEVICE pointer; the caller allocates and owns
+ *     it.  No entry point allocates, frees or synchronises: they are
+ *     asynchronous, stream-ordered and capturable into a hipGraph.
+ *   - A "source table" `d_src` is a device array of K device pointers, one per
+ *     client, in the client order of the reference's raw_grad_list.
+ *   - `d_w` holds the per-client weights precomputed on the host exactly as the
+ *     reference does: w_i = float32(float64(n_i) / float64(sum_j n_j))
+ *     (agg_operator.py:24-28 and :39; the Python float is rounded to the tensor
+ *     opmath type float32 by torch's mul-by-scalar).
+ *   - `flags` bit FEDAGG_ALIGNED16 asserts that every source and output pointer
+ *     is 16-byte aligned; then the 16-byte vector path is used, otherwise a
+ *     scalar path of identical arithmetic.
+ *   - Return value: 0 on success, otherwise a FEDAGG_E* code or a hipError_t
+ *     (> 0).  fedagg_last_error() returns a thread-local description.
+ *   - Thread-safe: no mutable global state apart from the thread-local error.
+ *
+ * Arithmetic contract (bit-exact with the reference on the same inputs):
+ *   acc = fl(p_0 * w_0);  acc = fl(acc + fl(p_i * w_i)) for i = 1..K-1,
+ *   two separately rounded IEEE operations (never an FMA), clients in order.
+ */
+#ifndef FEDAGG_H_
+#define FEDAGG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* hipStream_t is an opaque pointer; declared here so that callers (ctypes, cgo)
+ * need no HIP headers.  Pass 0 for the null stream. */
+typedef void* fedagg_stream_t;
+
+#define FEDAGG_OK 0
+#define FEDAGG_EINVAL (-1)      /* bad argument (K < 1, N < 0, null pointer) */
+#define FEDAGG_ENOKERNEL (-2)   /* no kernel for this configuration */
+
+#define FEDAGG_ALIGNED16 1u     /* flags: all pointers 16-byte aligned */
+
+/* bf16 / f16 accumulation modes (see fedagg_wsum_bf16) */
+#define FEDAGG_ACC_REFERENCE 0  /* round to bf16/f16 after every mul and add, as torch CPU does */
+#define FEDAGG_ACC_FP32 1       /* accumulate in fp32, round once at the end */
+
+/* ---- FedAvg / FedProx weighted sum ------------------------------------- */
+
+/* fp32 clients -> fp32 average.
+ * Replaces agg_operator.py:35-44 (FedAvg) and :45-54 (FedProx) for fp32 keys;
+ * same arithmetic as simulation/sp/fedavg/fedavg_api.py:144-159 and
+ * simulation/mpi/fedopt/FedOptAggregator.py:93-101.
+ * Also used as the client-axis partial of the multi-GPU mode (w_i are then the
+ * GLOBAL weights, the partial is over this GPU's clients only). */
+int fedagg_wsum_f32(const float* const* d_src, const float* d_w, int32_t K,
+                    int64_t N, float* d_out, uint32_t flags,
+                    fedagg_stream_t stream);
+
+/* bf16 clients -> bf16 average (agg_operator.py:35-44 for bf16 keys).
+ * acc_mode FEDAGG_ACC_REFERENCE reproduces torch's CPU chain bit-exactly:
+ *   acc = bf16(f32(p_0) * w_0);  acc = bf16(f32(acc) + f32(bf16(f32(p_i) * w_i))).
+ * acc_mode FEDAGG_ACC_FP32 keeps an fp32 accumulator and rounds once. */
+int fedagg_wsum_bf16(const uint16_t* const* d_src, const float* d_w, int32_t K,
+                     int64_t N, uint16_t* d_out, int32_t acc_mode,
+                     uint32_t flags, fedagg_stream_t stream);
+
+/* bf16 clients -> fp32 partial (fp32 accumulate, no final rounding): the
+ * per-GPU pre-reduction of the client-axis multi-GPU mode. */
+int fedagg_wsum_bf16_f32out(const uint16_t* const* d_src, const float* d_w,
+                            int32_t K, int64_t N, float* d_out,
+                            uint32_t flags, fedagg_stream_t stream);
+
+/* fp16 clients -> fp16 average; acc_mode as for bf16. */
+int fedagg_wsum_f16(const uint16_t* const* d_src, const float* d_w, int32_t K,
+                    int64_t N, uint16_t* d_out, int32_t acc_mode,
+                    uint32_t flags, fedagg_stream_t stream);
+
+/* fp64 clients -> fp64 average; d_w64 holds the float64 weights n_i / sum n
+ * (a Python float times a double tensor is a double multiply). */
+int fedagg_wsum_f64(const double* const* d_src, const double* d_w64, int32_t K,
+                    int64_t N, double* d_out, uint32_t flags,
+                    fedagg_stream_t stream);
+
+/* int64 clients -> fp32 average.  torch promotes int64 * Python float to the
+ * default dtype float32: acc = fl32(fl32(v_0) * w_0); acc = fl32(acc + fl32(fl32(v_i) * w_i)).
+ * This is what happens to BatchNorm num_batches_tracked in the reference. */
+int fedagg_wsum_i64_f32(const int64_t* const* d_src, const float* d_w,
+                        int32_t K, int64_t N, float* d_out, uint32_t flags,
+                        fedagg_stream_t stream);
+
+/* ---- FedAvg_seq / FedDyn unweighted sum -------------------------------- */
+
+/* out = p_0 + p_1 + ... + p_{K-1} in the source dtype, sequential order.
+ * Replaces agg_operator.py:55-63 (FedAvg_seq) and :68-77 (FedDyn).  The
+ * reference aliases client 0's tensor and adds into it in place; pass
+ * d_out == d_src[0] (host-side value) to reproduce that.  dtype codes:
+ * FEDAGG_DT_* below. */
+#define FEDAGG_DT_F32 0
+#define FEDAGG_DT_BF16 1
+#define FEDAGG_DT_F16 2
+#define FEDAGG_DT_F64 3
+#define FEDAGG_DT_I64 4
+#define FEDAGG_DT_I32 5
+int fedagg_sum(int32_t dtype, const void* const* d_src, int32_t K, int64_t N,
+               void* d_out, uint32_t flags, fedagg_stream_t stream);
+
+/* ---- Multi-tensor (one launch over every state-dict key) --------------- */
+
+/* T tensors ("keys") of one dtype, each with its own K client pointers and
+ * element count, reduced in ONE launch (the per-key loop of agg_operator.py:36
+ * becomes a segment table).  d_src is a [T][K] device pointer table, d_out a
+ * [T] device pointer table, d_numel a [T] device int64 array, and
+ * d_block_begin a [T+1] device int64 prefix array of workgroup offsets that the
+ * host computed with fedagg_multi_blocks() for the same numels.
+ * Supported dtype codes: FEDAGG_DT_F32 only (other dtypes go key by key). */
+int64_t fedagg_multi_blocks(int32_t dtype, int64_t numel);
+int fedagg_wsum_multi_f32(const float* const* d_src, float* const* d_out,
+                          const int64_t* d_numel, const int64_t* d_block_begin,
+                          int32_t T, const float* d_w, int32_t K,
+                          int64_t total_blocks, fedagg_stream_t stream);
+
+/* ---- FedOpt server step (fused epilogue) ------------------------------- */
+
+/* Server SGD with momentum over named parameters, fused with the pseudo
+ * gradient (simulation/mpi/fedopt/FedOptAggregator.py:104-130 with
+ * torch.optim.SGD, dampening 0, nesterov False, weight_decay 0):
+ *   g     = p_old - p_avg
+ *   buf   = first_step ? g : fl(fl(buf * momentum) + g)
+ *   p_new = p_old - lr * buf          (fused multiply-add, as torch's
+ *                                      vectorised add_(buf, alpha=-lr))
+ * d_param is updated in place, d_mom too (momentum == 0 leaves it unused). */
+int fedagg_fedopt_sgd_f32(float* d_param, float* d_mom, const float* d_avg,
+                          int64_t N, float lr, float momentum,
+                          int32_t first_step, fedagg_stream_t stream);
+
+/* ---- Introspection ------------------------------------------------------ */
+const char* fedagg_last_error(void);
+int32_t fedagg_version(void);
+
+/* Tuning entry (not part of the product path): fp32 weighted sum with an
+ * explicit kernel variant; used by tools/tune_wsum.py to pick the shipped
+ * variant.  variant indexes the table printed by fedagg_variant_name(). */
+int fedagg_wsum_f32_variant(const float* const* d_src, const float* d_w,
+                            int32_t K, int64_t N, float* d_out,
+                            int32_t variant, fedagg_stream_t stream);
+const char* fedagg_variant_name(int32_t variant);
+int32_t fedagg_num_variants(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAGG_H_ */

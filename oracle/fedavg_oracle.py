@@ -1,0 +1,302 @@
+"""numpy restatement of FedML's torch_aggregator — TEST INFRASTRUCTURE ONLY.
+
+This module is the parity checker for the HIP path.  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import it; the
+product package fedml_amd/ never does.
+
+It restates, branch by branch, python/fedml/ml/aggregator/agg_operator.py:
+  FedMLAggOperator.agg            :10-30   (Σ n_i, tuple arity per optimizer)
+  torch_aggregator  FedAvg        :35-44
+                    FedProx       :45-54   (identical arithmetic)
+                    FedAvg_seq    :55-63   (unweighted, aliases client 0)
+                    FedOpt/FedNova :64-67  (`pass` -> UnboundLocalError)
+                    FedDyn        :68-77   (unweighted, aliases client 0)
+                    SCAFFOLD      :100-118 (overwrites with the last client)
+                    Mime          :119-133
+and the FedOpt server step of simulation/mpi/fedopt/FedOptAggregator.py:81-130.
+
+Inputs and outputs are CPU torch tensors (the reference's own currency); all
+arithmetic is numpy in the tensor's opmath type with one IEEE rounding per
+operation, exactly as torch's CPU kernels round (the conventions are stated in
+oracle/fedavg_oracle.c).  Pinned against golden vectors produced by the
+reference itself: tests/golden/ (see tests/test_oracle_golden.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from collections import OrderedDict
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_CLIB = os.path.join(HERE, "_build", "liboracle.so")
+
+_INT_DTYPES = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
+
+
+# --------------------------------------------------------------------------
+# bf16 / dtype helpers
+
+
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """c10::BFloat16 round-to-nearest-even; NaN -> 0x7FC0."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    u = x.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    r[np.isnan(x)] = 0x7FC0
+    return r
+
+
+def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
+    return (np.ascontiguousarray(b, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def _rbf(x: np.ndarray) -> np.ndarray:
+    return bf16_bits_to_f32(f32_to_bf16_bits(x))
+
+
+def _rf16(x: np.ndarray) -> np.ndarray:
+    return x.astype(np.float16).astype(np.float32)
+
+
+def to_np(t: torch.Tensor) -> np.ndarray:
+    t = t.detach().cpu().contiguous()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16).copy()
+    return t.numpy().copy()
+
+
+def from_np(a: np.ndarray, dtype: torch.dtype, shape) -> torch.Tensor:
+    if dtype == torch.bfloat16:
+        return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).reshape(shape)
+    return torch.from_numpy(np.ascontiguousarray(a)).reshape(shape).to(dtype)
+
+
+def weight_f32(n_i, total) -> np.float32:
+    """agg_operator.py:39 `w = local_sample_number / training_num` (Python
+    float64 division; ZeroDivisionError when Σn == 0), then torch rounds the
+    scalar to the float32 opmath type."""
+    return np.float32(n_i / total)
+
+
+# --------------------------------------------------------------------------
+# Per-tensor chains
+
+
+def wsum(tensors: Sequence[torch.Tensor], ws: Sequence[float]) -> torch.Tensor:
+    """One state-dict key: avg = p_0*w_0 ; avg += p_i*w_i (agg_operator.py:40-44).
+
+    ws are the Python-float weights n_i / Σn.  Output dtype follows torch's
+    promotion of `tensor * python_float`: float types keep their dtype,
+    integer/bool tensors become float32."""
+    dt = tensors[0].dtype
+    shape = tensors[0].shape
+    if dt == torch.float32 or dt in _INT_DTYPES:
+        w32 = [np.float32(w) for w in ws]
+        acc = to_np(tensors[0]).astype(np.float32) * w32[0]
+        for t, w in zip(tensors[1:], w32[1:]):
+            acc = acc + to_np(t).astype(np.float32) * w
+        return from_np(acc.astype(np.float32), torch.float32, shape)
+    if dt == torch.float64:
+        acc = to_np(tensors[0]) * np.float64(ws[0])
+        for t, w in zip(tensors[1:], ws[1:]):
+            acc = acc + to_np(t) * np.float64(w)
+        return from_np(acc, torch.float64, shape)
+    if dt in (torch.bfloat16, torch.float16):
+        r = _rbf if dt == torch.bfloat16 else _rf16
+        conv = bf16_bits_to_f32 if dt == torch.bfloat16 else (lambda a: a.astype(np.float32))
+        w32 = [np.float32(w) for w in ws]
+        acc = r(conv(to_np(tensors[0])) * w32[0])
+        for t, w in zip(tensors[1:], w32[1:]):
+            acc = r(acc + r(conv(to_np(t)) * w))
+        if dt == torch.bfloat16:
+            return from_np(f32_to_bf16_bits(acc), torch.bfloat16, shape)
+        return from_np(acc.astype(np.float16), torch.float16, shape)
+    raise TypeError(f"oracle: unsupported dtype {dt}")
+
+
+def seqsum(tensors: Sequence[torch.Tensor]) -> np.ndarray:
+    """avg = p_0 ; avg += p_i in the source dtype (agg_operator.py:58-63)."""
+    dt = tensors[0].dtype
+    if dt == torch.bfloat16:
+        acc = bf16_bits_to_f32(to_np(tensors[0]))
+        for t in tensors[1:]:
+            acc = _rbf(acc + bf16_bits_to_f32(to_np(t)))
+        return f32_to_bf16_bits(acc)
+    if dt == torch.float16:
+        acc = to_np(tensors[0]).astype(np.float32)
+        for t in tensors[1:]:
+            acc = _rf16(acc + to_np(t).astype(np.float32))
+        return acc.astype(np.float16)
+    acc = to_np(tensors[0])
+    for t in tensors[1:]:
+        with np.errstate(over="ignore"):
+            acc = acc + to_np(t)  # integer adds wrap like torch's
+    return acc.astype(to_np(tensors[0]).dtype)
+
+
+# --------------------------------------------------------------------------
+# FedMLAggOperator.agg restatement
+
+
+def agg(args, raw_grad_list):
+    """agg_operator.py:10-30 then torch_aggregator :33-134.  Mutates the
+    client-0 dicts exactly as the reference does."""
+    opt = args.federated_optimizer
+    training_num = 0
+    if opt in ("SCAFFOLD", "Mime"):
+        for item in raw_grad_list:
+            local_sample_num, _, _ = item
+            training_num += local_sample_num
+    else:
+        for item in raw_grad_list:
+            local_sample_num, _ = item
+            training_num += local_sample_num
+    return torch_aggregator(args, raw_grad_list, training_num)
+
+
+def torch_aggregator(args, raw_grad_list, training_num):
+    opt = args.federated_optimizer
+    K = len(raw_grad_list)
+    if opt in ("FedAvg", "FedProx"):
+        avg_params = raw_grad_list[0][1]
+        for k in list(avg_params.keys()):
+            ts = [raw_grad_list[i][1][k] for i in range(K)]
+            ws = [raw_grad_list[i][0] / training_num for i in range(K)]
+            avg_params[k] = wsum(ts, ws)
+        return avg_params
+    if opt in ("FedAvg_seq", "FedDyn"):
+        avg_params = raw_grad_list[0][1]
+        for k in list(avg_params.keys()):
+            ts = [raw_grad_list[i][1][k] for i in range(K)]
+            res = seqsum(ts)
+            t0 = ts[0]  # aliased: client 0's tensor is updated in place
+            if t0.dtype == torch.bfloat16:
+                t0.view(torch.int16).copy_(torch.from_numpy(res.view(np.int16)).reshape(t0.shape))
+            else:
+                t0.copy_(torch.from_numpy(np.ascontiguousarray(res)).reshape(t0.shape))
+            avg_params[k] = t0
+        return avg_params
+    if opt == "SCAFFOLD":
+        total_weights_delta, total_c_delta_para = raw_grad_list[0][1], raw_grad_list[0][2]
+        for k in list(total_weights_delta.keys()):
+            # The weighted sums of :106-115 are computed and then discarded by
+            # :116-117; only the last client's tensors survive.
+            _, weights_delta, c_delta_para = raw_grad_list[K - 1]
+            w_c = 1 / args.client_num_in_total
+            total_weights_delta[k] = weights_delta[k]
+            total_c_delta_para[k] = wsum([c_delta_para[k]], [w_c])
+        return (total_weights_delta, total_c_delta_para)
+    if opt == "Mime":
+        avg_params, avg_local_grad = raw_grad_list[0][1], raw_grad_list[0][2]
+        assert args.client_num_per_round == K
+        for k in list(avg_params.keys()):
+            ws = [raw_grad_list[i][0] / training_num for i in range(K)]
+            avg_params[k] = wsum([raw_grad_list[i][1][k] for i in range(K)], ws)
+            avg_local_grad[k] = wsum([raw_grad_list[i][2][k] for i in range(K)], ws)
+        return (avg_params, avg_local_grad)
+    # FedOpt, FedNova (`pass`) and unknown names leave avg_params unbound.
+    raise UnboundLocalError("local variable 'avg_params' referenced before assignment")
+
+
+# --------------------------------------------------------------------------
+# C oracle (exact fmaf for the FedOpt step; scalar cross-check of wsum)
+
+
+def build_c(force: bool = False) -> str:
+    src = os.path.join(HERE, "fedavg_oracle.c")
+    if force or not os.path.exists(_CLIB) or os.path.getmtime(src) > os.path.getmtime(_CLIB):
+        subprocess.run(["make", "-s", "-C", HERE, "_build/liboracle.so"], check=True)
+    return _CLIB
+
+
+_clib = None
+
+
+def clib() -> ctypes.CDLL:
+    global _clib
+    if _clib is None:
+        lib = ctypes.CDLL(build_c())
+        P, I, L, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+        for name, args in {
+            "oracle_wsum_f32": [P, P, I, L, P],
+            "oracle_wsum_bf16": [P, P, I, L, P],
+            "oracle_wsum_i64_f32": [P, P, I, L, P],
+            "oracle_wsum_f64": [P, P, I, L, P],
+            "oracle_sum_f32": [P, I, L, P],
+            "oracle_sum_bf16": [P, I, L, P],
+            "oracle_sum_i64": [P, I, L, P],
+            "oracle_fedopt_sgd_f32": [P, P, P, L, F, F, I],
+        }.items():
+            fn = getattr(lib, name)
+            fn.restype = None
+            fn.argtypes = args
+        _clib = lib
+    return _clib
+
+
+def c_wsum(arrays: List[np.ndarray], ws: Sequence[float]) -> np.ndarray:
+    """Weighted sum through the C oracle; arrays are 1-D numpy arrays of one
+    dtype (float32, uint16 = bf16 bits, int64, float64)."""
+    lib = clib()
+    K = len(arrays)
+    arrays = [np.ascontiguousarray(a) for a in arrays]
+    N = arrays[0].size
+    ptrs = (ctypes.c_void_p * K)(*[a.ctypes.data for a in arrays])
+    dt = arrays[0].dtype
+    if dt == np.float64:
+        w = np.asarray(ws, dtype=np.float64)
+        out = np.empty(N, np.float64)
+        lib.oracle_wsum_f64(ptrs, w.ctypes.data, K, N, out.ctypes.data)
+        return out
+    w = np.asarray([np.float32(x) for x in ws], dtype=np.float32)
+    if dt == np.float32:
+        out = np.empty(N, np.float32)
+        lib.oracle_wsum_f32(ptrs, w.ctypes.data, K, N, out.ctypes.data)
+    elif dt == np.uint16:
+        out = np.empty(N, np.uint16)
+        lib.oracle_wsum_bf16(ptrs, w.ctypes.data, K, N, out.ctypes.data)
+    elif dt == np.int64:
+        out = np.empty(N, np.float32)
+        lib.oracle_wsum_i64_f32(ptrs, w.ctypes.data, K, N, out.ctypes.data)
+    else:
+        raise TypeError(dt)
+    return out
+
+
+def fedopt_sgd(p_old: np.ndarray, avg: np.ndarray, buf: np.ndarray | None, lr: float, momentum: float,
+               first: bool) -> Tuple[np.ndarray, np.ndarray | None]:
+    """One server SGD step on one named parameter (FedOptAggregator.py:104-125)."""
+    p = np.ascontiguousarray(p_old, dtype=np.float32).copy()
+    a = np.ascontiguousarray(avg, dtype=np.float32)
+    b = np.zeros_like(p) if buf is None else np.ascontiguousarray(buf, dtype=np.float32).copy()
+    clib().oracle_fedopt_sgd_f32(p.ctypes.data, b.ctypes.data, a.ctypes.data, p.size, float(lr),
+                                 float(momentum), int(first))
+    return p, (b if momentum != 0 else None)
+
+
+def fedopt_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],
+                 raw_grad_list, lr: float, momentum: float,
+                 mom_state: Dict[str, np.ndarray]) -> "OrderedDict[str, torch.Tensor]":
+    """FedOptAggregator.aggregate (:81-116): FedAvg, then the SGD step on named
+    parameters, averaged values for buffers (int64 buffers truncated by
+    load_state_dict's copy_).  mom_state carries the momentum buffers across
+    rounds (the optimizer state_dict round trip of :105-111)."""
+    class _A:
+        federated_optimizer = "FedAvg"
+    avg = agg(_A(), raw_grad_list)
+    out = OrderedDict()
+    for k, t_old in global_sd.items():
+        if k in param_names:
+            first = k not in mom_state
+            p, b = fedopt_sgd(to_np(t_old).ravel(), to_np(avg[k]).ravel(), mom_state.get(k), lr, momentum, first)
+            if b is not None:
+                mom_state[k] = b
+            out[k] = torch.from_numpy(p).reshape(t_old.shape)
+        else:
+            out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)
+    return out

@@ -1,0 +1,193 @@
+"""Golden-vector case specs and their deterministic input builders.
+
+Shared by gen_golden.py (which runs the REFERENCE on these inputs, in the CPU
+container only) and by the tests (which rebuild the identical inputs from the
+spec, check the sha256 recorded in the fixture, and compare against the stored
+reference outputs).  Inputs are rebuilt from seeds, so fixtures stay small.
+"""
+from __future__ import annotations
+
+import copy
+import json
+from collections import OrderedDict
+from typing import Any, Dict, List
+
+import torch
+
+from fedml_amd import shapes
+from fedml_amd.synth import host_clients
+
+F32, BF16, F16, F64, I64 = "float32", "bfloat16", "float16", "float64", "int64"
+DTYPES = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16, F64: torch.float64, I64: torch.int64,
+          "int32": torch.int32}
+
+
+def _entries(spec_keys) -> List[shapes.Entry]:
+    return [(k, tuple(s), DTYPES[d]) for k, s, d in spec_keys]
+
+
+def _model_keys(name: str) -> List[List[Any]]:
+    return [[k, list(s), str(d).replace("torch.", "")] for k, s, d in shapes.MODELS[name]()]
+
+
+RESNET_MINI = [
+    ["conv1.weight", [8, 3, 3, 3], F32],
+    ["bn1.weight", [8], F32], ["bn1.bias", [8], F32], ["bn1.running_mean", [8], F32],
+    ["bn1.running_var", [8], F32], ["bn1.num_batches_tracked", [], I64],
+    ["layer1.0.conv1.weight", [16, 8, 3, 3], F32],
+    ["layer1.0.bn1.weight", [16], F32], ["layer1.0.bn1.bias", [16], F32],
+    ["layer1.0.bn1.running_mean", [16], F32], ["layer1.0.bn1.running_var", [16], F32],
+    ["layer1.0.bn1.num_batches_tracked", [], I64],
+    ["fc.weight", [10, 16], F32], ["fc.bias", [10], F32],
+]
+
+RAGGED_BF16 = [["a", [37], BF16], ["b", [1007], BF16], ["c", [3, 5, 7], BF16], ["d", [4096 + 3], BF16]]
+RAGGED_F32 = [["a", [1], F32], ["b", [5], F32], ["c", [1023], F32], ["d", [4099], F32],
+              ["e", [0], F32], ["scalar", [], F32], ["big", [70001], F32]]
+
+CASES: List[Dict[str, Any]] = []
+
+
+def _add(name, optimizer, K, keys, seed=0, **kw):
+    CASES.append(dict(name=name, optimizer=optimizer, K=K, keys=keys, seed=seed, **kw))
+
+
+# configs 1 and 2 at full size
+_add("cfg1_lr_mnist_k4", "FedAvg", 4, _model_keys("lr_mnist"), seed=1)
+_add("cfg2_cnn_web_k32", "FedAvg", 32, _model_keys("cnn_web"), seed=2)
+# ResNet-structured (with int64 num_batches_tracked), reduced size
+_add("resnet_mini_k5", "FedAvg", 5, RESNET_MINI, seed=3, round_idx=7)
+_add("resnet_mini_bigint_k3", "FedAvg", 3, RESNET_MINI, seed=4, int_range=[-(2 ** 40), 2 ** 40])
+# client-count edge cases (unroll remainders, K = 1)
+for _k in (1, 2, 3, 9, 17, 128):
+    _add(f"ragged_f32_k{_k}", "FedAvg", _k, RAGGED_F32, seed=10 + _k)
+# 16-bit and 64-bit floats
+for _k in (2, 3, 32):
+    _add(f"ragged_bf16_k{_k}", "FedAvg", _k, RAGGED_BF16, seed=30 + _k)
+_add("ragged_f16_k3", "FedAvg", 3, [[k, s, F16] for k, s, _ in RAGGED_BF16], seed=40)
+_add("ragged_f64_k3", "FedAvg", 3, [[k, s, F64] for k, s, _ in RAGGED_BF16], seed=41)
+_add("mixed_dtypes_k4", "FedAvg", 4, [["w", [513], F32], ["h", [257], BF16], ["d", [33], F64],
+                                      ["n", [3], I64], ["m", [65], F16]], seed=42)
+# sample counts: floats and very large integers
+_add("float_samples_k5", "FedAvg", 5, RAGGED_F32[:4], seed=50, sample_nums=[10.5, 0.25, 3.0, 1e-3, 77.7])
+_add("huge_samples_k4", "FedAvg", 4, RAGGED_F32[:4], seed=51, sample_nums=[10 ** 12, 3, 10 ** 15 + 1, 7])
+# IEEE specials (NaN, ±inf, denormals, -0.0, FLT_MAX)
+_add("specials_f32_k4", "FedAvg", 4, [["x", [64], F32]], seed=60, specials=True)
+_add("specials_bf16_k4", "FedAvg", 4, [["x", [64], BF16]], seed=61, specials=True)
+# other optimizers
+_add("fedprox_k3", "FedProx", 3, RESNET_MINI, seed=70)
+_add("fedavg_seq_k4", "FedAvg_seq", 4, [["w", [1001], F32], ["n", [2], I64], ["h", [300], BF16]], seed=71)
+_add("feddyn_k3", "FedDyn", 3, [["w", [513], F32], ["n", [], I64]], seed=72)
+_add("mime_k3", "Mime", 3, RAGGED_F32[:4], seed=73, client_num_per_round=3, triple=True)
+_add("scaffold_k3", "SCAFFOLD", 3, RAGGED_F32[:4], seed=74, client_num_in_total=10, triple=True)
+# errors the reference raises
+_add("err_zero_samples", "FedAvg", 2, RAGGED_F32[:2], seed=80, sample_nums=[0, 0], expect_error=True)
+_add("err_missing_key", "FedAvg", 2, RAGGED_F32[:2], seed=81, drop_key=[1, "b"], expect_error=True)
+_add("err_fedopt_plugin", "FedOpt", 2, RAGGED_F32[:2], seed=82, expect_error=True)
+_add("err_fednova_plugin", "FedNova", 2, RAGGED_F32[:2], seed=83, expect_error=True)
+
+# known answer from the reference's own test fixture
+# python/tests/security/defense/utils.py:51-64 create_fake_model_list(k):
+# client i = (i+1) * A with n_i = i + 10.
+FAKE_W = [[0.1, 0.2, 0.2, 0.1], [0.15, 0.12, 0.02, 0.2], [0.3, 0.01, 0.21, 0.11]]
+FAKE_B = [0.01, 0.19, 0.21]
+for _k in (1, 2, 3, 5, 10):
+    CASES.append(dict(name=f"kat_fake_model_list_k{_k}", optimizer="FedAvg", K=_k, fake_model_list=True))
+
+# FedOpt server step (simulation/mpi/fedopt/FedOptAggregator.py), 3 rounds
+FEDOPT_MODEL = [
+    ["0.weight", [5, 10], F32], ["0.bias", [5], F32],
+    ["1.weight", [5], F32], ["1.bias", [5], F32], ["1.running_mean", [5], F32], ["1.running_var", [5], F32],
+    ["1.num_batches_tracked", [], I64],
+    ["2.weight", [3, 5], F32], ["2.bias", [3], F32],
+]
+FEDOPT_PARAMS = ["0.weight", "0.bias", "1.weight", "1.bias", "2.weight", "2.bias"]
+FEDOPT_CASES = [
+    dict(name="fedopt_sgd_m09_lr1", K=4, rounds=3, lr=1.0, momentum=0.9, seed=90),
+    dict(name="fedopt_sgd_m09_lr1e-3", K=4, rounds=3, lr=0.001, momentum=0.9, seed=91),
+    dict(name="fedopt_sgd_m0_lr05", K=3, rounds=2, lr=0.5, momentum=0.0, seed=92),
+]
+
+
+def fake_model_list(k: int):
+    """python/tests/security/defense/utils.py:51-64 (data only)."""
+    A = torch.FloatTensor(FAKE_W)
+    b = torch.FloatTensor(FAKE_B)
+    out = []
+    for i in range(k):
+        d = OrderedDict()
+        d["linear.weight"] = (i + 1) * A
+        d["linear.bias"] = (i + 1) * b
+        out.append((i + 10, d))
+    return out
+
+
+def _specials(raw):
+    for i, item in enumerate(raw):
+        for t in item[1].values():
+            big = torch.finfo(t.dtype).max
+            vals = [float("nan"), float("inf"), float("-inf"), 1e-40, -1e-42, -0.0, big, -big, 1e-45]
+            flat = t.view(-1)
+            for j, v in enumerate(vals):
+                pos = (j * 7 + i * 3) % flat.numel()
+                flat[pos] = v
+            if i == 0:
+                flat[-1] = float("inf")
+            if i == 1:
+                flat[-1] = float("-inf")  # inf + -inf -> NaN in the sum
+    return raw
+
+
+def build_inputs(spec: Dict[str, Any]):
+    """The reference's raw_grad_list for this case (fresh objects every call)."""
+    if spec.get("fake_model_list"):
+        return fake_model_list(spec["K"])
+    entries = _entries(spec["keys"])
+    raw = host_clients(entries, spec["K"], spec["seed"], round_idx=spec.get("round_idx", 0),
+                       sample_nums=spec.get("sample_nums"), int_range=spec.get("int_range"))
+    if spec.get("specials"):
+        raw = _specials(raw)
+    if spec.get("triple"):
+        second = host_clients(entries, spec["K"], spec["seed"] + 1000)
+        raw = [(n, d, second[i][1]) for i, (n, d) in enumerate(raw)]
+    if spec.get("drop_key"):
+        idx, key = spec["drop_key"]
+        del raw[idx][1][key]
+    return raw
+
+
+class Args:
+    def __init__(self, spec):
+        self.federated_optimizer = spec["optimizer"]
+        if "client_num_per_round" in spec:
+            self.client_num_per_round = spec["client_num_per_round"]
+        if "client_num_in_total" in spec:
+            self.client_num_in_total = spec["client_num_in_total"]
+
+
+def fedopt_global_init(spec):
+    raw = host_clients(_entries(FEDOPT_MODEL), 1, spec["seed"])
+    return raw[0][1]
+
+
+def fedopt_round_inputs(spec, global_sd, r):
+    """Clients of round r: global + small noise (fresh objects)."""
+    noise = host_clients(_entries(FEDOPT_MODEL), spec["K"], spec["seed"] * 100 + r, round_idx=r)
+    out = []
+    for n, d in noise:
+        nd = OrderedDict()
+        for k, t in d.items():
+            if t.dtype == torch.int64:
+                nd[k] = t.clone()
+            else:
+                nd[k] = (global_sd[k] + 0.2 * t).contiguous()
+        out.append((n, nd))
+    return out
+
+
+def spec_json(spec) -> str:
+    return json.dumps(spec, sort_keys=True)
+
+
+def clone_raw(raw):
+    return copy.deepcopy(raw)

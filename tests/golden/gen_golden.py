@@ -1,0 +1,157 @@
+"""Generate golden vectors by running the REFERENCE aggregator (CPU container).
+
+    python tests/golden/gen_golden.py
+
+Imports FedML's own code from /root/reference/python (read-only) through
+namespace-package stubs, so only the modules on the aggregation path load:
+
+  fedml.ml.aggregator.agg_operator.FedMLAggOperator     agg_operator.py:8-234
+  fedml.simulation.mpi.fedopt.FedOptAggregator          FedOptAggregator.py:14-130
+  (+ its optrepo; `wandb` is absent and replaced by an empty module)
+
+For each case of tests/golden/cases.py it records the sha256 of the inputs,
+the reference's outputs (bit patterns), the exception type it raises, and the
+aliasing it exhibits.  Only data is written (tests/golden/fixtures/*.npz, no
+pickles); no reference source is copied.  The GPU box never runs this file.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+import cases  # noqa: E402
+from fedml_amd.synth import fingerprint  # noqa: E402
+
+REF = "/root/reference/python/fedml"
+OUT_DIR = os.path.join(HERE, "fixtures")
+
+
+def import_reference():
+    for name, path in [
+        ("fedml", REF), ("fedml.core", f"{REF}/core"), ("fedml.simulation", f"{REF}/simulation"),
+        ("fedml.simulation.mpi", f"{REF}/simulation/mpi"),
+        ("fedml.simulation.mpi.fedopt", f"{REF}/simulation/mpi/fedopt"),
+    ]:
+        m = types.ModuleType(name)
+        m.__path__ = [path]
+        sys.modules[name] = m
+    sys.modules.setdefault("wandb", types.ModuleType("wandb"))
+    from fedml.ml.aggregator.agg_operator import FedMLAggOperator
+    from fedml.simulation.mpi.fedopt.FedOptAggregator import FedOptAggregator
+    return FedMLAggOperator, FedOptAggregator
+
+
+def tensor_bytes(t: torch.Tensor) -> np.ndarray:
+    t = t.detach().cpu().contiguous()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16).copy()
+    if t.dtype == torch.bool:
+        return t.numpy().astype(np.uint8)
+    return t.numpy().copy()
+
+
+def save(name: str, meta: dict, arrays: dict) -> None:
+    os.makedirs(OUT_DIR, exist_ok=True)
+    payload = {f"a{i}": v for i, v in enumerate(arrays.values())}
+    meta["array_names"] = list(arrays.keys())
+    np.savez_compressed(os.path.join(OUT_DIR, f"{name}.npz"), meta=np.array(json.dumps(meta)), **payload)
+
+
+def run_agg_case(FedMLAggOperator, spec):
+    raw = cases.build_inputs(spec)
+    sha = fingerprint(raw)
+    client0_before = OrderedDict((k, t.clone()) for k, t in raw[0][1].items())
+    client0_objs = dict(raw[0][1])
+    meta = {"spec": spec, "in_sha256": sha, "error": None}
+    arrays = {}
+    try:
+        res = FedMLAggOperator.agg(cases.Args(spec), raw)
+    except Exception as e:  # the reference's own error behaviour is part of the contract
+        meta["error"] = type(e).__name__
+        save(spec["name"], meta, arrays)
+        return
+    groups = list(res) if isinstance(res, tuple) else [res]
+    meta["tuple"] = isinstance(res, tuple)
+    meta["result_is_client0_dict"] = groups[0] is raw[0][1]
+    meta["outputs"] = []
+    for g, d in enumerate(groups):
+        for k, t in d.items():
+            arrays[f"o{g}:{k}"] = tensor_bytes(t)
+            meta["outputs"].append({"group": g, "key": k, "dtype": str(t.dtype).replace("torch.", ""),
+                                    "shape": list(t.shape),
+                                    "is_client0_tensor": (k in client0_objs and t is client0_objs[k])})
+    mutated = [k for k, t in client0_objs.items()
+               if not torch.equal(t.view(torch.int16) if t.dtype == torch.bfloat16 else t,
+                                  client0_before[k].view(torch.int16) if t.dtype == torch.bfloat16
+                                  else client0_before[k])
+               and not (t.is_floating_point() and torch.isnan(t).any())]
+    meta["client0_tensors_mutated"] = mutated
+    save(spec["name"], meta, arrays)
+
+
+def run_fedopt_case(FedOptAggregator, spec):
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(10, 5), torch.nn.BatchNorm1d(5), torch.nn.Linear(5, 3))
+    model.load_state_dict(cases.fedopt_global_init(spec))
+
+    class ServerAgg:
+        def __init__(self, m):
+            self.model = m
+
+        def get_model_params(self):
+            return self.model.state_dict()
+
+        def set_model_params(self, sd):
+            self.model.load_state_dict(sd)
+
+    class A:
+        server_optimizer = "sgd"
+        server_lr = spec["lr"]
+        server_momentum = spec["momentum"]
+
+    agg = object.__new__(FedOptAggregator)
+    agg.aggregator = ServerAgg(model)
+    agg.args = A()
+    agg.worker_num = spec["K"]
+    agg.model_dict, agg.sample_num_dict, agg.flag_client_model_uploaded_dict = {}, {}, {}
+    agg.opt = agg._instantiate_opt()
+    meta = {"spec": spec, "rounds": [], "param_names": cases.FEDOPT_PARAMS}
+    arrays = {}
+    for k, t in cases.fedopt_global_init(spec).items():
+        arrays[f"init:{k}"] = tensor_bytes(t)
+    gsd = OrderedDict((k, t.clone()) for k, t in model.state_dict().items())
+    for r in range(spec["rounds"]):
+        raw = cases.fedopt_round_inputs(spec, gsd, r)
+        meta["rounds"].append({"in_sha256": fingerprint(raw)})
+        for i, (n, d) in enumerate(raw):
+            agg.add_local_trained_result(i, d, n)
+        out = agg.aggregate()
+        gsd = OrderedDict((k, t.detach().clone()) for k, t in out.items())
+        for k, t in gsd.items():
+            arrays[f"r{r}:{k}"] = tensor_bytes(t)
+    save(spec["name"], meta, arrays)
+
+
+def main():
+    FedMLAggOperator, FedOptAggregator = import_reference()
+    for spec in cases.CASES:
+        run_agg_case(FedMLAggOperator, spec)
+        print("wrote", spec["name"])
+    for spec in cases.FEDOPT_CASES:
+        run_fedopt_case(FedOptAggregator, spec)
+        print("wrote", spec["name"])
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,85 @@
+"""Loading golden fixtures and comparing results bit for bit."""
+from __future__ import annotations
+
+import glob
+import json
+import os
+from collections import OrderedDict
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+
+FIX_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fixtures")
+
+_NP = {"float32": np.float32, "float64": np.float64, "float16": np.float16, "int64": np.int64,
+       "int32": np.int32, "bfloat16": np.uint16}
+_TORCH = {"float32": torch.float32, "float64": torch.float64, "float16": torch.float16, "int64": torch.int64,
+          "int32": torch.int32, "bfloat16": torch.bfloat16}
+
+
+def fixture_names(prefix: str = "") -> List[str]:
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(FIX_DIR, f"{prefix}*.npz")))
+
+
+def load(name: str) -> Tuple[dict, Dict[str, np.ndarray]]:
+    with np.load(os.path.join(FIX_DIR, f"{name}.npz"), allow_pickle=False) as z:
+        meta = json.loads(str(z["meta"]))
+        arrays = {n: z[f"a{i}"] for i, n in enumerate(meta["array_names"])}
+    return meta, arrays
+
+
+def to_tensor(a: np.ndarray, dtype: str, shape) -> torch.Tensor:
+    if dtype == "bfloat16":
+        return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).reshape(shape)
+    return torch.from_numpy(a.copy()).reshape(shape)
+
+
+def expected_groups(meta, arrays) -> List["OrderedDict[str, torch.Tensor]"]:
+    groups: List[OrderedDict] = []
+    for o in meta["outputs"]:
+        while len(groups) <= o["group"]:
+            groups.append(OrderedDict())
+        groups[o["group"]][o["key"]] = to_tensor(arrays[f"o{o['group']}:{o['key']}"], o["dtype"], o["shape"])
+    return groups
+
+
+def bits(t: torch.Tensor) -> np.ndarray:
+    t = t.detach().cpu().contiguous()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16)
+    if t.dtype == torch.float16:
+        return t.view(torch.int16).numpy().view(np.uint16)
+    if t.dtype == torch.float32:
+        return t.numpy().view(np.uint32)
+    if t.dtype == torch.float64:
+        return t.numpy().view(np.uint64)
+    return t.numpy()
+
+
+def assert_same(actual: torch.Tensor, expected: torch.Tensor, what: str = "") -> None:
+    """Bit-identical, except that any NaN matches any NaN (payloads are not part
+    of torch's contract either)."""
+    assert actual.dtype == expected.dtype, f"{what}: dtype {actual.dtype} != {expected.dtype}"
+    assert tuple(actual.shape) == tuple(expected.shape), f"{what}: shape {actual.shape} != {expected.shape}"
+    a, e = bits(actual).ravel(), bits(expected).ravel()
+    if actual.is_floating_point():
+        an = torch.isnan(actual.detach().cpu().float()).numpy().ravel()
+        en = torch.isnan(expected.float()).numpy().ravel()
+        assert np.array_equal(an, en), f"{what}: NaN positions differ"
+        a, e = a[~an], e[~en]
+    bad = np.nonzero(a != e)[0]
+    assert bad.size == 0, (f"{what}: {bad.size} of {a.size} elements differ; first at {bad[0]}: "
+                           f"got {actual.detach().cpu().reshape(-1)[bad[0]].item()!r} "
+                           f"want {expected.reshape(-1)[bad[0]].item()!r}")
+
+
+def assert_groups(actual, meta, arrays, what="") -> None:
+    exp = expected_groups(meta, arrays)
+    got = list(actual) if isinstance(actual, tuple) else [actual]
+    assert bool(meta.get("tuple")) == isinstance(actual, tuple), f"{what}: tuple-ness differs"
+    assert len(got) == len(exp)
+    for g, (gd, ed) in enumerate(zip(got, exp)):
+        assert list(gd.keys()) == list(ed.keys()), f"{what}: key order differs"
+        for k in ed:
+            assert_same(gd[k], ed[k], f"{what}[{g}][{k}]")

@@ -1,0 +1,105 @@
+"""A/B the fp32 weighted-sum kernel variants on the headline shape (GPU only).
+
+Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24):
+every variant runs once per round, R rounds, median/min reported.  Each
+variant's output is checked bit-for-bit against a torch-on-GPU restatement of
+the reference chain (separate mul and add kernels: two roundings, like the
+reference's CPU loop).  Also times a plain device copy as the achievable-HBM
+reference point.
+
+    python tools/tune_wsum.py --K 128 --N 25610152 --rounds 10
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from fedml_amd import _native as nat  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--N", type=int, default=25_610_152)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--no-check", action="store_true")
+    a = ap.parse_args()
+    K, N = a.K, a.N
+    dev = torch.device("cuda:0")
+    lib = nat.lib()
+    g = torch.Generator(device=dev).manual_seed(0)
+    row = (N + 63) // 64 * 64
+    bucket = torch.empty((K, row), dtype=torch.float32, device=dev)
+    for i in range(K):
+        bucket[i].normal_(0.0, 0.05, generator=g)
+    n = torch.randint(100, 1001, (K,), generator=torch.Generator().manual_seed(1)).tolist()
+    tot = sum(n)
+    w = torch.tensor([float(x) / float(tot) for x in n], dtype=torch.float32, device=dev)
+    ptrs = torch.tensor([bucket[i].data_ptr() for i in range(K)], dtype=torch.int64, device=dev)
+    out = torch.empty(N, dtype=torch.float32, device=dev)
+    st = nat.stream_handle()
+
+    ref = None
+    if not a.no_check:
+        wl = w.cpu().tolist()
+        ref = bucket[0, :N] * wl[0]
+        for i in range(1, K):
+            ref += bucket[i, :N] * wl[i]
+
+    nv = lib.fedagg_num_variants()
+    names = [lib.fedagg_variant_name(v).decode() for v in range(nv)]
+    times = {nm: [] for nm in names}
+    times["copy"] = []
+    src_copy = bucket.view(-1)[: 8 * row].clone()
+    dst_copy = torch.empty_like(src_copy)
+    bytes_alg = (K + 1) * N * 4
+
+    def run(v: int) -> None:
+        nat.check(lib.fedagg_wsum_f32_variant(ptrs.data_ptr(), w.data_ptr(), K, N, out.data_ptr(), v, st),
+                  names[v])
+
+    for v in range(nv):  # warm-up + correctness
+        run(v)
+        torch.cuda.synchronize()
+        if ref is not None:
+            ok = torch.equal(out.view(torch.int32), ref.view(torch.int32))
+            print(f"{names[v]}: bitwise={'OK' if ok else 'MISMATCH'}", flush=True)
+            if not ok:
+                d = (out - ref).abs().max().item()
+                print(f"   max abs diff {d}", flush=True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    for r in range(a.rounds):
+        for v in range(nv):
+            ev0.record()
+            run(v)
+            ev1.record()
+            ev1.synchronize()
+            times[names[v]].append(ev0.elapsed_time(ev1))
+        ev0.record()
+        dst_copy.copy_(src_copy)
+        ev1.record()
+        ev1.synchronize()
+        times["copy"].append(ev0.elapsed_time(ev1))
+    res = {}
+    for nm, ts in times.items():
+        med = statistics.median(ts)
+        b = bytes_alg if nm != "copy" else 2 * src_copy.numel() * 4
+        res[nm] = {"median_ms": round(med, 4), "min_ms": round(min(ts), 4),
+                   "GBps_median": round(b / med / 1e6, 1), "frac_8TBps": round(b / med / 1e6 / 8000, 4)}
+        print(f"{nm:10s} median {med:8.4f} ms  min {min(ts):8.4f} ms  {b / med / 1e6:8.1f} GB/s  "
+              f"({b / med / 1e6 / 8000:.3f} of 8 TB/s)", flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/tune_K{K}_N{N}.json", "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
