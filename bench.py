@@ -1,0 +1,265 @@
+#!/usr/bin/env python
+"""Headline benchmark: device-resident FedAvg aggregation on MI355X.
+
+One step = one server aggregation round over client updates already resident
+in HBM: host computes the weights w_i = n_i/Σn, uploads them, and the
+weighted-sum kernels reduce every client row (one launch per dtype group;
+with --gpus > 1 also the RCCL reduce-scatter of the client-axis mode).
+
+Default workload = BASELINE.json config 3: 128 clients x ResNet-50 state dict
+(25,610,152 fp32 + 53 int64 elements per client), synthetic data generated
+in HBM.  With --gpus N each rank holds its own 128 clients (weak scaling).
+
+    python bench.py                       # 1 GPU, default steps
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8
+
+Prints ONE JSON line on rank 0 (contract in the task statement); the
+cpu_baseline leg times the reference's own CPU loop (oracle/cpu_baseline.py)
+on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from fedml_amd import shapes  # noqa: E402
+from fedml_amd.bucket import ClientBucket  # noqa: E402
+from fedml_amd.sharded import ClientAxisAggregator, ParamAxisAggregator  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    "cfg2": dict(model="cnn_web", K=32, desc="FedAvg 32 clients x LeNet CNN_WEB (62,006 params) fp32"),
+    "cfg3": dict(model="resnet50", K=128,
+                 desc="FedAvg 128 clients x ResNet-50 state dict (25,610,152 fp32 + 53 int64) fp32"),
+    "cfg4": dict(model="vit_b16", K=128, desc="FedAvg 128 clients/GPU x ViT-B/16 (86,567,656) bf16"),
+    "cfg5": dict(model="llama2_7b_lora", K=64, desc="FedAvg 64 clients x Llama-2-7B LoRA r=8 q/v fp32"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="client", choices=["client", "param"],
+                    help="multi-GPU partitioning (ignored at 1 GPU)")
+    ap.add_argument("--chunks", type=int, default=8, help="client mode: reduce-scatter pipeline depth")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-elems", type=int, default=2_600_000)
+    return ap.parse_args()
+
+
+def fill_rows(rows: torch.Tensor, length: int, seed: int, round_idx: int = 0) -> None:
+    """Synthetic updates in HBM: base ~ N(0, 0.05²), client_i = base + 0.01·ε_i
+    (SURVEY.md §8(d)); int64 rows get round_idx + i."""
+    K = rows.shape[0]
+    if rows.dtype == torch.int64:
+        for i in range(K):
+            rows[i].fill_(round_idx + i)
+        return
+    g = torch.Generator(device=rows.device).manual_seed(seed)
+    base = torch.randn(length, generator=g, device=rows.device) * 0.05
+    eps = torch.empty(length, device=rows.device)
+    for i in range(K):
+        eps.normal_(0.0, 1.0, generator=g)
+        rows[i, :length].copy_(base + 0.01 * eps)
+        rows[i, length:].zero_()
+    del base, eps
+
+
+def cpu_baseline(entries, K: int, sample_elems: int) -> dict:
+    """The reference's own CPU loop (torch eager, oracle/cpu_baseline.py) on the
+    first keys of the same state dict up to ~sample_elems elements per client,
+    all K clients; reported in client-params/s."""
+    from oracle import cpu_baseline as cb
+    from fedml_amd.synth import host_clients
+
+    sub, tot = [], 0
+    for e in entries:
+        n = 1
+        for s in e[1]:
+            n *= s
+        if tot + n > sample_elems and sub:
+            break
+        sub.append(e)
+        tot += n
+    raw = host_clients(sub, K, seed=123)
+    r = cb.time_fedavg(raw, reps=3)
+    return {"value": K * tot / r["median_s"], "unit": "client-params/s", "cores": r["threads"], "kind": "port",
+            "sample": f"{K} clients x first {len(sub)} of {len(entries)} state-dict keys ({tot:,} elements/client), "
+                      f"torch-eager restatement of agg_operator.py:35-44, median of {r['reps']} after 1 warm-up, "
+                      f"{r['median_s'] * 1e3:.1f} ms/aggregation"}
+
+
+def load_traffic(config: str, mode: str, world: int):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return d.get(f"{config}:{mode if world > 1 else 'single'}", {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[a.config]
+    entries = shapes.MODELS[cfg["model"]]()
+    K = cfg["K"]
+    mode = a.mode if world > 1 else "single"
+
+    bucket = ClientBucket(entries, K, dev)
+    for gi, (dt, g) in enumerate(bucket.groups.items()):
+        fill_rows(g.rows, g.length, seed=1000 * rank + gi, round_idx=3)
+    from fedml_amd.synth import sample_nums
+    ns_all = sample_nums(K * world, seed=1)
+    ns_local = ns_all[rank * K:(rank + 1) * K]
+    torch.cuda.synchronize()
+
+    groups = list(bucket.groups.items())
+    dom_dt = max(groups, key=lambda kv: kv[1].length * kv[1].rows.element_size())[0]
+    n_elems = bucket.num_elements()
+
+    # per-step work -------------------------------------------------------------
+    if mode == "single":
+        outs = bucket.new_outputs()
+        w = bucket.weights(ns_local)
+
+        def step(ev=None):
+            bucket.reduce_into(outs, w, events={dom_dt: ev} if ev is not None else None)
+
+        n_launch = 1
+        dom_bytes = K * bucket.groups[dom_dt].length * bucket.groups[dom_dt].rows.element_size() + \
+            bucket.groups[dom_dt].length * torch.empty((), dtype=bucket.groups[dom_dt].out_dtype).element_size()
+    elif mode == "client":
+        total = sum(ns_all)
+        w = [n / total for n in ns_all[rank * K:(rank + 1) * K]]
+        aggs = {dt: ClientAxisAggregator(g.rows, g.length, chunks=a.chunks if dt == dom_dt else 1)
+                for dt, g in groups}
+
+        def step(ev=None):
+            for dt, agg in aggs.items():
+                agg.aggregate(w, events=ev if dt == dom_dt else None)
+
+        n_launch = len(aggs[dom_dt].bounds)
+        gd = bucket.groups[dom_dt]
+        dom_bytes = K * gd.length * gd.rows.element_size() + gd.length * 4  # rows in, fp32 partial out
+    else:  # param axis: this rank's rows ARE its column shard of every client
+        w = bucket.weights(ns_local)
+        aggs = {dt: ParamAxisAggregator(g.rows, g.length) for dt, g in groups}
+
+        def step(ev=None):
+            for dt, agg in aggs.items():
+                agg.aggregate(w, events=ev if dt == dom_dt else None)
+
+        n_launch = 1
+        gd = bucket.groups[dom_dt]
+        dom_bytes = K * gd.length * gd.rows.element_size() + \
+            gd.length * torch.empty((), dtype=gd.out_dtype).element_size()
+
+    def new_events():
+        return [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+                for _ in range(n_launch)]
+
+    for _ in range(a.warmup):
+        step()
+    evs = [new_events() for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        ev = evs[s]
+        if mode == "single":
+            step(ev[0])
+        else:
+            step(ev)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(e0.elapsed_time(e1) for ev in evs for e0, e1 in ev) / a.steps  # per step
+    achieved = dom_bytes / (kern_ms / 1e3) / 1e9
+    if world > 1:
+        t = torch.tensor([achieved], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)  # slowest rank's kernel
+        achieved = float(t.item())
+
+    ms_per_step = elapsed / a.steps * 1e3
+    value = world * K * n_elems / (elapsed / a.steps)
+    traffic = load_traffic(a.config, mode, world)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "client-params/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if dom_dt == torch.bfloat16 else "f32",
+        "data": "synthetic (base~N(0,0.05^2), client=base+0.01*eps, generated in HBM)",
+        "config": {
+            "workload": cfg["desc"],
+            "clients_per_gpu": K,
+            "clients_total": K * world,
+            "elements_per_client": n_elems,
+            "layout": "ClientBucket rows [K, L] per dtype, 256-B aligned rows",
+            "parallelism": {"single": "1 GPU", "client": f"client-axis x{world}, RCCL reduce-scatter, "
+                                                         f"{a.chunks}-chunk pipeline",
+                            "param": f"parameter-axis x{world}, no collective"}[mode],
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "kernel": f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step",
+            "alg_bytes_per_step": dom_bytes,
+            "kernel_ms_per_step": round(kern_ms, 4),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(entries, K, a.cpu_sample_elems)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

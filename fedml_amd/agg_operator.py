@@ -1,0 +1,317 @@
+"""Drop-in replacement of FedML's aggregation operator, computed on MI355X.
+
+Mirrors python/fedml/ml/aggregator/agg_operator.py (same names, argument
+meaning, return values, aliasing and exceptions):
+
+  FedMLAggOperator.agg(args, raw_grad_list)            agg_operator.py:8-30
+  model_aggregator(args, raw_grad_list, training_num)   :223-234
+  torch_aggregator(args, raw_grad_list, training_num)   :33-134
+
+Every reduction runs in libfedagg.so (include/fedagg.h); there is no CPU
+arithmetic and no CPU fallback.  Where the reference's tensors already live on
+the GPU (server `using_gpu`, ml_engine_adapter.py:234-254) the kernels read
+them in place through pointer tables — all fp32 keys in ONE launch; host
+tensors are packed per client into pinned staging rows, copied to HBM, reduced
+with one launch per dtype, and copied back, so the result lives where the
+inputs did, as in the reference.
+
+Options read from ``args`` (all optional, duck-typed like FedML's Arguments):
+  fedagg_device             torch device for host inputs (default: current GPU)
+  fedagg_low_precision_acc  "reference" (default: bf16/f16 rounded after every
+                            op, bit-exact with torch's CPU chain) or "fp32"
+                            (accumulate in fp32, round once)
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+
+from . import _native as nat
+from . import kernels as kn
+
+# torch promotes `int_tensor * python_float` to the default dtype float32.
+_INT_TO_I64 = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
+_FLOAT = (torch.float32, torch.bfloat16, torch.float16, torch.float64)
+
+
+class FedMLAggOperator:
+    """Same interface as fedml.ml.aggregator.agg_operator.FedMLAggOperator."""
+
+    @staticmethod
+    def agg(args, raw_grad_list: List[Tuple[float, "OrderedDict"]]) -> "OrderedDict":
+        # agg_operator.py:11-28 — Σ n_i with the same tuple unpacking (and so the
+        # same ValueError on a wrong arity).
+        training_num = 0
+        if args.federated_optimizer in ("SCAFFOLD", "Mime"):
+            for i in range(len(raw_grad_list)):
+                local_sample_num, _, _ = raw_grad_list[i]
+                training_num += local_sample_num
+        else:
+            for i in range(len(raw_grad_list)):
+                local_sample_num, local_model_params = raw_grad_list[i]
+                training_num += local_sample_num
+        return model_aggregator(args, raw_grad_list, training_num)
+
+
+def model_aggregator(args, raw_grad_list, training_num):
+    """agg_operator.py:223-234.  Only the torch engine is on the MI355X path."""
+    engine = getattr(args, "ml_engine", None)
+    if engine in ("tf", "jax", "mxnet"):
+        raise NotImplementedError(f"fedml_amd aggregates torch state dicts; ml_engine={engine!r} is not supported")
+    return torch_aggregator(args, raw_grad_list, training_num)
+
+
+def _acc_mode(args) -> int:
+    mode = getattr(args, "fedagg_low_precision_acc", "reference")
+    if mode == "reference":
+        return kn.ACC_REFERENCE
+    if mode == "fp32":
+        return kn.ACC_FP32
+    raise ValueError(f"fedagg_low_precision_acc must be 'reference' or 'fp32', got {mode!r}")
+
+
+def _host_device(args) -> torch.device:
+    dev = getattr(args, "fedagg_device", None)
+    if dev is not None:
+        return torch.device(dev)
+    if not torch.cuda.is_available():
+        raise nat.FedAggNativeError("fedml_amd needs a GPU: host inputs are reduced on the device")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _gather(dicts: Sequence["OrderedDict"], keys: Sequence[str]) -> Dict[str, List[torch.Tensor]]:
+    """Per-key client tensors; KeyError for a missing key, as the reference's
+    `local_model_params[k]` raises."""
+    out = {}
+    for k in keys:
+        ts = [d[k] for d in dicts]
+        t0 = ts[0]
+        for t in ts[1:]:
+            if t.shape != t0.shape:
+                raise RuntimeError(f"key {k!r}: client tensor shapes differ ({tuple(t.shape)} vs {tuple(t0.shape)})")
+            if t.dtype != t0.dtype:
+                raise TypeError(f"key {k!r}: client tensor dtypes differ ({t.dtype} vs {t0.dtype})")
+            if t.device != t0.device:
+                raise RuntimeError(f"key {k!r}: client tensors on different devices ({t.device} vs {t0.device})")
+        if t0.dtype not in _FLOAT and t0.dtype not in _INT_TO_I64:
+            raise TypeError(f"key {k!r}: unsupported dtype {t0.dtype}")
+        out[k] = ts
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Reduction engine
+
+
+class _Staged:
+    """Host inputs of one dtype group packed into device rows [K, L]."""
+
+    def __init__(self, keys, numels, dtype, dev_rows):
+        self.keys, self.numels, self.dtype, self.rows = keys, numels, dtype, dev_rows
+        self.offsets = []
+        o = 0
+        for n in numels:
+            self.offsets.append(o)
+            o += n
+        self.length = o
+
+
+def _pad(n: int, a: int = 64) -> int:
+    return (n + a - 1) // a * a
+
+
+def _stage_host(per_key: Dict[str, List[torch.Tensor]], keys: Sequence[str], dtype: torch.dtype,
+                device: torch.device) -> _Staged:
+    """Pack each client's tensors of this dtype into a pinned row (one host
+    memcpy) and send it to HBM on a copy stream, double-buffered so packing
+    client i+1 overlaps the PCIe transfer of client i."""
+    K = len(per_key[keys[0]])
+    numels = [per_key[k][0].numel() for k in keys]
+    L = sum(numels)
+    rows = torch.empty((K, _pad(max(L, 1))), dtype=dtype, device=device)
+    cur = torch.cuda.current_stream(device)
+    copy_stream = torch.cuda.Stream(device)
+    copy_stream.wait_stream(cur)
+    pinned = [torch.empty(max(L, 1), dtype=dtype).pin_memory() for _ in range(2)]
+    done = [None, None]
+    with torch.cuda.stream(copy_stream):
+        for i in range(K):
+            b = i & 1
+            if done[b] is not None:
+                done[b].synchronize()
+            parts = [per_key[k][i].reshape(-1) for k in keys]
+            if parts:
+                parts = [p if p.dtype == dtype else p.to(dtype) for p in parts]
+                torch.cat(parts, out=pinned[b][:L])
+            rows[i, :L].copy_(pinned[b][:L], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(copy_stream)
+            done[b] = ev
+    cur.wait_stream(copy_stream)  # the reduction (on cur) runs after the last row landed
+    return _Staged(list(keys), numels, dtype, rows)
+
+
+def _to_host(flat: torch.Tensor, staged: _Staged, shapes: Dict[str, torch.Size]) -> Dict[str, torch.Tensor]:
+    """One D2H of the group's result, then independent per-key host tensors
+    (each its own storage, as the reference's per-key results are; a view into
+    one buffer would pickle the whole buffer per key on broadcast)."""
+    host = torch.empty(flat.numel(), dtype=flat.dtype).pin_memory()
+    host.copy_(flat)  # synchronous: the result is needed on the host now
+    out = {}
+    for k, off, n in zip(staged.keys, staged.offsets, staged.numels):
+        out[k] = host[off:off + n].clone().reshape(shapes[k])
+    return out
+
+
+def _row_ptrs(rows: torch.Tensor) -> List[int]:
+    return [rows[i].data_ptr() for i in range(rows.shape[0])]
+
+
+def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights: Sequence[float], args
+                    ) -> "OrderedDict[str, torch.Tensor]":
+    """avg[k] = Σ_i fl(p_i[k] · w_i) in client order for every key (the FedAvg
+    inner loops, agg_operator.py:36-44), on the GPU.  Returns results on the
+    inputs' device."""
+    per_key = _gather(dicts, keys)
+    acc_mode = _acc_mode(args)
+    K = len(dicts)
+    results: Dict[str, torch.Tensor] = {}
+    host_keys = [k for k in keys if not per_key[k][0].is_cuda]
+    dev_keys = [k for k in keys if per_key[k][0].is_cuda]
+
+    # ---- host-resident inputs: stage per dtype group, one launch per group --
+    if host_keys:
+        device = _host_device(args)
+        with torch.cuda.device(device):
+            groups: Dict[torch.dtype, List[str]] = OrderedDict()
+            for k in host_keys:
+                dt = per_key[k][0].dtype
+                groups.setdefault(torch.int64 if dt in _INT_TO_I64 else dt, []).append(k)
+            for dt, gkeys in groups.items():
+                st = _stage_host(per_key, gkeys, dt, device)
+                out_dt = torch.float32 if dt == torch.int64 else dt
+                out = torch.empty(_pad(max(st.length, 1)), dtype=out_dt, device=device)
+                if st.length:
+                    w_dev = kn.upload_f64(weights, device) if dt == torch.float64 else kn.upload_f32(weights, device)
+                    d_ptrs = kn.upload_i64(_row_ptrs(st.rows), device)
+                    kn.wsum_ptrs(dt, d_ptrs, w_dev, K, st.length, out, True, acc_mode)
+                results.update(_to_host(out[:st.length], st, {k: per_key[k][0].shape for k in gkeys}))
+
+    # ---- device-resident inputs: read in place --------------------------------
+    if dev_keys:
+        by_dev: Dict[torch.device, List[str]] = OrderedDict()
+        for k in dev_keys:
+            by_dev.setdefault(per_key[k][0].device, []).append(k)
+        for device, dkeys in by_dev.items():
+            with torch.cuda.device(device):
+                w32 = kn.upload_f32(weights, device)
+                w64 = None
+                multi_keys, multi_src, multi_out = [], [], []
+                for k in dkeys:
+                    ts = [t if t.is_contiguous() else t.contiguous() for t in per_key[k]]
+                    dt = ts[0].dtype
+                    if dt in _INT_TO_I64 and dt != torch.int64:
+                        ts = [t.to(torch.int64) for t in ts]
+                        dt = torch.int64
+                    out = torch.empty(ts[0].shape, dtype=torch.float32 if dt == torch.int64 else dt,
+                                      device=device)
+                    results[k] = out
+                    n = out.numel()
+                    if n == 0:
+                        continue
+                    ptrs = [t.data_ptr() for t in ts]
+                    if dt == torch.float32 and kn.aligned16(ptrs) and (out.data_ptr() & 15) == 0:
+                        multi_keys.append(k)
+                        multi_src.extend(ptrs)
+                        multi_out.append(out.data_ptr())
+                        per_key[k] = ts  # keep any contiguous copies alive
+                        continue
+                    if dt == torch.float64 and w64 is None:
+                        w64 = kn.upload_f64(weights, device)
+                    kn.wsum_ptrs(dt, kn.upload_i64(ptrs, device), w64 if dt == torch.float64 else w32, K, n, out,
+                                 kn.aligned16(ptrs), acc_mode)
+                if multi_keys:
+                    plan = kn.MultiF32Plan([results[k].numel() for k in multi_keys])
+                    plan.launch(multi_src, multi_out, w32, K, device)
+
+    return OrderedDict((k, results[k]) for k in keys)
+
+
+def sequential_sum_inplace(dicts: Sequence["OrderedDict"], keys: Sequence[str], args) -> None:
+    """avg = p_0 ; avg += p_i, updating client 0's tensors in place
+    (agg_operator.py:55-63, :68-77)."""
+    per_key = _gather(dicts, keys)
+    K = len(dicts)
+    for k in keys:
+        ts = per_key[k]
+        t0 = ts[0]
+        if t0.numel() == 0:
+            continue
+        dt = t0.dtype
+        if dt not in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32):
+            raise TypeError(f"key {k!r}: unsupported dtype {dt} for an unweighted sum")
+        if t0.is_cuda and all(t.is_contiguous() for t in ts):
+            device = t0.device
+            with torch.cuda.device(device):
+                ptrs = [t.data_ptr() for t in ts]
+                kn.sum_ptrs(dt, kn.upload_i64(ptrs, device), K, t0.numel(), t0, kn.aligned16(ptrs))
+            continue
+        device = t0.device if t0.is_cuda else _host_device(args)
+        with torch.cuda.device(device):
+            st = _stage_host({k: ts}, [k], dt, device)
+            d_ptrs = kn.upload_i64(_row_ptrs(st.rows), device)
+            row0 = st.rows[0]
+            kn.sum_ptrs(dt, d_ptrs, K, st.length, row0, True)
+            t0.copy_(row0[:st.length].reshape(t0.shape))
+
+
+def torch_aggregator(args, raw_grad_list, training_num):
+    """agg_operator.py:33-134, branch for branch."""
+    opt = args.federated_optimizer
+    K = len(raw_grad_list)
+    if opt in ("FedAvg", "FedProx"):
+        (num0, avg_params) = raw_grad_list[0]
+        keys = list(avg_params.keys())
+        if not keys:
+            return avg_params
+        weights = [raw_grad_list[i][0] / training_num for i in range(K)]  # ZeroDivisionError as :39
+        res = weighted_reduce([raw_grad_list[i][1] for i in range(K)], keys, weights, args)
+        for k in keys:  # rebinds client 0's keys; its original tensors stay untouched
+            avg_params[k] = res[k]
+        return avg_params
+    if opt in ("FedAvg_seq", "FedDyn"):
+        (num0, avg_params) = raw_grad_list[0]
+        keys = list(avg_params.keys())
+        sequential_sum_inplace([raw_grad_list[i][1] for i in range(K)], keys, args)
+        return avg_params
+    if opt == "SCAFFOLD":
+        (num0, total_weights_delta, total_c_delta_para) = raw_grad_list[0]
+        keys = list(total_weights_delta.keys())
+        _gather([raw_grad_list[i][1] for i in range(K)], keys)  # KeyError parity
+        _gather([raw_grad_list[i][2] for i in range(K)], keys)
+        _, weights_delta, c_delta_para = raw_grad_list[K - 1]
+        w_c = 1 / args.client_num_in_total
+        # :116-117 overwrite the weighted sums with the LAST client's delta and
+        # its control variate times w_c; only that survives.
+        scaled = weighted_reduce([c_delta_para], keys, [w_c], args)
+        for k in keys:
+            total_weights_delta[k] = weights_delta[k]
+            total_c_delta_para[k] = scaled[k]
+        return (total_weights_delta, total_c_delta_para)
+    if opt == "Mime":
+        (num0, avg_params, avg_local_grad) = raw_grad_list[0]
+        assert args.client_num_per_round == len(raw_grad_list)
+        keys = list(avg_params.keys())
+        weights = [raw_grad_list[i][0] / training_num for i in range(K)] if keys else []
+        res_p = weighted_reduce([raw_grad_list[i][1] for i in range(K)], keys, weights, args)
+        res_g = weighted_reduce([raw_grad_list[i][2] for i in range(K)], keys, weights, args)
+        for k in keys:
+            avg_params[k] = res_p[k]
+            avg_local_grad[k] = res_g[k]
+        return (avg_params, avg_local_grad)
+    # FedOpt / FedNova are `pass` in the reference (:64-67) and any other name
+    # falls through: `return avg_params` then raises UnboundLocalError.  Server
+    # optimizers live in fedml_amd.fedopt instead.
+    raise UnboundLocalError("local variable 'avg_params' referenced before assignment")

@@ -246,8 +246,18 @@ struct Seg {
 template <class OP>
 __device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const typename OP::w_t* __restrict__ w,
                                               int K, int64_t e) {
-  typename OP::acc_t acc = OP::first(s.src[0][e], w ? w[0] : typename OP::w_t(0));
-  for (int c = 1; c < K; ++c) acc = OP::step(acc, s.src[c][e], w ? w[c] : typename OP::w_t(0));
+  using w_t = typename OP::w_t;
+  constexpr int SU = 16;  // clients in flight per lane: tiny tensors are latency-bound
+  typename OP::acc_t acc = OP::first(s.src[0][e], w ? w[0] : w_t(0));
+  int c = 1;
+  for (; c + SU <= K; c += SU) {
+    typename OP::in_t x[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) x[u] = s.src[c + u][e];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) acc = OP::step(acc, x[u], w ? w[c + u] : w_t(0));
+  }
+  for (; c < K; ++c) acc = OP::step(acc, s.src[c][e], w ? w[c] : w_t(0));
   s.out[e] = OP::fin(acc);
 }
 

@@ -1,0 +1,145 @@
+"""Thin typed wrappers over the C ABI (include/fedagg.h) for torch tensors.
+
+Every function here launches on the CURRENT torch stream of the tensors'
+device and returns without synchronising.  Pointer tables and weight vectors
+are uploaded from pinned host memory on that same stream, so they are
+stream-ordered with the kernel that reads them.  There is no CPU fallback:
+non-CUDA tensors raise.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+
+from . import _native as nat
+
+_DT_CODE = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16, torch.float16: nat.DT_F16,
+            torch.float64: nat.DT_F64, torch.int64: nat.DT_I64, torch.int32: nat.DT_I32}
+
+ACC_REFERENCE = nat.FEDAGG_ACC_REFERENCE
+ACC_FP32 = nat.FEDAGG_ACC_FP32
+
+
+def _require_cuda(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise nat.FedAggNativeError(f"{what}: expected a device tensor, got {t.device} (no CPU fallback)")
+
+
+def upload_i64(values: Sequence[int], device: torch.device) -> torch.Tensor:
+    host = torch.tensor(list(values), dtype=torch.int64)
+    if torch.cuda.is_available():
+        host = host.pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def upload_f32(values: Sequence[float], device: torch.device) -> torch.Tensor:
+    host = torch.tensor([float(v) for v in values], dtype=torch.float32)
+    if torch.cuda.is_available():
+        host = host.pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def upload_f64(values: Sequence[float], device: torch.device) -> torch.Tensor:
+    host = torch.tensor([float(v) for v in values], dtype=torch.float64)
+    if torch.cuda.is_available():
+        host = host.pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def aligned16(ptrs: Sequence[int]) -> bool:
+    return all((p & 15) == 0 for p in ptrs)
+
+
+def wsum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int,
+              out: torch.Tensor, aligned: bool, acc_mode: int = ACC_REFERENCE) -> None:
+    """Weighted sum over K sources given as a device pointer table."""
+    _require_cuda(out, "wsum")
+    lib = nat.lib()
+    st = nat.stream_handle()
+    flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0
+    a = (d_ptrs.data_ptr(), d_w.data_ptr(), K, N, out.data_ptr())
+    if dtype == torch.float32:
+        if out.dtype == torch.float32:
+            rc = lib.fedagg_wsum_f32(*a, flags, st)
+        else:
+            raise TypeError("fp32 sources produce fp32")
+    elif dtype == torch.bfloat16:
+        if out.dtype == torch.bfloat16:
+            rc = lib.fedagg_wsum_bf16(*a, acc_mode, flags, st)
+        elif out.dtype == torch.float32:
+            rc = lib.fedagg_wsum_bf16_f32out(*a, flags, st)
+        else:
+            raise TypeError("bf16 sources produce bf16 or an fp32 partial")
+    elif dtype == torch.float16:
+        rc = lib.fedagg_wsum_f16(*a, acc_mode, flags, st)
+    elif dtype == torch.float64:
+        rc = lib.fedagg_wsum_f64(*a, flags, st)
+    elif dtype == torch.int64:
+        rc = lib.fedagg_wsum_i64_f32(*a, flags, st)
+    else:
+        raise TypeError(f"wsum: unsupported dtype {dtype}")
+    nat.check(rc, f"wsum[{dtype}]")
+
+
+def sum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor, aligned: bool) -> None:
+    """Unweighted sequential sum (FedAvg_seq / FedDyn)."""
+    _require_cuda(out, "sum")
+    if dtype not in _DT_CODE:
+        raise TypeError(f"sum: unsupported dtype {dtype}")
+    flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0
+    nat.check(nat.lib().fedagg_sum(_DT_CODE[dtype], d_ptrs.data_ptr(), K, N, out.data_ptr(), flags,
+                                   nat.stream_handle()), f"sum[{dtype}]")
+
+
+def wsum_tensors(tensors: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
+                 acc_mode: int = ACC_REFERENCE) -> None:
+    """Weighted sum of K contiguous same-shape device tensors into out."""
+    dev = out.device
+    ptrs = [t.data_ptr() for t in tensors]
+    d_ptrs = upload_i64(ptrs, dev)
+    dtype = tensors[0].dtype
+    d_w = upload_f64(weights, dev) if dtype == torch.float64 else upload_f32(weights, dev)
+    wsum_ptrs(dtype, d_ptrs, d_w, len(tensors), tensors[0].numel(), out, aligned16(ptrs), acc_mode)
+
+
+class MultiF32Plan:
+    """Segment table for the one-launch multi-tensor fp32 kernel
+    (fedagg_wsum_multi_f32): T keys, each with K client pointers."""
+
+    def __init__(self, numels: Sequence[int]):
+        lib = nat.lib()
+        self.numels = [int(n) for n in numels]
+        begin = [0]
+        for n in self.numels:
+            nb = lib.fedagg_multi_blocks(nat.DT_F32, n)
+            if nb < 0:
+                raise ValueError("bad numel")
+            begin.append(begin[-1] + nb)
+        self.block_begin = begin
+        self.total_blocks = begin[-1]
+
+    def launch(self, src_ptrs: List[int], out_ptrs: List[int], d_w: torch.Tensor, K: int,
+               device: torch.device) -> List[torch.Tensor]:
+        """src_ptrs is the flattened [T][K] table.  Returns the device tables,
+        which must stay referenced until the launch has been enqueued."""
+        T = len(self.numels)
+        d_src = upload_i64(src_ptrs, device)
+        d_out = upload_i64(out_ptrs, device)
+        d_numel = upload_i64(self.numels, device)
+        d_begin = upload_i64(self.block_begin, device)
+        nat.check(nat.lib().fedagg_wsum_multi_f32(d_src.data_ptr(), d_out.data_ptr(), d_numel.data_ptr(),
+                                                  d_begin.data_ptr(), T, d_w.data_ptr(), K, self.total_blocks,
+                                                  nat.stream_handle()), "wsum_multi_f32")
+        return [d_src, d_out, d_numel, d_begin]
+
+
+def fedopt_sgd(param: torch.Tensor, mom: torch.Tensor | None, avg: torch.Tensor, lr: float, momentum: float,
+               first_step: bool) -> None:
+    """Fused server SGD(+momentum) step on flat fp32 device tensors, in place."""
+    _require_cuda(param, "fedopt_sgd")
+    if param.dtype != torch.float32 or avg.dtype != torch.float32:
+        raise TypeError("fedopt_sgd: fp32 only")
+    nat.check(nat.lib().fedagg_fedopt_sgd_f32(param.data_ptr(), mom.data_ptr() if mom is not None else None,
+                                              avg.data_ptr(), param.numel(), float(lr), float(momentum),
+                                              int(first_step), nat.stream_handle()), "fedopt_sgd_f32")

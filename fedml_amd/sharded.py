@@ -1,0 +1,201 @@
+"""Multi-GPU server aggregation inside one node.
+
+The reference server is one process (fedml/__init__.py:339-347 forces one
+process per silo for the server), so this is new: one process per GPU, the
+round's client updates spread over G GPUs, torch.distributed over RCCL/xGMI.
+
+Two partitionings:
+
+client axis (``ClientAxisAggregator``, the north-star mode)
+    GPU g holds whole updates of its own clients K_g (they arrive whole per
+    client) and computes the fp32 partial Σ_{i∈K_g} fl(p_i·w_i) with the
+    GLOBAL weights w_i = n_i / Σ_all n.  One RCCL reduce-scatter(sum) then
+    leaves GPU g owning elements [g·N/G, (g+1)·N/G) of the average.  The
+    parameter axis is cut into chunks; the reduce-scatter of chunk c runs on a
+    communication stream while chunk c+1 is being reduced, so the exchange
+    ((G-1)/G · N · 4 B per GPU) hides under the HBM-bound reduction.  The
+    addition order across GPUs differs from the single-GPU chain, so results
+    carry a stated tolerance (see ``tolerance``).
+
+parameter axis (``ParamAxisAggregator``)
+    GPU g holds columns [g·N/G, (g+1)·N/G) of EVERY client and reduces them
+    locally in the reference order: zero exchange, bit-exact.  The result is
+    sharded exactly like the client-axis result.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as kn
+
+F32_EPS = 2.0 ** -24
+
+
+def shard_range(n: int, world: int, rank: int, align: int = 64) -> Tuple[int, int]:
+    """Rank's [lo, hi) of an n-element axis, boundaries 64-element aligned."""
+    per = (n + world - 1) // world
+    per = (per + align - 1) // align * align
+    lo = min(n, rank * per)
+    return lo, min(n, lo + per)
+
+
+class ClientAxisAggregator:
+    """Client-axis sharded FedAvg over fp32 or bf16 rows.
+
+    rows: this rank's [K_local, L_pad] client rows (any layout; only the first
+    ``length`` elements are reduced).  ``aggregate(global_weights_local)``
+    returns this rank's shard of the fp32 result (``[shard_len]``) on the
+    current stream.
+    """
+
+    def __init__(self, rows: torch.Tensor, length: int, group=None, chunks: int = 8, reducer=None):
+        """reducer: test hook ``reducer(rows_chunk [K, n], weights, out [n])``
+        replacing the HIP kernel, so the partitioning and the collective can be
+        exercised with host tensors over gloo (tests/test_sharded_gloo.py)."""
+        self.rows = rows
+        self.reducer = reducer
+        self.on_gpu = rows.is_cuda
+        self.dtype = rows.dtype
+        self.length = length
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.K = rows.shape[0]
+        dev = rows.device
+        self.device = dev
+        esz = rows.element_size()
+        # Chunk c covers [c*chunk_len, (c+1)*chunk_len) of a world*64-aligned
+        # padded axis, so every chunk splits into `world` equal, aligned pieces.
+        unit = self.world * 64
+        padded = (length + unit - 1) // unit * unit
+        chunks = max(1, min(chunks, padded // unit))
+        chunk_len = (padded // chunks + unit - 1) // unit * unit
+        self.chunk_len = chunk_len
+        self.bounds: List[Tuple[int, int]] = []
+        lo = 0
+        while lo < length:
+            self.bounds.append((lo, min(length, lo + chunk_len)))
+            lo += chunk_len
+        self.piece = chunk_len // self.world
+        self.partial = torch.zeros(len(self.bounds) * chunk_len, dtype=torch.float32, device=dev)
+        self.shard = torch.empty(len(self.bounds) * self.piece, dtype=torch.float32, device=dev)
+        if self.on_gpu:
+            # per-chunk source pointer tables (row base + chunk offset)
+            self.d_ptrs = [kn.upload_i64([rows[i].data_ptr() + lo * esz for i in range(self.K)], dev)
+                           for lo, _ in self.bounds]
+        elif reducer is None:
+            raise ValueError("host rows need a reducer (the HIP kernels read HBM only)")
+        self.comm_stream = torch.cuda.Stream(dev) if self.world > 1 and self.on_gpu else None
+
+    def owned_ranges(self) -> List[Tuple[int, int]]:
+        """Global element ranges this rank owns, in shard order (one per chunk)."""
+        out = []
+        for c, (lo, _) in enumerate(self.bounds):
+            a = lo + self.rank * self.piece
+            out.append((a, a + self.piece))
+        return out
+
+    def aggregate(self, weights: Sequence[float], events: Optional[List] = None) -> torch.Tensor:
+        """weights: the GLOBAL w_i of this rank's K_local clients, in order."""
+        if not self.on_gpu:
+            return self._aggregate_host(weights)
+        cur = torch.cuda.current_stream(self.device)
+        d_w = kn.upload_f32(weights, self.device)
+        works = []
+        for c, (lo, hi) in enumerate(self.bounds):
+            part = self.partial[c * self.chunk_len: c * self.chunk_len + (hi - lo)]
+            if events is not None:
+                events[c][0].record(cur)
+            if self.reducer is not None:
+                self.reducer(self.rows[:, lo:hi], weights, part)
+            else:
+                kn.wsum_ptrs(self.dtype, self.d_ptrs[c], d_w, self.K, hi - lo, part, True)
+            if events is not None:
+                events[c][1].record(cur)
+            if self.world > 1:
+                # chunk c's exchange overlaps chunk c+1's reduction
+                self.comm_stream.wait_stream(cur)
+                with torch.cuda.stream(self.comm_stream):
+                    works.append(dist.reduce_scatter_tensor(
+                        self.shard[c * self.piece:(c + 1) * self.piece],
+                        self.partial[c * self.chunk_len:(c + 1) * self.chunk_len],
+                        op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            else:
+                self.shard[c * self.piece:(c + 1) * self.piece].copy_(
+                    self.partial[c * self.chunk_len:(c + 1) * self.chunk_len])
+        for w in works:
+            w.wait()  # makes the current stream wait for the collective
+        if self.world > 1:
+            cur.wait_stream(self.comm_stream)
+        return self.shard
+
+    def _aggregate_host(self, weights: Sequence[float]) -> torch.Tensor:
+        for c, (lo, hi) in enumerate(self.bounds):
+            self.reducer(self.rows[:, lo:hi], weights, self.partial[c * self.chunk_len: c * self.chunk_len + (hi - lo)])
+            src = self.partial[c * self.chunk_len:(c + 1) * self.chunk_len]
+            dst = self.shard[c * self.piece:(c + 1) * self.piece]
+            if self.world > 1:
+                dist.reduce_scatter_tensor(dst, src, op=dist.ReduceOp.SUM, group=self.group)
+            else:
+                dst.copy_(src)
+        return self.shard
+
+    def gather_full(self) -> torch.Tensor:
+        """Reassemble the full [length] result on every rank (all-gather of the
+        shards; used by tests and when the model must be replicated)."""
+        parts = [torch.empty_like(self.shard) for _ in range(self.world)]
+        if self.world > 1:
+            dist.all_gather(parts, self.shard, group=self.group)
+        else:
+            parts = [self.shard]
+        full = torch.empty(len(self.bounds) * self.chunk_len, dtype=self.shard.dtype, device=self.shard.device)
+        for c in range(len(self.bounds)):
+            for r in range(self.world):
+                full[c * self.chunk_len + r * self.piece: c * self.chunk_len + (r + 1) * self.piece] = \
+                    parts[r][c * self.piece:(c + 1) * self.piece]
+        return full[:self.length]
+
+    @staticmethod
+    def tolerance(abs_terms_sum: torch.Tensor, k_total: int, world: int) -> torch.Tensor:
+        """Per-element bound vs the single-GPU chain: both are sums of the same
+        products fl(w_i p_i) in different orders, so
+        |Δ| <= 2·(K + log2 G + 1)·2^-24·Σ_i |fl(w_i p_i)|."""
+        import math
+
+        return 2.0 * (k_total + math.ceil(math.log2(max(world, 1))) + 1) * F32_EPS * abs_terms_sum
+
+
+class ParamAxisAggregator:
+    """Parameter-axis sharded FedAvg: bit-exact, no collective.
+
+    rows: this rank's [K, L_pad] slice of every client (columns of its shard).
+    """
+
+    def __init__(self, rows: torch.Tensor, length: int, reducer=None):
+        self.rows = rows
+        self.length = length
+        self.K = rows.shape[0]
+        self.device = rows.device
+        self.reducer = reducer
+        if rows.is_cuda:
+            self.d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(self.K)], self.device)
+        elif reducer is None:
+            raise ValueError("host rows need a reducer (the HIP kernels read HBM only)")
+        out_dtype = torch.float32 if rows.dtype == torch.int64 else rows.dtype
+        self.out = torch.empty(max(length, 1), dtype=out_dtype, device=self.device)
+
+    def aggregate(self, weights: Sequence[float], events: Optional[List] = None) -> torch.Tensor:
+        if self.reducer is not None:
+            self.reducer(self.rows[:, :self.length], weights, self.out[:self.length])
+            return self.out[:self.length]
+        cur = torch.cuda.current_stream(self.device)
+        d_w = kn.upload_f32(weights, self.device)
+        if events is not None:
+            events[0][0].record(cur)
+        kn.wsum_ptrs(self.rows.dtype, self.d_ptrs, d_w, self.K, self.length, self.out, True)
+        if events is not None:
+            events[0][1].record(cur)
+        return self.out[:self.length]

@@ -1,0 +1,113 @@
+"""CPU-side checks of the boundary: the library loads, exports every symbol the
+header declares with the ctypes signatures we bind, validates arguments
+without touching a GPU, and the product path refuses to run without one."""
+from __future__ import annotations
+
+import os
+import re
+from collections import OrderedDict
+
+import pytest
+import torch
+
+from fedml_amd import _native as nat
+from fedml_amd import build as fbuild
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fedagg.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fedagg_\w+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    fbuild.build()
+    return nat.lib()
+
+
+def test_every_header_symbol_exported(lib):
+    names = header_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(nat.SIGNATURES), "ctypes signatures out of sync with include/fedagg.h"
+
+
+def test_library_is_gfx950_code_object():
+    path = fbuild.build()
+    data = open(path, "rb").read()
+    assert b"gfx950" in data
+    assert b"__hip_fatbin" in data or b"HIP_FATBIN" in data or b".hip_fatbin" in data
+
+
+def test_argument_validation_without_gpu(lib):
+    # invalid sizes are rejected before any HIP call
+    assert lib.fedagg_wsum_f32(None, None, 0, 10, None, 0, None) == -1
+    assert b"K must be" in lib.fedagg_last_error()
+    assert lib.fedagg_wsum_f32(None, None, 4, -1, None, 0, None) == -1
+    assert lib.fedagg_wsum_bf16(1, 1, 2, 10, 1, 7, 1, None) == -1
+    assert lib.fedagg_sum(99, 1, 2, 10, 1, 0, None) == -1
+    assert lib.fedagg_multi_blocks(1, 100) == -1
+    assert lib.fedagg_version() == 1
+    assert lib.fedagg_num_variants() > 0
+
+
+def test_multi_block_plan(lib):
+    from fedml_amd.kernels import MultiF32Plan
+
+    plan = MultiF32Plan([0, 1, 4096, 25_000_000])
+    assert plan.block_begin[0] == 0 and plan.block_begin[1] == 0
+    assert plan.block_begin[2] == 1
+    per_block = 4096 // (plan.block_begin[3] - plan.block_begin[2])
+    assert per_block >= 1024
+    assert plan.total_blocks == plan.block_begin[-1]
+
+
+def test_no_cpu_fallback():
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check")
+    from fedml_amd.agg_operator import FedMLAggOperator
+
+    raw = [(1, OrderedDict(a=torch.ones(3))), (3, OrderedDict(a=torch.zeros(3)))]
+    with pytest.raises(nat.FedAggNativeError):
+        FedMLAggOperator.agg(type("A", (), {"federated_optimizer": "FedAvg"})(), raw)
+
+
+def test_reference_errors_before_device_work():
+    """Errors the reference raises on the host come out identically, without a GPU."""
+    from fedml_amd.agg_operator import FedMLAggOperator
+
+    A = type("A", (), {"federated_optimizer": "FedAvg"})
+    with pytest.raises(ZeroDivisionError):
+        FedMLAggOperator.agg(A(), [(0, OrderedDict(a=torch.ones(3))), (0, OrderedDict(a=torch.ones(3)))])
+    with pytest.raises(ValueError):
+        FedMLAggOperator.agg(A(), [(1, OrderedDict(a=torch.ones(3)), OrderedDict())])
+    with pytest.raises(UnboundLocalError):
+        FedMLAggOperator.agg(type("B", (), {"federated_optimizer": "FedOpt"})(), [(1, OrderedDict())])
+    with pytest.raises(NotImplementedError):
+        FedMLAggOperator.agg(type("C", (), {"federated_optimizer": "FedAvg", "ml_engine": "tf"})(),
+                             [(1, OrderedDict())])
+    # empty state dict: the reference never divides, returns client 0's dict
+    d = OrderedDict()
+    assert FedMLAggOperator.agg(A(), [(0, d)]) is d
+
+
+def test_server_aggregator_surface():
+    from fedml_amd.server_aggregator import MI355XServerAggregator
+
+    m = torch.nn.Linear(3, 2)
+    args = type("A", (), {"federated_optimizer": "FedAvg"})()
+    agg = MI355XServerAggregator(m, args)
+    sd = agg.get_model_params()
+    assert list(sd.keys()) == ["weight", "bias"]
+    lst = [(1, sd), (2, sd)]
+    out, idxs = agg.on_before_aggregation(lst)
+    assert out is lst and idxs == [0, 1]
+    x = OrderedDict(a=torch.ones(1))
+    assert agg.on_after_aggregation(x) is x
+    with pytest.raises(NotImplementedError):
+        MI355XServerAggregator(m, type("B", (), {"federated_optimizer": "FedAvg", "enable_dp": True})())

@@ -1,0 +1,127 @@
+"""Multi-rank partitioning, exercised on CPU with gloo (world_size 2 and 3).
+
+The GPU run uses RCCL and the HIP kernels; here the same partitioning code
+runs with host rows and the oracle as the per-rank reducer, so chunking,
+shard ownership, the reduce-scatter call pattern and reassembly are all
+checked without a GPU.
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import socket
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from fedml_amd.sharded import ClientAxisAggregator, ParamAxisAggregator, shard_range
+from oracle import fedavg_oracle as orc
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _clients(K: int, L: int) -> torch.Tensor:
+    rng = np.random.default_rng(1234)
+    base = rng.standard_normal(L, dtype=np.float32) * np.float32(0.05)
+    rows = np.stack([base + np.float32(0.01) * rng.standard_normal(L, dtype=np.float32) for _ in range(K)])
+    return torch.from_numpy(rows)
+
+
+def _oracle_reducer(rows, weights, out):
+    out.copy_(orc.wsum([rows[i].contiguous() for i in range(rows.shape[0])], weights))
+
+
+def _worker(rank, world, port, K_local, L, chunks, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        K = K_local * world
+        allrows = _clients(K, L)
+        ns = [int(v) for v in np.random.default_rng(7).integers(100, 1001, K)]
+        tot = sum(ns)
+        ws = [n / tot for n in ns]
+        # client axis: this rank owns clients [rank*K_local, (rank+1)*K_local)
+        mine = allrows[rank * K_local:(rank + 1) * K_local].clone()
+        agg = ClientAxisAggregator(mine, L, chunks=chunks, reducer=_oracle_reducer)
+        agg.aggregate(ws[rank * K_local:(rank + 1) * K_local])
+        full = agg.gather_full()
+        # param axis: this rank owns columns [lo, hi) of every client
+        lo, hi = shard_range(L, world, rank)
+        pagg = ParamAxisAggregator(allrows[:, lo:hi].contiguous(), hi - lo, reducer=_oracle_reducer)
+        pshard = pagg.aggregate(ws).clone()
+        sizes = [torch.tensor([0]) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([hi - lo]))
+        maxn = max(int(s) for s in sizes)
+        buf = torch.zeros(maxn)
+        buf[:hi - lo] = pshard
+        parts = [torch.zeros(maxn) for _ in range(world)]
+        dist.all_gather(parts, buf)
+        pfull = torch.cat([parts[r][:int(sizes[r])] for r in range(world)])
+        q.put((rank, full.numpy().copy(), pfull.numpy().copy(), agg.owned_ranges(), None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, None, None, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,K_local,L,chunks", [(2, 4, 10_001, 3), (3, 3, 4_097, 8), (2, 1, 65, 8)])
+def test_client_and_param_axis(world, K_local, L, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, K_local, L, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        rank, full, pfull, owned, err = q.get(timeout=120)
+        assert err is None, err
+        results[rank] = (full, pfull, owned)
+    for p in procs:
+        p.join(timeout=60)
+    K = K_local * world
+    allrows = _clients(K, L)
+    ns = [int(v) for v in np.random.default_rng(7).integers(100, 1001, K)]
+    ws = [n / sum(ns) for n in ns]
+    chain = orc.wsum([allrows[i] for i in range(K)], ws).numpy()
+    partials = [orc.wsum([allrows[i] for i in range(r * K_local, (r + 1) * K_local)],
+                         ws[r * K_local:(r + 1) * K_local]).numpy() for r in range(world)]
+    for r in range(world):
+        full, pfull, owned = results[r]
+        # parameter axis: bit-exact with the single-GPU chain
+        assert np.array_equal(pfull.view(np.uint32), chain.view(np.uint32))
+        # client axis: identical on every rank, and within the stated bound
+        assert np.array_equal(full.view(np.uint32), results[0][0].view(np.uint32))
+        terms = np.zeros(L, dtype=np.float64)
+        for i in range(K):
+            terms += np.abs(allrows[i].numpy().astype(np.float64) * np.float32(ws[i]))
+        bound = ClientAxisAggregator.tolerance(torch.from_numpy(terms), K, world).numpy()
+        assert np.all(np.abs(full.astype(np.float64) - chain.astype(np.float64)) <= bound)
+        if world == 2:  # two partials: the reduce-scatter sum is one rounding
+            assert np.array_equal(full.view(np.uint32), (partials[0] + partials[1]).view(np.uint32))
+        # ownership: disjoint pieces that tile the padded axis
+        for a, b in owned:
+            assert b > a
+    covered = sorted(rng for r in range(world) for rng in results[r][2])
+    for (a0, b0), (a1, b1) in zip(covered, covered[1:]):
+        assert b0 == a1
+    assert covered[0][0] == 0 and covered[-1][1] >= L
+
+
+def test_shard_range_tiles_axis():
+    for n in (0, 1, 63, 64, 65, 25_610_152):
+        for world in (1, 2, 3, 4, 8):
+            spans = [shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a0, b0), (a1, b1) in zip(spans, spans[1:]):
+                assert b0 == a1
+            for a, _ in spans:
+                assert a % 64 == 0 or a == n
