@@ -6,9 +6,9 @@ each tensor is moved to the device as the client arrives
 (cross_silo/server/fedml_aggregator.py:58-67 -> ml_engine_adapter.py:234-254).
 
 Here the round's updates live in one row-major [capacity, L] tensor per dtype:
-row i is client slot i, every state-dict key sits at a fixed element offset in
-the row (rows padded to 64 elements = 256 B so every row starts 16-byte
-aligned).  ``put`` copies an arriving client's dict straight into its row (the
+row i is client slot i, every state-dict key sits at a fixed, 16-byte aligned
+element offset in the row (rows padded to 64 elements = 256 B; the few
+alignment-gap elements are zero and reduce to zero).  ``put`` copies an arriving client's dict straight into its row (the
 H2D ingest point), and ``aggregate`` is then one kernel launch per dtype group
 over the whole model: for ResNet-50 one fp32 launch over 25,610,152 elements
 and one int64 launch over 53.
@@ -57,12 +57,16 @@ class _Group:
         self.d_ptrs: Optional[torch.Tensor] = None
 
     def add(self, key: str, shape) -> None:
+        # every key starts 16-byte aligned, so any run of keys can be reduced
+        # on the vector path (gaps are a few elements per key, zero-filled)
+        align = max(1, 16 // torch.empty((), dtype=self.dtype).element_size())
+        start = (self.length + align - 1) // align * align
         n = _numel(shape)
         self.keys.append(key)
         self.shapes.append(tuple(shape))
-        self.offsets.append(self.length)
+        self.offsets.append(start)
         self.numels.append(n)
-        self.length += n
+        self.length = start + n
 
 
 def _out_dtype(dt: torch.dtype) -> torch.dtype:
@@ -110,7 +114,7 @@ class ClientBucket:
             g.add(key, shape)
         with torch.cuda.device(self.device):
             for g in self.groups.values():
-                g.rows = torch.empty((capacity, _pad(max(g.length, 1))), dtype=g.dtype, device=self.device)
+                g.rows = torch.zeros((capacity, _pad(max(g.length, 1))), dtype=g.dtype, device=self.device)
                 g.d_ptrs = kn.upload_i64([g.rows[i].data_ptr() for i in range(capacity)], self.device)
         self.sample_nums: List[Optional[float]] = [None] * capacity
         self._side: Optional[torch.cuda.Stream] = None
@@ -236,4 +240,5 @@ class ClientBucket:
         return tot
 
     def num_elements(self) -> int:
-        return sum(g.length for g in self.groups.values())
+        """State-dict elements per client (excluding alignment gaps)."""
+        return sum(sum(g.numels) for g in self.groups.values())

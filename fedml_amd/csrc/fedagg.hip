@@ -233,18 +233,77 @@ __device__ __forceinline__ void store_pack(T* p, const T (&v)[E]) {
   }
 }
 
-// One tensor ("segment") of the reduction: K source pointers, one output.
+// One tensor ("segment") of the reduction: K source pointers and its length.
 template <class OP>
 struct Seg {
   const typename OP::in_t* const* src;  // device table of K pointers
-  typename OP::out_t* out;
   int64_t numel;
+};
+
+// Epilogues: what happens to a finished running sum.  pack() takes the E sums
+// of one 16-byte input pack at element offset `off`, one() a single element.
+
+// Plain FedAvg: round to the output dtype and store (non-temporal: written once).
+template <class OP>
+struct StoreEpi {
+  typename OP::out_t* out;
+  static constexpr int E = 16 / sizeof(typename OP::in_t);
+  __device__ __forceinline__ void pack(int64_t off, const typename OP::acc_t (&acc)[E]) const {
+    typename OP::out_t o[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) o[e] = OP::fin(acc[e]);
+    store_pack<typename OP::out_t, E>(out + off, o);
+  }
+  __device__ __forceinline__ void one(int64_t e, typename OP::acc_t a) const { out[e] = OP::fin(a); }
+};
+
+// FedOpt server step fused onto the fp32 average (FedOptAggregator.py:104-125
+// with torch.optim.SGD): the average never goes to HBM.
+//   g = p_old - avg ; buf = first ? g : fl(fl(buf*m) + g) ; p = fma(buf, -lr, p_old)
+// momentum == 0: torch steps with g directly and keeps no buffer.
+struct SgdEpi {
+  float* p;
+  float* mom;  // nullptr when momentum == 0
+  float neg_lr, m;
+  int first;
+  static constexpr int E = 4;
+  __device__ __forceinline__ float step1(float po, float avg, float* mb) const {
+    const float g = po - avg;
+    float b = g;
+    if (mom) {
+      if (!first) {
+        const float t = *mb * m;  // buf.mul_(m)
+        b = t + g;                // .add_(grad): two roundings (-ffp-contract=off)
+      }
+      *mb = b;
+    }
+    return __builtin_fmaf(b, neg_lr, po);  // p.add_(buf, alpha=-lr): torch's fused fmadd
+  }
+  __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E]) const {
+    auto pv = load_pack<float, false>(p + off);
+    Pack<float, 4> mv = {};
+    if (mom && !first) mv = load_pack<float, false>(mom + off);
+    float po[E], mo[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float mb = mv.v[e];
+      po[e] = step1(pv.v[e], acc[e], &mb);
+      mo[e] = mb;
+    }
+    store_pack<float, E>(p + off, po);
+    if (mom) store_pack<float, E>(mom + off, mo);
+  }
+  __device__ __forceinline__ void one(int64_t e, float a) const {
+    float mb = (mom && !first) ? mom[e] : 0.f;
+    p[e] = step1(p[e], a, &mb);
+    if (mom) mom[e] = mb;
+  }
 };
 
 // Scalar path: one element at a time, identical arithmetic.  Used for the
 // ragged tail of a tensor and for unaligned pointers.
-template <class OP>
-__device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const typename OP::w_t* __restrict__ w,
+template <class OP, class EPI>
+__device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, const typename OP::w_t* __restrict__ w,
                                               int K, int64_t e) {
   using w_t = typename OP::w_t;
   constexpr int SU = 16;  // clients in flight per lane: tiny tensors are latency-bound
@@ -258,25 +317,24 @@ __device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const typename O
     for (int u = 0; u < SU; ++u) acc = OP::step(acc, x[u], w ? w[c + u] : w_t(0));
   }
   for (; c < K; ++c) acc = OP::step(acc, s.src[c][e], w ? w[c] : w_t(0));
-  s.out[e] = OP::fin(acc);
+  epi.one(e, acc);
 }
 
-// Body of one workgroup: packs [pack0, pack0 + kBlock*V) of segment s.
-template <class OP, int U, int V, bool NT, bool ALIGNED>
-__device__ __forceinline__ void reduce_block(const Seg<OP>& s, const typename OP::w_t* __restrict__ w,
-                                             int K, int64_t pack0) {
+// Body of one workgroup of BS lanes: packs [pack0, pack0 + BS*V) of segment s.
+template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI>
+__device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
+                                             const typename OP::w_t* __restrict__ w, int K, int64_t pack0) {
   using in_t = typename OP::in_t;
-  using out_t = typename OP::out_t;
   using w_t = typename OP::w_t;
   constexpr int E = 16 / sizeof(in_t);
   const int t = threadIdx.x;
   const int64_t full_packs = s.numel / E;
 
-  if (ALIGNED && pack0 + int64_t(kBlock) * V <= full_packs) {
+  if (ALIGNED && pack0 + int64_t(BS) * V <= full_packs) {
     // ---- fast path: every lane owns V whole 16-byte packs --------------------
     int64_t off[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) off[v] = (pack0 + v * kBlock + t) * E;
+    for (int v = 0; v < V; ++v) off[v] = (pack0 + v * BS + t) * E;
 
     typename OP::acc_t acc[V][E];
     {
@@ -318,30 +376,25 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const typename OP
       }
     }
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      out_t o[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) o[e] = OP::fin(acc[v][e]);
-      store_pack<out_t, E>(s.out + off[v], o);
-    }
+    for (int v = 0; v < V; ++v) epi.pack(off[v], acc[v]);
   } else {
     // ---- edge path: element-wise with bounds ---------------------------------
     const int64_t e0 = pack0 * E;
-    const int64_t e1 = min(s.numel, (pack0 + int64_t(kBlock) * V) * E);
-    for (int64_t e = e0 + t; e < e1; e += kBlock) reduce_scalar<OP>(s, w, K, e);
+    const int64_t e1 = min(s.numel, (pack0 + int64_t(BS) * V) * E);
+    for (int64_t e = e0 + t; e < e1; e += BS) reduce_scalar<OP>(s, epi, w, K, e);
   }
 }
 
-template <class OP, int U, int V, bool NT, bool ALIGNED>
-__global__ __launch_bounds__(kBlock) void reduce_kernel(Seg<OP> s, const typename OP::w_t* __restrict__ w,
-                                                         int K) {
-  reduce_block<OP, U, V, NT, ALIGNED>(s, w, K, int64_t(blockIdx.x) * kBlock * V);
+template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI = StoreEpi<OP>>
+__global__ __launch_bounds__(BS) void reduce_kernel(Seg<OP> s, EPI epi, const typename OP::w_t* __restrict__ w,
+                                                    int K) {
+  reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, int64_t(blockIdx.x) * BS * V);
 }
 
 // Multi-tensor form: blockIdx -> (segment, block within segment) by binary
 // search over the prefix of per-segment block counts (wave-uniform, s_load).
-template <class OP, int U, int V, bool NT>
-__global__ __launch_bounds__(kBlock) void reduce_multi_kernel(
+template <class OP, int U, int V, bool NT, int BS>
+__global__ __launch_bounds__(BS) void reduce_multi_kernel(
     const typename OP::in_t* const* __restrict__ src_tab, typename OP::out_t* const* __restrict__ out_tab,
     const int64_t* __restrict__ numel, const int64_t* __restrict__ block_begin, int T,
     const typename OP::w_t* __restrict__ w, int K) {
@@ -351,37 +404,41 @@ __global__ __launch_bounds__(kBlock) void reduce_multi_kernel(
     const int mid = (lo + hi + 1) >> 1;
     if (block_begin[mid] <= b) lo = mid; else hi = mid - 1;
   }
-  Seg<OP> s{src_tab + int64_t(lo) * K, out_tab[lo], numel[lo]};
-  reduce_block<OP, U, V, NT, true>(s, w, K, (b - block_begin[lo]) * kBlock * V);
+  Seg<OP> s{src_tab + int64_t(lo) * K, numel[lo]};
+  StoreEpi<OP> epi{out_tab[lo]};
+  reduce_block<OP, U, V, NT, true, BS>(s, epi, w, K, (b - block_begin[lo]) * BS * V);
 }
 
 // ---------------------------------------------------------------------------
 // Shipped kernel configuration per op (chosen by tools/tune_wsum.py on MI355X).
 
-template <class OP> struct Cfg { static constexpr int U = 8, V = 1; static constexpr bool NT = true; };
+// fp32 at 128 x 25.6M on MI355X: U4V4nt 6.44 TB/s vs U8V1nt 6.25 (profiles/r01_tune_variants_s2.json).
+template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; static constexpr bool NT = true; };
 
 template <class OP>
 int64_t blocks_for(int64_t numel) {
   constexpr int E = 16 / sizeof(typename OP::in_t);
   const int64_t packs = (numel + E - 1) / E;
-  const int64_t per = int64_t(kBlock) * Cfg<OP>::V;
+  const int64_t per = int64_t(Cfg<OP>::BS) * Cfg<OP>::V;
   return (packs + per - 1) / per;
 }
 
-template <class OP, int U, int V, bool NT>
+template <class OP, int U, int V, bool NT, int BS = 256>
 int launch_uvn(const typename OP::in_t* const* src, const typename OP::w_t* w, int32_t K, int64_t N,
                typename OP::out_t* out, bool aligned, hipStream_t stream, const char* name) {
   constexpr int E = 16 / sizeof(typename OP::in_t);
   const int64_t packs = (N + E - 1) / E;
-  const int64_t per = int64_t(kBlock) * V;
+  const int64_t per = int64_t(BS) * V;
   const int64_t grid = (packs + per - 1) / per;
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, std::string(name) + ": N too large");
-  Seg<OP> s{src, out, N};
+  Seg<OP> s{src, N};
+  StoreEpi<OP> epi{out};
   if (aligned) {
-    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, true>), dim3(unsigned(grid)), dim3(kBlock), 0, stream, s, w, K);
-  } else {
-    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, false>), dim3(unsigned(grid)), dim3(kBlock), 0, stream, s, w,
+    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, true, BS>), dim3(unsigned(grid)), dim3(BS), 0, stream, s, epi, w,
                        K);
+  } else {
+    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, false, BS>), dim3(unsigned(grid)), dim3(BS), 0, stream, s, epi,
+                       w, K);
   }
   return check_launch(name);
 }
@@ -392,7 +449,7 @@ int launch(const void* const* src, const void* w, int32_t K, int64_t N, void* ou
   if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, std::string(name) + ": K must be >= 1 and N >= 0");
   if (!src || !out || (need_w && !w)) return set_error(FEDAGG_EINVAL, std::string(name) + ": null pointer");
   if (N == 0) return FEDAGG_OK;
-  return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT>(
+  return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS>(
       reinterpret_cast<const typename OP::in_t* const*>(src), reinterpret_cast<const typename OP::w_t*>(w), K, N,
       reinterpret_cast<typename OP::out_t*>(out), (flags & FEDAGG_ALIGNED16) != 0,
       reinterpret_cast<hipStream_t>(stream), name);
@@ -406,18 +463,19 @@ struct Variant {
   int (*fn)(const float* const*, const float*, int32_t, int64_t, float*, hipStream_t);
 };
 
-template <int U, int V, bool NT>
+template <int U, int V, bool NT, int BS>
 int variant_fn(const float* const* src, const float* w, int32_t K, int64_t N, float* out, hipStream_t st) {
-  return launch_uvn<OpF32, U, V, NT>(src, w, K, N, out, true, st, "fedagg_wsum_f32_variant");
+  return launch_uvn<OpF32, U, V, NT, BS>(src, w, K, N, out, true, st, "fedagg_wsum_f32_variant");
 }
 
 const Variant kVariants[] = {
-    {"U4V1nt", variant_fn<4, 1, true>},   {"U8V1nt", variant_fn<8, 1, true>},
-    {"U16V1nt", variant_fn<16, 1, true>}, {"U4V2nt", variant_fn<4, 2, true>},
-    {"U8V2nt", variant_fn<8, 2, true>},   {"U4V4nt", variant_fn<4, 4, true>},
-    {"U4V1", variant_fn<4, 1, false>},    {"U8V1", variant_fn<8, 1, false>},
-    {"U16V1", variant_fn<16, 1, false>},  {"U4V2", variant_fn<4, 2, false>},
-    {"U8V2", variant_fn<8, 2, false>},    {"U4V4", variant_fn<4, 4, false>},
+    {"U8V1nt", variant_fn<8, 1, true, 256>},      {"U8V2nt", variant_fn<8, 2, true, 256>},
+    {"U4V4nt", variant_fn<4, 4, true, 256>},      {"U2V4nt", variant_fn<2, 4, true, 256>},
+    {"U8V4nt", variant_fn<8, 4, true, 256>},      {"U2V8nt", variant_fn<2, 8, true, 256>},
+    {"U4V8nt", variant_fn<4, 8, true, 256>},      {"U1V8nt", variant_fn<1, 8, true, 256>},
+    {"U4V4nt_b128", variant_fn<4, 4, true, 128>}, {"U4V4nt_b512", variant_fn<4, 4, true, 512>},
+    {"U2V4nt_b512", variant_fn<2, 4, true, 512>}, {"U4V2nt_b1024", variant_fn<4, 2, true, 1024>},
+    {"U4V4", variant_fn<4, 4, false, 256>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -522,7 +580,7 @@ int fedagg_wsum_multi_f32(const float* const* d_src, float* const* d_out, const 
   if (total_blocks == 0) return FEDAGG_OK;
   if (total_blocks > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi_f32: too many blocks");
   using C = Cfg<OpF32>;
-  hipLaunchKernelGGL((reduce_multi_kernel<OpF32, C::U, C::V, C::NT>), dim3(unsigned(total_blocks)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((reduce_multi_kernel<OpF32, C::U, C::V, C::NT, C::BS>), dim3(unsigned(total_blocks)), dim3(C::BS), 0,
                      reinterpret_cast<hipStream_t>(stream), d_src, d_out, d_numel, d_block_begin, T, d_w, K);
   return check_launch("fedagg_wsum_multi_f32");
 }
@@ -536,6 +594,29 @@ int fedagg_fedopt_sgd_f32(float* d_param, float* d_mom, const float* d_avg, int6
   hipLaunchKernelGGL(fedopt_sgd_kernel, dim3(grid), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), d_param,
                      momentum != 0.0f ? d_mom : nullptr, d_avg, N, -lr, momentum, first_step);
   return check_launch("fedagg_fedopt_sgd_f32");
+}
+
+int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float* d_param,
+                               float* d_mom, float lr, float momentum, int32_t first_step, uint32_t flags,
+                               fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: K must be >= 1 and N >= 0");
+  if (!d_src || !d_w || !d_param || (momentum != 0.0f && !d_mom))
+    return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  using C = Cfg<OpF32>;
+  const int64_t grid = blocks_for<OpF32>(N);
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: N too large");
+  Seg<OpF32> s{d_src, N};
+  SgdEpi epi{d_param, momentum != 0.0f ? d_mom : nullptr, -lr, momentum, first_step};
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  if (flags & FEDAGG_ALIGNED16) {
+    hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, SgdEpi>), dim3(unsigned(grid)),
+                       dim3(C::BS), 0, st, s, epi, d_w, K);
+  } else {
+    hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, SgdEpi>), dim3(unsigned(grid)),
+                       dim3(C::BS), 0, st, s, epi, d_w, K);
+  }
+  return check_launch("fedagg_wsum_fedopt_sgd_f32");
 }
 
 const char* fedagg_last_error(void) { return g_last_error.c_str(); }

@@ -143,3 +143,15 @@ def fedopt_sgd(param: torch.Tensor, mom: torch.Tensor | None, avg: torch.Tensor,
     nat.check(nat.lib().fedagg_fedopt_sgd_f32(param.data_ptr(), mom.data_ptr() if mom is not None else None,
                                               avg.data_ptr(), param.numel(), float(lr), float(momentum),
                                               int(first_step), nat.stream_handle()), "fedopt_sgd_f32")
+
+
+def wsum_fedopt_sgd(d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int, param: torch.Tensor,
+                    mom: torch.Tensor | None, lr: float, momentum: float, first_step: bool, aligned: bool) -> None:
+    """FedAvg of K fp32 sources fused with the server SGD step: param (flat,
+    N elements) goes from p_old to p_new in place, mom is the momentum buffer."""
+    _require_cuda(param, "wsum_fedopt_sgd")
+    ok = aligned and (param.data_ptr() & 15) == 0 and (mom is None or (mom.data_ptr() & 15) == 0)
+    nat.check(nat.lib().fedagg_wsum_fedopt_sgd_f32(
+        d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), mom.data_ptr() if mom is not None else None,
+        float(lr), float(momentum), int(first_step), nat.FEDAGG_ALIGNED16 if ok else 0, nat.stream_handle()),
+        "wsum_fedopt_sgd_f32")

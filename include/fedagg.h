@@ -141,6 +141,18 @@ int fedagg_fedopt_sgd_f32(float* d_param, float* d_mom, const float* d_avg,
                           int64_t N, float lr, float momentum,
                           int32_t first_step, fedagg_stream_t stream);
 
+/* FedAvg of K fp32 clients fused with the server SGD step above, in ONE pass:
+ * the average is formed in registers and never written to HBM (saves 2·N·4 B
+ * against fedagg_wsum_f32 + fedagg_fedopt_sgd_f32).  Bit-identical to that
+ * two-kernel sequence and to FedOptAggregator.aggregate's named-parameter
+ * update (FedOptAggregator.py:93-112, :118-125).  d_param holds p_old on entry
+ * and p_new on return; d_mom the momentum buffer (unused if momentum == 0). */
+int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w,
+                               int32_t K, int64_t N, float* d_param,
+                               float* d_mom, float lr, float momentum,
+                               int32_t first_step, uint32_t flags,
+                               fedagg_stream_t stream);
+
 /* ---- Introspection ------------------------------------------------------ */
 const char* fedagg_last_error(void);
 int32_t fedagg_version(void);

@@ -185,3 +185,29 @@ def test_kernel_errors_are_loud(cuda_device):
     with pytest.raises(nat.FedAggNativeError):
         nat.check(nat.lib().fedagg_wsum_f32(None, None, 0, 10, None, 0, None), "bad")
     assert "K must be" in nat.lib().fedagg_last_error().decode()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.int64])
+def test_client_axis_single_rank_kernel_path(dtype, cuda_device):
+    """ClientAxisAggregator on one GPU (no collective): chunked kernel launches
+    over pointer tables offset per chunk must reproduce the single chain
+    (fp32 partial; bf16/int64 sources accumulate in fp32)."""
+    from fedml_amd.sharded import ClientAxisAggregator
+
+    K, L = 12, 300_007
+    g = torch.Generator(device=cuda_device).manual_seed(4)
+    rows = torch.zeros(K, (L + 63) // 64 * 64, device=cuda_device, dtype=dtype)
+    if dtype == torch.int64:
+        rows[:, :L] = torch.randint(-1000, 1000, (K, L), generator=g, device=cuda_device)
+    else:
+        rows[:, :L] = (torch.randn(K, L, generator=g, device=cuda_device) * 0.05).to(dtype)
+    ns = list(range(10, 10 + K))
+    ws = [n / sum(ns) for n in ns]
+    agg = ClientAxisAggregator(rows, L, chunks=5)
+    full = agg.aggregate(ws)[:L].cpu()
+    cpu_rows = rows[:, :L].cpu()
+    if dtype == torch.bfloat16:  # fp32 accumulate of bf16 inputs
+        exp = orc.wsum([cpu_rows[i].float() for i in range(K)], ws)
+    else:
+        exp = orc.wsum([cpu_rows[i] for i in range(K)], ws)
+    gu.assert_same(full, exp, f"client-axis {dtype}")
