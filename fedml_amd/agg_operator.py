@@ -30,10 +30,14 @@ import torch
 
 from . import _native as nat
 from . import kernels as kn
+from .bucket import ClientBucket
+
+_ACC_NAME = {kn.ACC_REFERENCE: "reference", kn.ACC_FP32: "fp32"}
 
 # torch promotes `int_tensor * python_float` to the default dtype float32.
 _INT_TO_I64 = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
 _FLOAT = (torch.float32, torch.bfloat16, torch.float16, torch.float64)
+_SUM_DTYPES = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32)
 
 
 class FedMLAggOperator:
@@ -105,68 +109,21 @@ def _gather(dicts: Sequence["OrderedDict"], keys: Sequence[str]) -> Dict[str, Li
 # Reduction engine
 
 
-class _Staged:
-    """Host inputs of one dtype group packed into device rows [K, L]."""
-
-    def __init__(self, keys, numels, dtype, dev_rows):
-        self.keys, self.numels, self.dtype, self.rows = keys, numels, dtype, dev_rows
-        self.offsets = []
-        o = 0
-        for n in numels:
-            self.offsets.append(o)
-            o += n
-        self.length = o
+_BUCKETS: "OrderedDict[tuple, ClientBucket]" = OrderedDict()
+_BUCKET_CACHE_SIZE = 2
 
 
-def _pad(n: int, a: int = 64) -> int:
-    return (n + a - 1) // a * a
-
-
-def _stage_host(per_key: Dict[str, List[torch.Tensor]], keys: Sequence[str], dtype: torch.dtype,
-                device: torch.device) -> _Staged:
-    """Pack each client's tensors of this dtype into a pinned row (one host
-    memcpy) and send it to HBM on a copy stream, double-buffered so packing
-    client i+1 overlaps the PCIe transfer of client i."""
-    K = len(per_key[keys[0]])
-    numels = [per_key[k][0].numel() for k in keys]
-    L = sum(numels)
-    rows = torch.empty((K, _pad(max(L, 1))), dtype=dtype, device=device)
-    cur = torch.cuda.current_stream(device)
-    copy_stream = torch.cuda.Stream(device)
-    copy_stream.wait_stream(cur)
-    pinned = [torch.empty(max(L, 1), dtype=dtype).pin_memory() for _ in range(2)]
-    done = [None, None]
-    with torch.cuda.stream(copy_stream):
-        for i in range(K):
-            b = i & 1
-            if done[b] is not None:
-                done[b].synchronize()
-            parts = [per_key[k][i].reshape(-1) for k in keys]
-            if parts:
-                parts = [p if p.dtype == dtype else p.to(dtype) for p in parts]
-                torch.cat(parts, out=pinned[b][:L])
-            rows[i, :L].copy_(pinned[b][:L], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(copy_stream)
-            done[b] = ev
-    cur.wait_stream(copy_stream)  # the reduction (on cur) runs after the last row landed
-    return _Staged(list(keys), numels, dtype, rows)
-
-
-def _to_host(flat: torch.Tensor, staged: _Staged, shapes: Dict[str, torch.Size]) -> Dict[str, torch.Tensor]:
-    """One D2H of the group's result, then independent per-key host tensors
-    (each its own storage, as the reference's per-key results are; a view into
-    one buffer would pickle the whole buffer per key on broadcast)."""
-    host = torch.empty(flat.numel(), dtype=flat.dtype).pin_memory()
-    host.copy_(flat)  # synchronous: the result is needed on the host now
-    out = {}
-    for k, off, n in zip(staged.keys, staged.offsets, staged.numels):
-        out[k] = host[off:off + n].clone().reshape(shapes[k])
-    return out
-
-
-def _row_ptrs(rows: torch.Tensor) -> List[int]:
-    return [rows[i].data_ptr() for i in range(rows.shape[0])]
+def _cached_bucket(layout, K: int, device: torch.device, acc: str) -> ClientBucket:
+    """Host-input rounds reuse their HBM rows and pinned staging: a server
+    aggregates the same model shape every round (LRU of 2 layouts)."""
+    key = (tuple((k, s, str(d)) for k, s, d in layout), K, str(device), acc)
+    b = _BUCKETS.pop(key, None)
+    if b is None:
+        b = ClientBucket(layout, K, device, low_precision_acc=acc)
+        while len(_BUCKETS) >= _BUCKET_CACHE_SIZE:
+            _BUCKETS.popitem(last=False)
+    _BUCKETS[key] = b
+    return b
 
 
 def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights: Sequence[float], args
@@ -181,23 +138,17 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
     host_keys = [k for k in keys if not per_key[k][0].is_cuda]
     dev_keys = [k for k in keys if per_key[k][0].is_cuda]
 
-    # ---- host-resident inputs: stage per dtype group, one launch per group --
+    # ---- host-resident inputs: pinned staging -> HBM rows, one launch per dtype --
     if host_keys:
         device = _host_device(args)
         with torch.cuda.device(device):
-            groups: Dict[torch.dtype, List[str]] = OrderedDict()
-            for k in host_keys:
-                dt = per_key[k][0].dtype
-                groups.setdefault(torch.int64 if dt in _INT_TO_I64 else dt, []).append(k)
-            for dt, gkeys in groups.items():
-                st = _stage_host(per_key, gkeys, dt, device)
-                out_dt = torch.float32 if dt == torch.int64 else dt
-                out = torch.empty(_pad(max(st.length, 1)), dtype=out_dt, device=device)
-                if st.length:
-                    w_dev = kn.upload_f64(weights, device) if dt == torch.float64 else kn.upload_f32(weights, device)
-                    d_ptrs = kn.upload_i64(_row_ptrs(st.rows), device)
-                    kn.wsum_ptrs(dt, d_ptrs, w_dev, K, st.length, out, True, acc_mode)
-                results.update(_to_host(out[:st.length], st, {k: per_key[k][0].shape for k in gkeys}))
+            layout = [(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in host_keys]
+            bucket = _cached_bucket(layout, K, device, _ACC_NAME[acc_mode])
+            for i in range(K):
+                bucket.put(i, {k: per_key[k][i] for k in host_keys}, 1)
+            outs = bucket.new_outputs()
+            bucket.reduce_into(outs, weights)
+            results.update(bucket.to_host(outs))
 
     # ---- device-resident inputs: read in place --------------------------------
     if dev_keys:
@@ -244,27 +195,38 @@ def sequential_sum_inplace(dicts: Sequence["OrderedDict"], keys: Sequence[str], 
     (agg_operator.py:55-63, :68-77)."""
     per_key = _gather(dicts, keys)
     K = len(dicts)
+    staged = []
     for k in keys:
         ts = per_key[k]
         t0 = ts[0]
         if t0.numel() == 0:
             continue
-        dt = t0.dtype
-        if dt not in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32):
-            raise TypeError(f"key {k!r}: unsupported dtype {dt} for an unweighted sum")
-        if t0.is_cuda and all(t.is_contiguous() for t in ts):
+        if t0.is_cuda and t0.dtype in _SUM_DTYPES and all(t.is_contiguous() for t in ts):
             device = t0.device
-            with torch.cuda.device(device):
+            with torch.cuda.device(device):  # in place, straight into client 0's tensor
                 ptrs = [t.data_ptr() for t in ts]
-                kn.sum_ptrs(dt, kn.upload_i64(ptrs, device), K, t0.numel(), t0, kn.aligned16(ptrs))
-            continue
-        device = t0.device if t0.is_cuda else _host_device(args)
+                kn.sum_ptrs(t0.dtype, kn.upload_i64(ptrs, device), K, t0.numel(), t0, kn.aligned16(ptrs))
+        else:
+            staged.append(k)
+    if not staged:
+        return
+    # host tensors (and exotic dtypes): rows in HBM, sum into row 0, copy back
+    by_dev: Dict[torch.device, List[str]] = OrderedDict()
+    for k in staged:
+        t0 = per_key[k][0]
+        by_dev.setdefault(t0.device if t0.is_cuda else _host_device(args), []).append(k)
+    for device, dkeys in by_dev.items():
         with torch.cuda.device(device):
-            st = _stage_host({k: ts}, [k], dt, device)
-            d_ptrs = kn.upload_i64(_row_ptrs(st.rows), device)
-            row0 = st.rows[0]
-            kn.sum_ptrs(dt, d_ptrs, K, st.length, row0, True)
-            t0.copy_(row0[:st.length].reshape(t0.shape))
+            bucket = ClientBucket([(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in dkeys], K, device)
+            for i in range(K):
+                bucket.put(i, {k: per_key[k][i] for k in dkeys}, 1)
+            bucket.sync_ingest()
+            for dt, g in bucket.groups.items():
+                if g.length:
+                    kn.sum_ptrs(dt, g.d_ptrs, K, g.length, g.rows[0], True)
+            row0 = bucket.view(0)
+            for k in dkeys:
+                per_key[k][0].copy_(row0[k])  # dtype cast back (integer sums wrap like torch's)
 
 
 def torch_aggregator(args, raw_grad_list, training_num):

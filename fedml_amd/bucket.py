@@ -19,6 +19,8 @@ client rows + 102 MB of result, well inside 288 GB; capacity can grow to about
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -29,6 +31,12 @@ from . import kernels as kn
 from .shapes import Entry
 
 _ROW_ALIGN = 64
+# host threads for packing a client into pinned staging (the GPU box gives a
+# process 16 CPUs; os.cpu_count() reports the whole machine there)
+# (8 threads + 3 staging rows: 54 GB/s ingest = 95 % of the measured pinned
+# H2D rate, tools/ingest_probe.py; 16 threads contend with the DMA reads)
+_PACK_THREADS = int(os.environ.get("FEDAGG_PACK_THREADS", min(8, os.cpu_count() or 1)))
+_STAGES = 3
 
 
 def _pad(n: int) -> int:
@@ -118,6 +126,10 @@ class ClientBucket:
                 g.d_ptrs = kn.upload_i64([g.rows[i].data_ptr() for i in range(capacity)], self.device)
         self.sample_nums: List[Optional[float]] = [None] * capacity
         self._side: Optional[torch.cuda.Stream] = None
+        self._copy: Optional[torch.cuda.Stream] = None
+        self._staging: Dict[torch.dtype, dict] = {}
+        self._result_host: Dict[torch.dtype, torch.Tensor] = {}
+        self._pending = False
 
     # ---- ingest ---------------------------------------------------------------
 
@@ -133,23 +145,82 @@ class ClientBucket:
             out[key] = g.rows[slot, g.offsets[j]:g.offsets[j] + g.numels[j]].view(g.shapes[j])
         return out
 
-    def put(self, slot: int, state_dict, sample_num: float, non_blocking: bool = True) -> None:
+    def put(self, slot: int, state_dict, sample_num: float) -> None:
         """Copy one client's update into its row (FedMLAggregator.
-        add_local_trained_result, fedml_aggregator.py:58-67).  Host tensors
-        travel H2D; pinned host tensors asynchronously."""
+        add_local_trained_result, fedml_aggregator.py:58-67 — the reference
+        moves each tensor to the server device there too).
+
+        Device tensors are copied D2D on the current stream.  Host tensors of a
+        dtype group are packed into a pinned staging row (one host pass) and
+        sent with ONE asynchronous H2D per group on the bucket's copy stream;
+        staging is double-buffered, so packing the next client overlaps this
+        client's PCIe transfer.  The reduction waits for every pending H2D
+        (``sync_ingest``, called by reduce_into)."""
         if not 0 <= slot < self.capacity:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
+        host: Dict[torch.dtype, List[Tuple[int, int, torch.Tensor]]] = {}
         for key, _, _ in self.entries:
             t = state_dict[key]
             g, j = self.where[key]
             if tuple(t.shape) != g.shapes[j]:
                 raise RuntimeError(f"key {key!r}: shape {tuple(t.shape)} != layout {g.shapes[j]}")
-            dst = g.rows[slot, g.offsets[j]:g.offsets[j] + g.numels[j]]
-            src = t.reshape(-1)
-            if src.dtype != g.dtype:
-                src = src.to(g.dtype)
-            dst.copy_(src, non_blocking=non_blocking)
+            if g.numels[j] == 0:
+                continue
+            if t.is_cuda:
+                src = t.reshape(-1)
+                if src.dtype != g.dtype:
+                    src = src.to(g.dtype)
+                g.rows[slot, g.offsets[j]:g.offsets[j] + g.numels[j]].copy_(src, non_blocking=True)
+            else:
+                host.setdefault(g.dtype, []).append((g.offsets[j], g.numels[j], t))
+        for dt, parts in host.items():
+            self._stage(dt, slot, parts)
         self.sample_nums[slot] = sample_num
+
+    def _stage(self, dt: torch.dtype, slot: int, parts) -> None:
+        g = self.groups[dt]
+        if self._copy is None:
+            self._copy = torch.cuda.Stream(self.device)
+            self._copy.wait_stream(torch.cuda.current_stream(self.device))  # rows were zero-filled there
+        st = self._staging.get(dt)
+        if st is None:  # per dtype group: _STAGES pinned rows used round-robin
+            st = self._staging[dt] = {"bufs": [[torch.empty(g.length, dtype=dt).pin_memory(), None]
+                                               for _ in range(_STAGES)], "next": 0}
+        b = st["bufs"][st["next"]]
+        st["next"] = (st["next"] + 1) % _STAGES
+        if b[1] is not None:
+            b[1].synchronize()  # this staging row's previous H2D has landed
+        stage = b[0]
+        lo = min(p[0] for p in parts)
+        hi = max(p[0] + p[1] for p in parts)
+        esz = stage.element_size()
+        keep = []
+        srcs, offs, nbytes = [], [], []
+        for off, n, t in parts:
+            src = t.reshape(-1)
+            if src.dtype != dt or not src.is_contiguous():
+                src = src.to(dt).contiguous()
+                keep.append(src)
+            srcs.append(src.data_ptr())
+            offs.append((off - lo) * esz)
+            nbytes.append(n * esz)
+        n = len(srcs)
+        nat.check(nat.lib().fedagg_host_pack(stage[lo:].data_ptr(), (ctypes.c_void_p * n)(*srcs),
+                                             (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*nbytes), n,
+                                             _PACK_THREADS), "host_pack")
+        del keep
+        with torch.cuda.stream(self._copy):
+            g.rows[slot, lo:hi].copy_(stage[lo:hi], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._copy)
+        b[1] = ev
+        self._pending = True
+
+    def sync_ingest(self) -> None:
+        """Make the current stream wait for every H2D issued by put()."""
+        if self._pending and self._copy is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._copy)
+            self._pending = False
 
     # ---- reduction ------------------------------------------------------------
 
@@ -178,6 +249,7 @@ class ClientBucket:
         if len(weights) != K:
             raise ValueError("one weight per client")
         with torch.cuda.device(self.device):
+            self.sync_ingest()
             cur = torch.cuda.current_stream(self.device)
             w32 = kn.upload_f32(weights, self.device)
             w64 = kn.upload_f64(weights, self.device) if torch.float64 in self.groups else None
@@ -242,3 +314,38 @@ class ClientBucket:
     def num_elements(self) -> int:
         """State-dict elements per client (excluding alignment gaps)."""
         return sum(sum(g.numels) for g in self.groups.values())
+
+    # ---- results to the host ----------------------------------------------------
+
+    def to_host(self, outs: Dict[torch.dtype, torch.Tensor]) -> "OrderedDict[str, torch.Tensor]":
+        """The averaged model as independent host tensors: one D2H per dtype
+        group into pinned memory, then a parallel native scatter into one
+        tensor per key (each key owns its storage, as the reference's results
+        do, so pickling for broadcast sends each key once)."""
+        res = OrderedDict()
+        with torch.cuda.device(self.device):
+            for dt, g in self.groups.items():
+                h = self._result_host.get(dt)
+                if h is None:
+                    h = self._result_host[dt] = torch.empty(max(g.length, 1), dtype=g.out_dtype).pin_memory()
+                h[:g.length].copy_(outs[dt][:g.length])  # synchronous: needed on the host now
+        per_key = {}
+        for dt, g in self.groups.items():
+            h = self._result_host[dt]
+            esz = h.element_size()
+            ts, offs, nbytes = [], [], []
+            for key, off, n, shape in zip(g.keys, g.offsets, g.numels, g.shapes):
+                t = torch.empty(shape, dtype=g.out_dtype)
+                per_key[key] = t
+                if n:
+                    ts.append(t.data_ptr())
+                    offs.append(off * esz)
+                    nbytes.append(n * esz)
+            n = len(ts)
+            if n:
+                nat.check(nat.lib().fedagg_host_unpack(h.data_ptr(), (ctypes.c_void_p * n)(*ts),
+                                                       (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*nbytes),
+                                                       n, _PACK_THREADS), "host_unpack")
+        for key, _, _ in self.entries:
+            res[key] = per_key[key]
+        return res

@@ -36,6 +36,8 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/fedagg.h"
 
@@ -500,6 +502,50 @@ __global__ __launch_bounds__(kBlock) void fedopt_sgd_kernel(float* __restrict__ 
 
 }  // namespace
 
+namespace {
+// Parallel copy of n byte ranges: range i goes from src_base[i] to dst_base[i]
+// (nbytes[i] bytes).  The total is cut into `threads` contiguous slices.
+template <class SrcAt, class DstAt>
+void parallel_ranges(int32_t n, const int64_t* nbytes, int32_t threads, SrcAt src_at, DstAt dst_at) {
+  int64_t total = 0;
+  for (int32_t i = 0; i < n; ++i) total += nbytes[i];
+  if (total == 0) return;
+  int32_t T = threads < 1 ? 1 : threads;
+  if (total < (4ll << 20)) T = 1;  // below ~4 MiB one thread beats spawning
+  auto work = [&](int64_t b0, int64_t b1) {
+    int64_t pos = 0;
+    for (int32_t i = 0; i < n && pos < b1; ++i) {
+      const int64_t lo = pos, hi = pos + nbytes[i];
+      pos = hi;
+      if (hi <= b0) continue;
+      const int64_t a = lo > b0 ? lo : b0, b = hi < b1 ? hi : b1;
+      memcpy(dst_at(i) + (a - lo), src_at(i) + (a - lo), size_t(b - a));
+    }
+  };
+  if (T == 1) {
+    work(0, total);
+    return;
+  }
+  const int64_t per = ((total + T - 1) / T + 4095) & ~int64_t(4095);
+  std::vector<std::thread> pool;
+  pool.reserve(T);
+  for (int32_t t = 0; t < T; ++t) {
+    const int64_t b0 = int64_t(t) * per, b1 = b0 + per < total ? b0 + per : total;
+    if (b0 >= total) break;
+    pool.emplace_back(work, b0, b1);
+  }
+  for (auto& th : pool) th.join();
+}
+
+int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, const int64_t* nbytes,
+                 const char* what) {
+  if (n < 0 || (n > 0 && (!a || !b || !offs || !nbytes))) return set_error(FEDAGG_EINVAL, std::string(what) + ": bad argument");
+  for (int32_t i = 0; i < n; ++i)
+    if (nbytes[i] < 0 || offs[i] < 0) return set_error(FEDAGG_EINVAL, std::string(what) + ": negative size");
+  return FEDAGG_OK;
+}
+}  // namespace
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -617,6 +663,24 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
                        dim3(C::BS), 0, st, s, epi, d_w, K);
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
+}
+
+int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs, const int64_t* nbytes, int32_t n,
+                     int32_t threads) {
+  if (int rc = check_ranges(n, dst, srcs, dst_offs, nbytes, "fedagg_host_pack")) return rc;
+  parallel_ranges(
+      n, nbytes, threads, [&](int32_t i) { return static_cast<const char*>(srcs[i]); },
+      [&](int32_t i) { return static_cast<char*>(dst) + dst_offs[i]; });
+  return FEDAGG_OK;
+}
+
+int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_offs, const int64_t* nbytes, int32_t n,
+                       int32_t threads) {
+  if (int rc = check_ranges(n, src, dsts, src_offs, nbytes, "fedagg_host_unpack")) return rc;
+  parallel_ranges(
+      n, nbytes, threads, [&](int32_t i) { return static_cast<const char*>(src) + src_offs[i]; },
+      [&](int32_t i) { return static_cast<char*>(dsts[i]); });
+  return FEDAGG_OK;
 }
 
 const char* fedagg_last_error(void) { return g_last_error.c_str(); }

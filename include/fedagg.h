@@ -153,6 +153,22 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w,
                                int32_t first_step, uint32_t flags,
                                fedagg_stream_t stream);
 
+/* ---- Host ingest helper -------------------------------------------------- */
+
+/* HOST-side gather of n host buffers into one host buffer (normally pinned
+ * staging for a single H2D per client): srcs[i] (nbytes[i] bytes) goes to
+ * dst + dst_offs[i].  The total is split into `threads` contiguous byte
+ * ranges copied in parallel.  This is the packing step of the ingest path that
+ * replaces the reference's per-key tensor.to(device) at client arrival
+ * (ml_engine_adapter.py:234-254).  Synchronous; touches no device memory. */
+int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs,
+                     const int64_t* nbytes, int32_t n, int32_t threads);
+
+/* The inverse scatter for the broadcast side: src + src_offs[i] goes to
+ * dsts[i] (one host tensor per state-dict key, as the reference returns). */
+int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_offs,
+                       const int64_t* nbytes, int32_t n, int32_t threads);
+
 /* ---- Introspection ------------------------------------------------------ */
 const char* fedagg_last_error(void);
 int32_t fedagg_version(void);

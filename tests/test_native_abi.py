@@ -111,3 +111,49 @@ def test_server_aggregator_surface():
     assert agg.on_after_aggregation(x) is x
     with pytest.raises(NotImplementedError):
         MI355XServerAggregator(m, type("B", (), {"federated_optimizer": "FedAvg", "enable_dp": True})())
+
+
+@pytest.mark.parametrize("threads", [1, 3, 16])
+def test_host_pack_gathers_exactly(lib, threads):
+    """fedagg_host_pack is host code: check it fully on CPU (ragged sizes, gaps,
+    sizes above the threading threshold)."""
+    import ctypes
+
+    import numpy as np
+
+    rng = np.random.default_rng(0)
+    sizes = [0, 1, 7, 4096, 3_000_001, 5, 2_500_000]
+    srcs = [rng.integers(0, 255, s, dtype=np.uint8) for s in sizes]
+    offs, o = [], 0
+    for s in sizes:
+        offs.append(o)
+        o += s + 3  # gaps stay untouched
+    dst = np.full(o, 0xAB, dtype=np.uint8)
+    n = len(sizes)
+    rc = lib.fedagg_host_pack(dst.ctypes.data, (ctypes.c_void_p * n)(*[a.ctypes.data for a in srcs]),
+                              (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*sizes), n, threads)
+    assert rc == 0
+    for a, off in zip(srcs, offs):
+        assert np.array_equal(dst[off:off + a.size], a)
+        assert dst[off + a.size] == 0xAB
+    assert lib.fedagg_host_pack(None, None, None, None, -1, 1) == -1
+
+
+def test_host_unpack_scatters_exactly(lib):
+    import ctypes
+
+    import numpy as np
+
+    rng = np.random.default_rng(1)
+    sizes = [3, 0, 5_000_003, 64, 1]
+    src = rng.integers(0, 255, sum(sizes) + 40, dtype=np.uint8)
+    offs, o = [], 0
+    for s in sizes:
+        offs.append(o)
+        o += s + 8
+    dsts = [np.zeros(s, dtype=np.uint8) for s in sizes]
+    n = len(sizes)
+    assert lib.fedagg_host_unpack(src.ctypes.data, (ctypes.c_void_p * n)(*[d.ctypes.data for d in dsts]),
+                                  (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*sizes), n, 8) == 0
+    for d, off in zip(dsts, offs):
+        assert np.array_equal(d, src[off:off + d.size])
