@@ -40,6 +40,7 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 CONFIGS = {
+    "cfg1": dict(model="lr_mnist", K=4, desc="FedAvg 4 clients x LogisticRegression MNIST (7,850 params) fp32"),
     "cfg2": dict(model="cnn_web", K=32, desc="FedAvg 32 clients x LeNet CNN_WEB (62,006 params) fp32"),
     "cfg3": dict(model="resnet50", K=128,
                  desc="FedAvg 128 clients x ResNet-50 state dict (25,610,152 fp32 + 53 int64) fp32"),
@@ -57,6 +58,12 @@ def parse():
     ap.add_argument("--mode", default="client", choices=["client", "param"],
                     help="multi-GPU partitioning (ignored at 1 GPU)")
     ap.add_argument("--chunks", type=int, default=8, help="client mode: reduce-scatter pipeline depth")
+    ap.add_argument("--acc", default="reference", choices=["reference", "fp32"],
+                    help="bf16/f16 accumulation: torch's per-op chain (bit-exact) or fp32")
+    ap.add_argument("--fedopt", action="store_true",
+                    help="1 GPU: FedOpt server step fused into the reduction (SGD lr=1.0, momentum 0.9; config 5)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-elems", type=int, default=2_600_000)
     return ap.parse_args()
@@ -123,17 +130,33 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     cfg = CONFIGS[a.config]
     entries = shapes.MODELS[cfg["model"]]()
     K = cfg["K"]
     mode = a.mode if world > 1 else "single"
 
-    bucket = ClientBucket(entries, K, dev)
+    server = None
+    if a.fedopt:
+        if world > 1:
+            raise SystemExit("--fedopt is a 1-GPU measurement")
+        from collections import OrderedDict
+
+        from fedml_amd.fedopt import FedOptServer
+
+        init = OrderedDict((k, torch.zeros(s, dtype=d)) for k, s, d in entries)
+        params = [k for k, _, d in entries if d == torch.float32]
+        server = FedOptServer(init, params, K, "sgd", 1.0, 0.9, dev)
+        bucket = server.bucket
+    else:
+        bucket = ClientBucket(entries, K, dev, low_precision_acc=a.acc)
     for gi, (dt, g) in enumerate(bucket.groups.items()):
         fill_rows(g.rows, g.length, seed=1000 * rank + gi, round_idx=3)
     from fedml_amd.synth import sample_nums
@@ -146,7 +169,17 @@ def main():
     n_elems = bucket.num_elements()
 
     # per-step work -------------------------------------------------------------
-    if mode == "single":
+    if server is not None:
+        for i, n in enumerate(ns_local):
+            server.sample_num_dict[i] = n
+
+        def step(ev=None):
+            server.aggregate(events=ev)
+
+        n_launch = 1
+        server.aggregate()  # first step (no momentum read) happens before timing
+        dom_bytes = server.algorithmic_bytes()
+    elif mode == "single":
         outs = bucket.new_outputs()
         w = bucket.weights(ns_local)
 
@@ -236,6 +269,8 @@ def main():
             "clients_total": K * world,
             "elements_per_client": n_elems,
             "layout": "ClientBucket rows [K, L] per dtype, 256-B aligned rows",
+            "low_precision_acc": a.acc,
+            "server_step": "SGD lr=1.0 momentum=0.9 fused" if server is not None else None,
             "parallelism": {"single": "1 GPU", "client": f"client-axis x{world}, RCCL reduce-scatter, "
                                                          f"{a.chunks}-chunk pipeline",
                             "param": f"parameter-axis x{world}, no collective"}[mode],
@@ -247,7 +282,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step",
+            "kernel": ("reduce_kernel<OpF32,SgdEpi> (FedAvg+SGD fused)" if server is not None else
+                       f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step"),
             "alg_bytes_per_step": dom_bytes,
             "kernel_ms_per_step": round(kern_ms, 4),
         },

@@ -79,6 +79,15 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return static_cast<uint16_t>(u >> 16);
 }
 
+// Round an fp32 value to bf16 and back with gfx950's v_cvt_pk_bf16_f32 (RNE
+// under the default float mode; a NaN stays a NaN).  Used for the per-client
+// roundings of the reference chain; the final store uses f32_to_bf16 so a NaN
+// result carries torch's canonical 0x7FC0 pattern.
+__device__ __forceinline__ float bf16_round(float f) {
+  const __bf16 b = static_cast<__bf16>(f);
+  return bf16_to_f32(__builtin_bit_cast(uint16_t, b));
+}
+
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
   _Float16 v;
   __builtin_memcpy(&v, &h, 2);
@@ -106,7 +115,7 @@ struct OpF32 {  // fp32 FedAvg
 
 struct OpBF16Ref {  // bf16, torch CPU chain (round after every op)
   using in_t = uint16_t; using out_t = uint16_t; using acc_t = float; using w_t = float;
-  static __device__ __forceinline__ float r(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+  static __device__ __forceinline__ float r(float f) { return bf16_round(f); }
   static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return r(bf16_to_f32(x) * w); }
   static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return r(a + r(bf16_to_f32(x) * w)); }
   static __device__ __forceinline__ out_t fin(acc_t a) { return f32_to_bf16(a); }
@@ -250,7 +259,9 @@ template <class OP>
 struct StoreEpi {
   typename OP::out_t* out;
   static constexpr int E = 16 / sizeof(typename OP::in_t);
-  __device__ __forceinline__ void pack(int64_t off, const typename OP::acc_t (&acc)[E]) const {
+  struct Pre {};  // nothing to prefetch
+  __device__ __forceinline__ Pre pre(int64_t) const { return {}; }
+  __device__ __forceinline__ void pack(int64_t off, const typename OP::acc_t (&acc)[E], const Pre&) const {
     typename OP::out_t o[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) o[e] = OP::fin(acc[e]);
@@ -269,6 +280,18 @@ struct SgdEpi {
   float neg_lr, m;
   int first;
   static constexpr int E = 4;
+  // p_old and the momentum buffer are independent of the client loop: load
+  // them before it so their latency hides under the stream.
+  struct Pre {
+    Pack<float, 4> p, m;
+  };
+  __device__ __forceinline__ Pre pre(int64_t off) const {
+    Pre r;
+    r.p = load_pack<float, true>(p + off);
+    r.m = {};
+    if (mom && !first) r.m = load_pack<float, true>(mom + off);
+    return r;
+  }
   __device__ __forceinline__ float step1(float po, float avg, float* mb) const {
     const float g = po - avg;
     float b = g;
@@ -281,15 +304,12 @@ struct SgdEpi {
     }
     return __builtin_fmaf(b, neg_lr, po);  // p.add_(buf, alpha=-lr): torch's fused fmadd
   }
-  __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E]) const {
-    auto pv = load_pack<float, false>(p + off);
-    Pack<float, 4> mv = {};
-    if (mom && !first) mv = load_pack<float, false>(mom + off);
+  __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E], const Pre& pr) const {
     float po[E], mo[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      float mb = mv.v[e];
-      po[e] = step1(pv.v[e], acc[e], &mb);
+      float mb = pr.m.v[e];
+      po[e] = step1(pr.p.v[e], acc[e], &mb);
       mo[e] = mb;
     }
     store_pack<float, E>(p + off, po);
@@ -318,7 +338,15 @@ __device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, 
 #pragma unroll
     for (int u = 0; u < SU; ++u) acc = OP::step(acc, x[u], w ? w[c + u] : w_t(0));
   }
-  for (; c < K; ++c) acc = OP::step(acc, s.src[c][e], w ? w[c] : w_t(0));
+  if (c < K) {  // remaining < SU clients: issue every load before the first add
+    typename OP::in_t x[SU - 1];
+#pragma unroll
+    for (int u = 0; u < SU - 1; ++u)
+      if (c + u < K) x[u] = s.src[c + u][e];
+#pragma unroll
+    for (int u = 0; u < SU - 1; ++u)
+      if (c + u < K) acc = OP::step(acc, x[u], w ? w[c + u] : w_t(0));
+  }
   epi.one(e, acc);
 }
 
@@ -337,6 +365,10 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
     int64_t off[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) off[v] = (pack0 + v * BS + t) * E;
+
+    typename EPI::Pre pre[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) pre[v] = epi.pre(off[v]);
 
     typename OP::acc_t acc[V][E];
     {
@@ -367,18 +399,29 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
           for (int e = 0; e < E; ++e) acc[v][e] = OP::step(acc[v][e], x[u][v].v[e], wu);
       }
     }
-    for (; c < K; ++c) {
-      const in_t* p = s.src[c];
-      const w_t wc = w ? w[c] : w_t(0);
+    if constexpr (U > 1) {
+      if (c < K) {  // remaining < U clients (wave-uniform): all loads first, then the adds
+        Pack<in_t, E> x[U - 1][V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        auto x = load_pack<in_t, NT>(p + off[v]);
+        for (int u = 0; u < U - 1; ++u)
+          if (c + u < K) {
+            const in_t* p = s.src[c + u];
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc[v][e] = OP::step(acc[v][e], x.v[e], wc);
+            for (int v = 0; v < V; ++v) x[u][v] = load_pack<in_t, NT>(p + off[v]);
+          }
+#pragma unroll
+        for (int u = 0; u < U - 1; ++u)
+          if (c + u < K) {
+            const w_t wu = w ? w[c + u] : w_t(0);
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+#pragma unroll
+              for (int e = 0; e < E; ++e) acc[v][e] = OP::step(acc[v][e], x[u][v].v[e], wu);
+          }
       }
     }
 #pragma unroll
-    for (int v = 0; v < V; ++v) epi.pack(off[v], acc[v]);
+    for (int v = 0; v < V; ++v) epi.pack(off[v], acc[v], pre[v]);
   } else {
     // ---- edge path: element-wise with bounds ---------------------------------
     const int64_t e0 = pack0 * E;
@@ -417,6 +460,12 @@ __global__ __launch_bounds__(BS) void reduce_multi_kernel(
 // fp32 at 128 x 25.6M on MI355X: U4V4nt 6.44 TB/s vs U8V1nt 6.25 (profiles/r01_tune_variants_s2.json).
 template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; static constexpr bool NT = true; };
 
+// Tensors too small to fill the chip with 4,096-element tiles (configs 1-2,
+// LoRA-sized keys) use 256-element tiles of 64 lanes with 16 clients in flight
+// per lane: ~16x more workgroups and one memory round trip per 16 clients.
+struct SmallCfg { static constexpr int U = 16, V = 1, BS = 64; static constexpr bool NT = true; };
+constexpr int64_t kSmallBelowBlocks = 1024;  // shipped-tile workgroups below which SmallCfg is used
+
 template <class OP>
 int64_t blocks_for(int64_t numel) {
   constexpr int E = 16 / sizeof(typename OP::in_t);
@@ -451,10 +500,14 @@ int launch(const void* const* src, const void* w, int32_t K, int64_t N, void* ou
   if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, std::string(name) + ": K must be >= 1 and N >= 0");
   if (!src || !out || (need_w && !w)) return set_error(FEDAGG_EINVAL, std::string(name) + ": null pointer");
   if (N == 0) return FEDAGG_OK;
-  return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS>(
-      reinterpret_cast<const typename OP::in_t* const*>(src), reinterpret_cast<const typename OP::w_t*>(w), K, N,
-      reinterpret_cast<typename OP::out_t*>(out), (flags & FEDAGG_ALIGNED16) != 0,
-      reinterpret_cast<hipStream_t>(stream), name);
+  auto s = reinterpret_cast<const typename OP::in_t* const*>(src);
+  auto ww = reinterpret_cast<const typename OP::w_t*>(w);
+  auto o = reinterpret_cast<typename OP::out_t*>(out);
+  const bool al = (flags & FEDAGG_ALIGNED16) != 0;
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  if (blocks_for<OP>(N) < kSmallBelowBlocks)
+    return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS>(s, ww, K, N, o, al, st, name);
+  return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS>(s, ww, K, N, o, al, st, name);
 }
 
 // ---------------------------------------------------------------------------

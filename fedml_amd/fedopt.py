@@ -63,6 +63,7 @@ class FedOptServer:
                     self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].copy_(t.detach().reshape(-1))
             self.mom = torch.zeros_like(self.global_flat[torch.float32]) if (f32 and self.momentum) else None
         self.first_step = True
+        self._views: Optional["OrderedDict[str, torch.Tensor]"] = None
         self.runs: List[Tuple[bool, int, int]] = self._runs(f32) if f32 else []
         self.run_ptrs = [kn.upload_i64([f32.rows[i].data_ptr() + lo * 4 for i in range(worker_num)], self.device)
                          for _, lo, _ in self.runs]
@@ -100,13 +101,18 @@ class FedOptServer:
             self.flag_client_model_uploaded_dict[idx] = False
         return True
 
-    def aggregate(self) -> "OrderedDict[str, torch.Tensor]":
+    def aggregate(self, events=None) -> "OrderedDict[str, torch.Tensor]":
+        """events: optional (start, end) torch.cuda.Events recorded around the
+        fp32 launches (the benchmark's kernel timing)."""
         ns = [self.sample_num_dict[i] for i in range(self.worker_num)]
         weights = self.bucket.weights(ns)
         K = self.worker_num
         with torch.cuda.device(self.device):
+            self.bucket.sync_ingest()
             w32 = kn.upload_f32(weights, self.device)
             f32 = self.global_flat.get(torch.float32)
+            if events is not None:
+                events[0].record()
             for (is_param, lo, hi), d_ptrs in zip(self.runs, self.run_ptrs):
                 if is_param:
                     kn.wsum_fedopt_sgd(d_ptrs, w32, K, hi - lo, f32[lo:hi],
@@ -114,6 +120,8 @@ class FedOptServer:
                                        self.lr, self.momentum, self.first_step, True)
                 else:
                     kn.wsum_ptrs(torch.float32, d_ptrs, w32, K, hi - lo, f32[lo:hi], True)
+            if events is not None:
+                events[1].record()
             for dt, g in self.bucket.groups.items():
                 if dt == torch.float32 or g.length == 0:
                     continue
@@ -130,6 +138,10 @@ class FedOptServer:
         return self.get_global_model_params()
 
     def get_global_model_params(self) -> "OrderedDict[str, torch.Tensor]":
+        """Views of the persistent global vectors (built once; they track every
+        later aggregate())."""
+        if self._views is not None:
+            return self._views
         out = OrderedDict()
         for key, shape, _ in self.bucket.entries:
             g, j = self.bucket.where[key]
@@ -137,6 +149,7 @@ class FedOptServer:
                 out[key] = self._int_state[key]
             else:
                 out[key] = self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].view(g.shapes[j])
+        self._views = out
         return out
 
     def algorithmic_bytes(self) -> int:

@@ -88,7 +88,10 @@ class ClientAxisAggregator:
                            for lo, _ in self.bounds]
         elif reducer is None:
             raise ValueError("host rows need a reducer (the HIP kernels read HBM only)")
-        self.comm_stream = torch.cuda.Stream(dev) if self.world > 1 and self.on_gpu else None
+        # gloo has no device collectives: stage through the host (a rehearsal
+        # mode for N ranks sharing one GPU; RCCL is the production backend)
+        self.host_staged = (self.world > 1 and self.on_gpu and dist.get_backend(group) == "gloo")
+        self.comm_stream = torch.cuda.Stream(dev) if self.world > 1 and self.on_gpu and not self.host_staged else None
 
     def owned_ranges(self) -> List[Tuple[int, int]]:
         """Global element ranges this rank owns, in shard order (one per chunk)."""
@@ -115,7 +118,12 @@ class ClientAxisAggregator:
                 kn.wsum_ptrs(self.dtype, self.d_ptrs[c], d_w, self.K, hi - lo, part, True)
             if events is not None:
                 events[c][1].record(cur)
-            if self.world > 1:
+            if self.host_staged:
+                src = self.partial[c * self.chunk_len:(c + 1) * self.chunk_len].cpu()
+                dst = torch.empty(self.piece, dtype=src.dtype)
+                dist.reduce_scatter_tensor(dst, src, op=dist.ReduceOp.SUM, group=self.group)
+                self.shard[c * self.piece:(c + 1) * self.piece].copy_(dst)
+            elif self.world > 1:
                 # chunk c's exchange overlaps chunk c+1's reduction
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):
@@ -128,7 +136,7 @@ class ClientAxisAggregator:
                     self.partial[c * self.chunk_len:(c + 1) * self.chunk_len])
         for w in works:
             w.wait()  # makes the current stream wait for the collective
-        if self.world > 1:
+        if self.comm_stream is not None:
             cur.wait_stream(self.comm_stream)
         return self.shard
 
@@ -146,11 +154,15 @@ class ClientAxisAggregator:
     def gather_full(self) -> torch.Tensor:
         """Reassemble the full [length] result on every rank (all-gather of the
         shards; used by tests and when the model must be replicated)."""
-        parts = [torch.empty_like(self.shard) for _ in range(self.world)]
-        if self.world > 1:
-            dist.all_gather(parts, self.shard, group=self.group)
-        else:
+        if self.world == 1:
             parts = [self.shard]
+        elif self.host_staged:
+            parts = [torch.empty_like(self.shard, device="cpu") for _ in range(self.world)]
+            dist.all_gather(parts, self.shard.cpu(), group=self.group)
+            parts = [p.to(self.shard.device) for p in parts]
+        else:
+            parts = [torch.empty_like(self.shard) for _ in range(self.world)]
+            dist.all_gather(parts, self.shard, group=self.group)
         full = torch.empty(len(self.bounds) * self.chunk_len, dtype=self.shard.dtype, device=self.shard.device)
         for c in range(len(self.bounds)):
             for r in range(self.world):
