@@ -19,6 +19,7 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libfedagg.so")
 
 FEDAGG_ALIGNED16 = 1
+FEDAGG_HOST_WEIGHTS = 2
 FEDAGG_ACC_REFERENCE = 0
 FEDAGG_ACC_FP32 = 1
 

@@ -217,7 +217,8 @@ def sequential_sum_inplace(dicts: Sequence["OrderedDict"], keys: Sequence[str], 
         by_dev.setdefault(t0.device if t0.is_cuda else _host_device(args), []).append(k)
     for device, dkeys in by_dev.items():
         with torch.cuda.device(device):
-            bucket = ClientBucket([(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in dkeys], K, device)
+            bucket = ClientBucket([(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in dkeys], K, device,
+                                  promote_ints=False)  # integer sums stay exact
             for i in range(K):
                 bucket.put(i, {k: per_key[k][i] for k in dkeys}, 1)
             bucket.sync_ingest()

@@ -92,9 +92,15 @@ class ClientBucket:
         device: CUDA device holding the rows.
         low_precision_acc: "reference" (bit-exact with torch's per-op bf16/f16
             rounding) or "fp32" (fp32 accumulate, one final rounding).
+        promote_ints: store integer keys in the float32 rows as fl32(v) at
+            ingest (default).  The reference computes int64 * w as
+            fl32(fl32(v) * fl32(w)) with a float32 result, so this is
+            bit-identical and folds e.g. ResNet's 53 counters into the one fp32
+            launch.  False keeps exact int64 rows (unweighted integer sums).
     """
 
-    def __init__(self, layout, capacity: int, device=None, low_precision_acc: str = "reference"):
+    def __init__(self, layout, capacity: int, device=None, low_precision_acc: str = "reference",
+                 promote_ints: bool = True):
         if capacity < 1:
             raise ValueError("capacity must be >= 1")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -110,9 +116,12 @@ class ClientBucket:
         self.entries = entries
         self.groups: "OrderedDict[torch.dtype, _Group]" = OrderedDict()
         self.where: Dict[str, Tuple[_Group, int]] = {}
+        self.promote_ints = promote_ints
+        self.int_keys = set()
         for key, shape, dt in entries:
-            if dt in (torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool):
-                dt = torch.int64
+            if dt in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool):
+                self.int_keys.add(key)
+                dt = torch.float32 if promote_ints else torch.int64
             if dt not in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64):
                 raise TypeError(f"key {key!r}: unsupported dtype {dt}")
             g = self.groups.get(dt)
@@ -251,8 +260,9 @@ class ClientBucket:
         with torch.cuda.device(self.device):
             self.sync_ingest()
             cur = torch.cuda.current_stream(self.device)
-            w32 = kn.upload_f32(weights, self.device)
-            w64 = kn.upload_f64(weights, self.device) if torch.float64 in self.groups else None
+            # K <= 256: weights ride in the kernel arguments (no H2D per round)
+            w32 = kn.weights_for(weights, torch.float32, self.device)
+            w64 = kn.weights_for(weights, torch.float64, self.device) if torch.float64 in self.groups else None
             # The dominant group runs on the caller's stream; the small ones
             # (e.g. ResNet's 53 int64 counters) on a side stream beside it, so
             # their latency-bound launches stay off the critical path.

@@ -37,6 +37,7 @@
 
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/fedagg.h"
@@ -244,6 +245,21 @@ __device__ __forceinline__ void store_pack(T* p, const T (&v)[E]) {
   }
 }
 
+// Per-client weight sources.  PtrW reads a device array (s_load, wave-uniform);
+// InlW carries up to kInlineK weights by value in the kernel arguments, so a
+// round needs no weight upload at all (FEDAGG_HOST_WEIGHTS).
+template <class T>
+struct PtrW {
+  const T* p;
+  __device__ __forceinline__ T operator[](int i) const { return p ? p[i] : T(0); }
+};
+constexpr int kInlineK = 256;
+template <class T>
+struct InlW {
+  T v[kInlineK];
+  __device__ __forceinline__ T operator[](int i) const { return v[i]; }
+};
+
 // One tensor ("segment") of the reduction: K source pointers and its length.
 template <class OP>
 struct Seg {
@@ -324,19 +340,18 @@ struct SgdEpi {
 
 // Scalar path: one element at a time, identical arithmetic.  Used for the
 // ragged tail of a tensor and for unaligned pointers.
-template <class OP, class EPI>
-__device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, const typename OP::w_t* __restrict__ w,
-                                              int K, int64_t e) {
+template <class OP, class EPI, class WS>
+__device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, const WS& w, int K, int64_t e) {
   using w_t = typename OP::w_t;
   constexpr int SU = 16;  // clients in flight per lane: tiny tensors are latency-bound
-  typename OP::acc_t acc = OP::first(s.src[0][e], w ? w[0] : w_t(0));
+  typename OP::acc_t acc = OP::first(s.src[0][e], w[0]);
   int c = 1;
   for (; c + SU <= K; c += SU) {
     typename OP::in_t x[SU];
 #pragma unroll
     for (int u = 0; u < SU; ++u) x[u] = s.src[c + u][e];
 #pragma unroll
-    for (int u = 0; u < SU; ++u) acc = OP::step(acc, x[u], w ? w[c + u] : w_t(0));
+    for (int u = 0; u < SU; ++u) acc = OP::step(acc, x[u], w[c + u]);
   }
   if (c < K) {  // remaining < SU clients: issue every load before the first add
     typename OP::in_t x[SU - 1];
@@ -345,15 +360,14 @@ __device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, 
       if (c + u < K) x[u] = s.src[c + u][e];
 #pragma unroll
     for (int u = 0; u < SU - 1; ++u)
-      if (c + u < K) acc = OP::step(acc, x[u], w ? w[c + u] : w_t(0));
+      if (c + u < K) acc = OP::step(acc, x[u], w[c + u]);
   }
   epi.one(e, acc);
 }
 
 // Body of one workgroup of BS lanes: packs [pack0, pack0 + BS*V) of segment s.
-template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI>
-__device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
-                                             const typename OP::w_t* __restrict__ w, int K, int64_t pack0) {
+template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI, class WS>
+__device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi, const WS& w, int K, int64_t pack0) {
   using in_t = typename OP::in_t;
   using w_t = typename OP::w_t;
   constexpr int E = 16 / sizeof(in_t);
@@ -373,7 +387,7 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
     typename OP::acc_t acc[V][E];
     {
       const in_t* p = s.src[0];
-      const w_t w0 = w ? w[0] : w_t(0);
+      const w_t w0 = w[0];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         auto x = load_pack<in_t, NT>(p + off[v]);
@@ -392,7 +406,7 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const w_t wu = w ? w[c + u] : w_t(0);
+        const w_t wu = w[c + u];
 #pragma unroll
         for (int v = 0; v < V; ++v)
 #pragma unroll
@@ -412,7 +426,7 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
 #pragma unroll
         for (int u = 0; u < U - 1; ++u)
           if (c + u < K) {
-            const w_t wu = w ? w[c + u] : w_t(0);
+            const w_t wu = w[c + u];
 #pragma unroll
             for (int v = 0; v < V; ++v)
 #pragma unroll
@@ -430,10 +444,19 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi,
   }
 }
 
-template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI = StoreEpi<OP>>
-__global__ __launch_bounds__(BS) void reduce_kernel(Seg<OP> s, EPI epi, const typename OP::w_t* __restrict__ w,
-                                                    int K) {
+template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI = StoreEpi<OP>,
+          class WS = PtrW<typename OP::w_t>>
+__global__ __launch_bounds__(BS) void reduce_kernel(Seg<OP> s, EPI epi, WS w, int K) {
   reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, int64_t(blockIdx.x) * BS * V);
+}
+
+// Grid-stride form: a resident grid walks the tiles, so no partial last wave of
+// workgroups is left running alone at the end.
+template <class OP, int U, int V, bool NT, int BS>
+__global__ __launch_bounds__(BS) void reduce_persistent_kernel(Seg<OP> s, StoreEpi<OP> epi,
+                                                               PtrW<typename OP::w_t> w, int K, int64_t tiles) {
+  for (int64_t b = blockIdx.x; b < tiles; b += gridDim.x)
+    reduce_block<OP, U, V, NT, true, BS>(s, epi, w, K, b * BS * V);
 }
 
 // Multi-tensor form: blockIdx -> (segment, block within segment) by binary
@@ -442,7 +465,8 @@ template <class OP, int U, int V, bool NT, int BS>
 __global__ __launch_bounds__(BS) void reduce_multi_kernel(
     const typename OP::in_t* const* __restrict__ src_tab, typename OP::out_t* const* __restrict__ out_tab,
     const int64_t* __restrict__ numel, const int64_t* __restrict__ block_begin, int T,
-    const typename OP::w_t* __restrict__ w, int K) {
+    const typename OP::w_t* __restrict__ wp, int K) {
+  const PtrW<typename OP::w_t> w{wp};
   const int64_t b = blockIdx.x;
   int lo = 0, hi = T - 1;
   while (lo < hi) {  // largest s with block_begin[s] <= b
@@ -474,9 +498,9 @@ int64_t blocks_for(int64_t numel) {
   return (packs + per - 1) / per;
 }
 
-template <class OP, int U, int V, bool NT, int BS = 256>
-int launch_uvn(const typename OP::in_t* const* src, const typename OP::w_t* w, int32_t K, int64_t N,
-               typename OP::out_t* out, bool aligned, hipStream_t stream, const char* name) {
+template <class OP, int U, int V, bool NT, int BS = 256, class WS = PtrW<typename OP::w_t>>
+int launch_uvn(const typename OP::in_t* const* src, const WS& w, int32_t K, int64_t N, typename OP::out_t* out,
+               bool aligned, hipStream_t stream, const char* name) {
   constexpr int E = 16 / sizeof(typename OP::in_t);
   const int64_t packs = (N + E - 1) / E;
   const int64_t per = int64_t(BS) * V;
@@ -485,13 +509,30 @@ int launch_uvn(const typename OP::in_t* const* src, const typename OP::w_t* w, i
   Seg<OP> s{src, N};
   StoreEpi<OP> epi{out};
   if (aligned) {
-    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, true, BS>), dim3(unsigned(grid)), dim3(BS), 0, stream, s, epi, w,
-                       K);
+    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, true, BS, StoreEpi<OP>, WS>), dim3(unsigned(grid)), dim3(BS), 0,
+                       stream, s, epi, w, K);
   } else {
-    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, false, BS>), dim3(unsigned(grid)), dim3(BS), 0, stream, s, epi,
-                       w, K);
+    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, false, BS, StoreEpi<OP>, WS>), dim3(unsigned(grid)), dim3(BS), 0,
+                       stream, s, epi, w, K);
   }
   return check_launch(name);
+}
+
+template <class OP, class WS>
+int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t N, typename OP::out_t* o, bool al,
+              hipStream_t st, const char* name) {
+  if (blocks_for<OP>(N) < kSmallBelowBlocks)
+    return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
+  return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS, WS>(s, w, K, N, o, al, st, name);
+}
+
+// Weights passed in the kernel arguments (flags & FEDAGG_HOST_WEIGHTS): w is a
+// HOST array of K <= kInlineK values, copied into the launch packet.
+template <class T>
+bool inline_weights(const void* w, int32_t K, InlW<T>* out) {
+  if (K > kInlineK) return false;
+  memcpy(out->v, w, size_t(K) * sizeof(T));
+  return true;
 }
 
 template <class OP>
@@ -501,13 +542,17 @@ int launch(const void* const* src, const void* w, int32_t K, int64_t N, void* ou
   if (!src || !out || (need_w && !w)) return set_error(FEDAGG_EINVAL, std::string(name) + ": null pointer");
   if (N == 0) return FEDAGG_OK;
   auto s = reinterpret_cast<const typename OP::in_t* const*>(src);
-  auto ww = reinterpret_cast<const typename OP::w_t*>(w);
   auto o = reinterpret_cast<typename OP::out_t*>(out);
   const bool al = (flags & FEDAGG_ALIGNED16) != 0;
   auto st = reinterpret_cast<hipStream_t>(stream);
-  if (blocks_for<OP>(N) < kSmallBelowBlocks)
-    return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS>(s, ww, K, N, o, al, st, name);
-  return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS>(s, ww, K, N, o, al, st, name);
+  using w_t = typename OP::w_t;
+  if (w && (flags & FEDAGG_HOST_WEIGHTS)) {
+    InlW<w_t> iw;
+    if (!inline_weights<w_t>(w, K, &iw))
+      return set_error(FEDAGG_EINVAL, std::string(name) + ": FEDAGG_HOST_WEIGHTS needs K <= 256");
+    return launch_ws<OP>(s, iw, K, N, o, al, st, name);
+  }
+  return launch_ws<OP>(s, PtrW<w_t>{reinterpret_cast<const w_t*>(w)}, K, N, o, al, st, name);
 }
 
 // ---------------------------------------------------------------------------
@@ -520,7 +565,19 @@ struct Variant {
 
 template <int U, int V, bool NT, int BS>
 int variant_fn(const float* const* src, const float* w, int32_t K, int64_t N, float* out, hipStream_t st) {
-  return launch_uvn<OpF32, U, V, NT, BS>(src, w, K, N, out, true, st, "fedagg_wsum_f32_variant");
+  return launch_uvn<OpF32, U, V, NT, BS>(src, PtrW<float>{w}, K, N, out, true, st, "fedagg_wsum_f32_variant");
+}
+
+template <int U, int V, int BS, int PER_CU>
+int persistent_fn(const float* const* src, const float* w, int32_t K, int64_t N, float* out, hipStream_t st) {
+  constexpr int E = 4;
+  const int64_t tiles = ((N + E - 1) / E + int64_t(BS) * V - 1) / (int64_t(BS) * V);
+  const int64_t grid = tiles < 256 * PER_CU ? tiles : 256 * PER_CU;
+  Seg<OpF32> s{src, N};
+  StoreEpi<OpF32> epi{out};
+  hipLaunchKernelGGL((reduce_persistent_kernel<OpF32, U, V, true, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, s, epi,
+                     PtrW<float>{w}, K, tiles);
+  return check_launch("persistent");
 }
 
 const Variant kVariants[] = {
@@ -531,6 +588,8 @@ const Variant kVariants[] = {
     {"U4V4nt_b128", variant_fn<4, 4, true, 128>}, {"U4V4nt_b512", variant_fn<4, 4, true, 512>},
     {"U2V4nt_b512", variant_fn<2, 4, true, 512>}, {"U4V2nt_b1024", variant_fn<4, 2, true, 1024>},
     {"U4V4", variant_fn<4, 4, false, 256>},
+    {"U4V4nt_p4", persistent_fn<4, 4, 256, 4>},   {"U4V4nt_p5", persistent_fn<4, 4, 256, 5>},
+    {"U4V4nt_p8", persistent_fn<4, 4, 256, 8>},   {"U4V2nt_p8", persistent_fn<4, 2, 256, 8>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -708,12 +767,23 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
   Seg<OpF32> s{d_src, N};
   SgdEpi epi{d_param, momentum != 0.0f ? d_mom : nullptr, -lr, momentum, first_step};
   auto st = reinterpret_cast<hipStream_t>(stream);
-  if (flags & FEDAGG_ALIGNED16) {
-    hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, SgdEpi>), dim3(unsigned(grid)),
-                       dim3(C::BS), 0, st, s, epi, d_w, K);
+  auto go = [&](const auto& w) {
+    using WS = std::decay_t<decltype(w)>;
+    if (flags & FEDAGG_ALIGNED16) {
+      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, SgdEpi, WS>), dim3(unsigned(grid)),
+                         dim3(C::BS), 0, st, s, epi, w, K);
+    } else {
+      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, SgdEpi, WS>), dim3(unsigned(grid)),
+                         dim3(C::BS), 0, st, s, epi, w, K);
+    }
+  };
+  if (flags & FEDAGG_HOST_WEIGHTS) {
+    InlW<float> iw;
+    if (!inline_weights<float>(d_w, K, &iw))
+      return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
+    go(iw);
   } else {
-    hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, SgdEpi>), dim3(unsigned(grid)),
-                       dim3(C::BS), 0, st, s, epi, d_w, K);
+    go(PtrW<float>{d_w});
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
 }

@@ -54,13 +54,13 @@ class FedOptServer:
         with torch.cuda.device(self.device):
             self.global_flat: Dict[torch.dtype, torch.Tensor] = self.bucket.new_outputs()
             self._int_state: "OrderedDict[str, torch.Tensor]" = OrderedDict()
-            # the global model in the bucket's flat layout (int64 buffers kept as tensors)
+            # the global model in the bucket's flat layout; integer buffers
+            # (num_batches_tracked) also keep their own tensor of their dtype
             for k, t in global_state.items():
                 g, j = self.bucket.where[k]
-                if g.dtype == torch.int64:
-                    self._int_state[k] = t.detach().to(self.device, torch.int64).clone()
-                else:
-                    self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].copy_(t.detach().reshape(-1))
+                self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].copy_(t.detach().reshape(-1))
+                if k in self.bucket.int_keys:
+                    self._int_state[k] = t.detach().to(self.device).clone()
             self.mom = torch.zeros_like(self.global_flat[torch.float32]) if (f32 and self.momentum) else None
         self.first_step = True
         self._views: Optional["OrderedDict[str, torch.Tensor]"] = None
@@ -109,7 +109,7 @@ class FedOptServer:
         K = self.worker_num
         with torch.cuda.device(self.device):
             self.bucket.sync_ingest()
-            w32 = kn.upload_f32(weights, self.device)
+            w32 = kn.weights_for(weights, torch.float32, self.device)  # by value for K <= 256
             f32 = self.global_flat.get(torch.float32)
             if events is not None:
                 events[0].record()
@@ -125,15 +125,12 @@ class FedOptServer:
             for dt, g in self.bucket.groups.items():
                 if dt == torch.float32 or g.length == 0:
                     continue
-                avg = torch.empty(g.length, dtype=g.out_dtype, device=self.device)
-                w = kn.upload_f64(weights, self.device) if dt == torch.float64 else w32
-                kn.wsum_ptrs(dt, g.d_ptrs, w, K, g.length, avg, True)
-                if dt == torch.int64:
-                    for k, j in ((k, self.bucket.where[k][1]) for k in g.keys):
-                        # load_state_dict copy_: float32 -> int64 truncates toward zero
-                        self._int_state[k].reshape(-1).copy_(avg[g.offsets[j]:g.offsets[j] + g.numels[j]])
-                else:
-                    self.global_flat[dt][:g.length].copy_(avg)
+                w = kn.weights_for(weights, dt, self.device)
+                kn.wsum_ptrs(dt, g.d_ptrs, w, K, g.length, self.global_flat[dt], True)
+            for k, t in self._int_state.items():
+                # load_state_dict's copy_: the float32 average truncates toward zero
+                g, j = self.bucket.where[k]
+                t.reshape(-1).copy_(self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]])
         self.first_step = False
         return self.get_global_model_params()
 
@@ -145,7 +142,7 @@ class FedOptServer:
         out = OrderedDict()
         for key, shape, _ in self.bucket.entries:
             g, j = self.bucket.where[key]
-            if g.dtype == torch.int64:
+            if key in self._int_state:
                 out[key] = self._int_state[key]
             else:
                 out[key] = self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].view(g.shapes[j])

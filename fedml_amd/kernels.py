@@ -8,6 +8,7 @@ non-CUDA tensors raise.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Sequence
 
 import torch
@@ -47,6 +48,31 @@ def upload_f64(values: Sequence[float], device: torch.device) -> torch.Tensor:
     return host.to(device, non_blocking=True)
 
 
+INLINE_MAX_K = 256  # FEDAGG_HOST_WEIGHTS limit (include/fedagg.h)
+
+
+class HostWeights:
+    """Weights handed to a launch BY VALUE (kernel arguments): no upload, no
+    device buffer.  Only for K <= INLINE_MAX_K."""
+
+    def __init__(self, values: Sequence[float], dtype: torch.dtype = torch.float32):
+        if len(values) > INLINE_MAX_K:
+            raise ValueError(f"host weights need K <= {INLINE_MAX_K}")
+        ct = ctypes.c_double if dtype == torch.float64 else ctypes.c_float
+        self.buf = (ct * max(1, len(values)))(*[float(v) for v in values])
+
+    def data_ptr(self) -> int:
+        return ctypes.addressof(self.buf)
+
+
+def weights_for(values: Sequence[float], dtype: torch.dtype, device: torch.device):
+    """Kernel-argument weights when K allows, else a device array."""
+    wdt = torch.float64 if dtype == torch.float64 else torch.float32
+    if len(values) <= INLINE_MAX_K:
+        return HostWeights(values, wdt)
+    return upload_f64(values, device) if wdt == torch.float64 else upload_f32(values, device)
+
+
 def aligned16(ptrs: Sequence[int]) -> bool:
     return all((p & 15) == 0 for p in ptrs)
 
@@ -58,6 +84,8 @@ def wsum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, d_w: torch.Tensor, K: in
     lib = nat.lib()
     st = nat.stream_handle()
     flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0
+    if isinstance(d_w, HostWeights):
+        flags |= nat.FEDAGG_HOST_WEIGHTS
     a = (d_ptrs.data_ptr(), d_w.data_ptr(), K, N, out.data_ptr())
     if dtype == torch.float32:
         if out.dtype == torch.float32:
@@ -151,7 +179,7 @@ def wsum_fedopt_sgd(d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int, par
     N elements) goes from p_old to p_new in place, mom is the momentum buffer."""
     _require_cuda(param, "wsum_fedopt_sgd")
     ok = aligned and (param.data_ptr() & 15) == 0 and (mom is None or (mom.data_ptr() & 15) == 0)
+    flags = (nat.FEDAGG_ALIGNED16 if ok else 0) | (nat.FEDAGG_HOST_WEIGHTS if isinstance(d_w, HostWeights) else 0)
     nat.check(nat.lib().fedagg_wsum_fedopt_sgd_f32(
         d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), mom.data_ptr() if mom is not None else None,
-        float(lr), float(momentum), int(first_step), nat.FEDAGG_ALIGNED16 if ok else 0, nat.stream_handle()),
-        "wsum_fedopt_sgd_f32")
+        float(lr), float(momentum), int(first_step), flags, nat.stream_handle()), "wsum_fedopt_sgd_f32")

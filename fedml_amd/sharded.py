@@ -106,7 +106,7 @@ class ClientAxisAggregator:
         if not self.on_gpu:
             return self._aggregate_host(weights)
         cur = torch.cuda.current_stream(self.device)
-        d_w = kn.upload_f32(weights, self.device)
+        d_w = kn.weights_for(weights, torch.float32, self.device)
         works = []
         for c, (lo, hi) in enumerate(self.bounds):
             part = self.partial[c * self.chunk_len: c * self.chunk_len + (hi - lo)]
@@ -204,7 +204,7 @@ class ParamAxisAggregator:
             self.reducer(self.rows[:, :self.length], weights, self.out[:self.length])
             return self.out[:self.length]
         cur = torch.cuda.current_stream(self.device)
-        d_w = kn.upload_f32(weights, self.device)
+        d_w = kn.weights_for(weights, torch.float32, self.device)
         if events is not None:
             events[0][0].record(cur)
         kn.wsum_ptrs(self.rows.dtype, self.d_ptrs, d_w, self.K, self.length, self.out, True)

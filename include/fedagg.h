@@ -47,6 +47,9 @@ typedef void* fedagg_stream_t;
 #define FEDAGG_ENOKERNEL (-2)   /* no kernel for this configuration */
 
 #define FEDAGG_ALIGNED16 1u     /* flags: all pointers 16-byte aligned */
+#define FEDAGG_HOST_WEIGHTS 2u  /* flags: d_w is a HOST array of K <= 256 weights,
+                                   passed by value in the kernel arguments (no
+                                   upload; the one exception to "device pointers") */
 
 /* bf16 / f16 accumulation modes (see fedagg_wsum_bf16) */
 #define FEDAGG_ACC_REFERENCE 0  /* round to bf16/f16 after every mul and add, as torch CPU does */

@@ -211,3 +211,40 @@ def test_client_axis_single_rank_kernel_path(dtype, cuda_device):
     else:
         exp = orc.wsum([cpu_rows[i] for i in range(K)], ws)
     gu.assert_same(full, exp, f"client-axis {dtype}")
+
+
+@pytest.mark.parametrize("K", [1, 7, 256, 257])
+def test_kernel_argument_weights_match_device_weights(K, cuda_device):
+    """FEDAGG_HOST_WEIGHTS (weights by value in the launch, K <= 256) and the
+    device-array path give identical bits; K = 257 falls back to the array."""
+    N = 70_001
+    g = torch.Generator(device=cuda_device).manual_seed(K)
+    rows = torch.randn(K, (N + 63) // 64 * 64, generator=g, device=cuda_device)
+    ws = [float(i + 1) for i in range(K)]
+    ws = [w / sum(ws) for w in ws]
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    a = torch.empty(N, device=cuda_device)
+    b = torch.empty(N, device=cuda_device)
+    kn.wsum_ptrs(torch.float32, d_ptrs, kn.upload_f32(ws, cuda_device), K, N, a, True)
+    hw = kn.weights_for(ws, torch.float32, cuda_device)
+    assert isinstance(hw, kn.HostWeights) == (K <= 256)
+    kn.wsum_ptrs(torch.float32, d_ptrs, hw, K, N, b, True)
+    gu.assert_same(a.cpu(), b.cpu(), f"K={K}")
+    exp = orc.wsum([rows[i, :N].cpu() for i in range(K)], ws)
+    gu.assert_same(b.cpu(), exp, f"K={K} vs oracle")
+
+
+@pytest.mark.parametrize("name", ["resnet_mini_k5", "resnet_mini_bigint_k3", "mixed_dtypes_k4"])
+def test_bucket_device_inputs_int_promotion(name, cuda_device):
+    """Integer keys ride in the fp32 rows as fl32(v) (converted on the GPU at
+    ingest): bit-identical to the reference's int64 * w, also for |v| > 2^24."""
+    meta, arrays = gu.load(name)
+    raw = _to_device(cases.build_inputs(meta["spec"]), cuda_device)
+    bucket = ClientBucket(raw[0][1], len(raw), cuda_device)
+    assert all(k in bucket.int_keys for k, t in raw[0][1].items() if not t.is_floating_point())
+    assert torch.int64 not in bucket.groups
+    for i, (n, d) in enumerate(raw):
+        bucket.put(i, d, n)
+    res = bucket.aggregate()
+    for k, e in gu.expected_groups(meta, arrays)[0].items():
+        gu.assert_same(res[k].cpu(), e, f"{name}[{k}]")

@@ -57,6 +57,18 @@ def main() -> None:
     names = [lib.fedagg_variant_name(v).decode() for v in range(nv)]
     times = {nm: [] for nm in names}
     times["copy"] = []
+    probe = None
+    try:  # pure-read ceiling over the SAME 13 GB of rows, same process (tools/hbm_probe.hip)
+        import ctypes
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+        import hbm_probe
+        probe = ctypes.CDLL(hbm_probe.build())
+        probe.probe_read_launch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_void_p]
+        probe_out = torch.empty(8192 * 256, device=dev)
+        times["read_probe"] = []
+    except Exception as e:  # noqa: BLE001
+        print("probe unavailable:", e)
     src_copy = bucket.view(-1)[: 8 * row].clone()
     dst_copy = torch.empty_like(src_copy)
     bytes_alg = (K + 1) * N * 4
@@ -88,10 +100,16 @@ def main() -> None:
         ev1.record()
         ev1.synchronize()
         times["copy"].append(ev0.elapsed_time(ev1))
+        if probe is not None:
+            ev0.record()
+            probe.probe_read_launch(bucket.data_ptr(), bucket.numel() // 4, probe_out.data_ptr(), 8192, 8, st)
+            ev1.record()
+            ev1.synchronize()
+            times["read_probe"].append(ev0.elapsed_time(ev1))
     res = {}
     for nm, ts in times.items():
         med = statistics.median(ts)
-        b = bytes_alg if nm != "copy" else 2 * src_copy.numel() * 4
+        b = {"copy": 2 * src_copy.numel() * 4, "read_probe": bucket.numel() * 4}.get(nm, bytes_alg)
         res[nm] = {"median_ms": round(med, 4), "min_ms": round(min(ts), 4),
                    "GBps_median": round(b / med / 1e6, 1), "frac_8TBps": round(b / med / 1e6 / 8000, 4)}
         print(f"{nm:10s} median {med:8.4f} ms  min {min(ts):8.4f} ms  {b / med / 1e6:8.1f} GB/s  "
