@@ -28,7 +28,7 @@ import torch
 
 from . import _native as nat
 from . import kernels as kn
-from .shapes import Entry
+from .layout import RowLayout
 
 _ROW_ALIGN = 64
 # host threads for packing a client into pinned staging (the GPU box gives a
@@ -41,45 +41,6 @@ _STAGES = 3
 
 def _pad(n: int) -> int:
     return (n + _ROW_ALIGN - 1) // _ROW_ALIGN * _ROW_ALIGN
-
-
-def _numel(shape) -> int:
-    n = 1
-    for s in shape:
-        n *= int(s)
-    return n
-
-
-class _Group:
-    """Keys of one storage dtype packed into one row layout."""
-
-    def __init__(self, dtype: torch.dtype, out_dtype: torch.dtype):
-        self.dtype = dtype
-        self.out_dtype = out_dtype
-        self.keys: List[str] = []
-        self.shapes: List[Tuple[int, ...]] = []
-        self.offsets: List[int] = []
-        self.numels: List[int] = []
-        self.length = 0
-        self.rows: Optional[torch.Tensor] = None
-        self.d_ptrs: Optional[torch.Tensor] = None
-
-    def add(self, key: str, shape) -> None:
-        # every key starts 16-byte aligned, so any run of keys can be reduced
-        # on the vector path (gaps are a few elements per key, zero-filled)
-        align = max(1, 16 // torch.empty((), dtype=self.dtype).element_size())
-        start = (self.length + align - 1) // align * align
-        n = _numel(shape)
-        self.keys.append(key)
-        self.shapes.append(tuple(shape))
-        self.offsets.append(start)
-        self.numels.append(n)
-        self.length = start + n
-
-
-def _out_dtype(dt: torch.dtype) -> torch.dtype:
-    # int64 * python float -> float32 (torch type promotion), floats keep theirs
-    return torch.float32 if dt == torch.int64 else dt
 
 
 class ClientBucket:
@@ -108,27 +69,12 @@ class ClientBucket:
             raise nat.FedAggNativeError("ClientBucket lives in HBM; give a CUDA device")
         self.capacity = capacity
         self.acc_mode = {"reference": kn.ACC_REFERENCE, "fp32": kn.ACC_FP32}[low_precision_acc]
-        entries: List[Entry]
-        if isinstance(layout, dict):
-            entries = [(k, tuple(t.shape), t.dtype) for k, t in layout.items()]
-        else:
-            entries = [(k, tuple(s), d) for k, s, d in layout]
-        self.entries = entries
-        self.groups: "OrderedDict[torch.dtype, _Group]" = OrderedDict()
-        self.where: Dict[str, Tuple[_Group, int]] = {}
+        self.layout = RowLayout(layout, promote_ints)
+        self.entries = self.layout.entries
+        self.groups = self.layout.groups
+        self.where = self.layout.where
+        self.int_keys = self.layout.int_keys
         self.promote_ints = promote_ints
-        self.int_keys = set()
-        for key, shape, dt in entries:
-            if dt in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool):
-                self.int_keys.add(key)
-                dt = torch.float32 if promote_ints else torch.int64
-            if dt not in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64):
-                raise TypeError(f"key {key!r}: unsupported dtype {dt}")
-            g = self.groups.get(dt)
-            if g is None:
-                g = self.groups[dt] = _Group(dt, _out_dtype(dt))
-            self.where[key] = (g, len(g.keys))
-            g.add(key, shape)
         with torch.cuda.device(self.device):
             for g in self.groups.values():
                 g.rows = torch.zeros((capacity, _pad(max(g.length, 1))), dtype=g.dtype, device=self.device)
@@ -184,6 +130,27 @@ class ClientBucket:
                 host.setdefault(g.dtype, []).append((g.offsets[j], g.numels[j], t))
         for dt, parts in host.items():
             self._stage(dt, slot, parts)
+        self.sample_nums[slot] = sample_num
+
+    def put_encoded(self, slot: int, message) -> None:
+        """Ingest a FAGG wire message (fedml_amd.wire): its payload already IS
+        this bucket's row image, so each dtype group is ONE host->device copy
+        straight from the message buffer (asynchronous when the transport
+        received it into pinned memory; the runtime stages pageable memory
+        itself at ~PCIe rate).  No per-key host work at all."""
+        from . import wire
+
+        if not 0 <= slot < self.capacity:
+            raise IndexError(f"slot {slot} outside [0, {self.capacity})")
+        sample_num, regions = wire.row_regions(message, self.layout)
+        if self._copy is None:
+            self._copy = torch.cuda.Stream(self.device)
+            self._copy.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._copy):
+            for dt, host in regions:
+                if host is not None:
+                    self.groups[dt].rows[slot, :host.numel()].copy_(host, non_blocking=True)
+        self._pending = True
         self.sample_nums[slot] = sample_num
 
     def _stage(self, dt: torch.dtype, slot: int, parts) -> None:
@@ -327,11 +294,17 @@ class ClientBucket:
 
     # ---- results to the host ----------------------------------------------------
 
-    def to_host(self, outs: Dict[torch.dtype, torch.Tensor]) -> "OrderedDict[str, torch.Tensor]":
+    def to_host(self, outs: Dict[torch.dtype, torch.Tensor], into: Optional[Dict[str, torch.Tensor]] = None
+                ) -> "OrderedDict[str, torch.Tensor]":
         """The averaged model as independent host tensors: one D2H per dtype
         group into pinned memory, then a parallel native scatter into one
         tensor per key (each key owns its storage, as the reference's results
-        do, so pickling for broadcast sends each key once)."""
+        do, so pickling for broadcast sends each key once).
+
+        into: existing contiguous host tensors of the result dtypes (e.g. the
+        server model's state_dict, which the reference fills with
+        load_state_dict right after aggregating) to write instead of
+        allocating: fresh host pages cost a first-touch fault each."""
         res = OrderedDict()
         with torch.cuda.device(self.device):
             for dt, g in self.groups.items():
@@ -345,7 +318,10 @@ class ClientBucket:
             esz = h.element_size()
             ts, offs, nbytes = [], [], []
             for key, off, n, shape in zip(g.keys, g.offsets, g.numels, g.shapes):
-                t = torch.empty(shape, dtype=g.out_dtype)
+                t = into.get(key) if into is not None else None
+                if t is None or t.dtype != g.out_dtype or not t.is_contiguous() or t.is_cuda \
+                        or tuple(t.shape) != tuple(shape):
+                    t = torch.empty(shape, dtype=g.out_dtype)
                 per_key[key] = t
                 if n:
                     ts.append(t.data_ptr())

@@ -248,3 +248,28 @@ def test_bucket_device_inputs_int_promotion(name, cuda_device):
     res = bucket.aggregate()
     for k, e in gu.expected_groups(meta, arrays)[0].items():
         gu.assert_same(res[k].cpu(), e, f"{name}[{k}]")
+
+
+@pytest.mark.parametrize("name", ["cfg2_cnn_web_k32", "resnet_mini_bigint_k3", "mixed_dtypes_k4", "ragged_f32_k17"])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_put_encoded_matches_reference(name, pinned, cuda_device):
+    """FAGG messages (fedml_amd.wire) ingested with one H2D per dtype group,
+    from pageable or pinned receive buffers, aggregate to the reference bits."""
+    from fedml_amd import wire
+
+    meta, arrays = gu.load(name)
+    raw = cases.build_inputs(meta["spec"])
+    bucket = ClientBucket(raw[0][1], len(raw), cuda_device)
+    msgs = []
+    for n, d in raw:
+        m = wire.encode(d, n)
+        if pinned:
+            t = torch.empty(len(m), dtype=torch.uint8).pin_memory()
+            t.numpy()[:] = np.frombuffer(m, dtype=np.uint8)
+            m = t.numpy()
+        msgs.append(m)
+    for i, m in enumerate(msgs):
+        bucket.put_encoded(i, m)
+    res = bucket.aggregate()
+    for k, e in gu.expected_groups(meta, arrays)[0].items():
+        gu.assert_same(res[k].cpu(), e, f"{name}[{k}]")

@@ -137,6 +137,31 @@ def main():
     res["e2e_ingest_plus_round_end_s"] = t2 - t0
     assert list(host.keys()) == [e[0] for e in entries]
 
+    # round-end breakdown (after every put has been issued)
+    bd = {}
+    for i, (n, d) in enumerate(raw):
+        bucket.put(i, d, n)
+    t0 = time.perf_counter()
+    bucket.sync_ingest()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    bucket.reduce_into(outs, bucket.weights([n for n, _ in raw]))
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    host = bucket.to_host(outs)
+    t3 = time.perf_counter()
+    host2 = bucket.to_host(outs, into=host)  # into existing tensors (model.load_state_dict analogue)
+    t4 = time.perf_counter()
+    pinned_only = bucket._result_host[torch.float32]
+    t5 = time.perf_counter()
+    pinned_only.copy_(outs[torch.float32][:pinned_only.numel()])
+    t6 = time.perf_counter()
+    bd.update(drain_pending_h2d_ms=(t1 - t0) * 1e3, reduce_ms=(t2 - t1) * 1e3,
+              to_host_fresh_tensors_ms=(t3 - t2) * 1e3, to_host_into_existing_ms=(t4 - t3) * 1e3,
+              d2h_only_ms=(t6 - t5) * 1e3)
+    assert all(host2[k] is host[k] for k in host)
+    res["round_end_breakdown"] = bd
+
     # the reference's call shape
     args = type("Args", (), {"federated_optimizer": "FedAvg"})()
     times = []
