@@ -162,6 +162,31 @@ def main():
     assert all(host2[k] is host[k] for k in host)
     res["round_end_breakdown"] = bd
 
+    # FAGG wire messages: ingest straight from the receive buffers
+    from fedml_amd import wire
+
+    msgs = [wire.encode(d, n) for n, d in raw]
+    pinned_msgs = []
+    for m in msgs[:32]:
+        t = torch.empty(len(m), dtype=torch.uint8).pin_memory()
+        t.numpy()[:] = memoryview(m)
+        pinned_msgs.append(t)
+    wb = {}
+    for label, ms in (("pageable", msgs), ("pinned", [t.numpy() for t in pinned_msgs])):
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i, m in enumerate(ms):
+                bucket.put_encoded(i, m)
+            bucket.sync_ingest()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+        wb[f"put_encoded_{label}_GBps"] = sum(len(m) for m in ms) / dt / 1e9
+    t0 = time.perf_counter()
+    _ = [wire.encode(d, n) for n, d in raw[:16]]
+    wb["encode_GBps_client_side"] = sum(len(m) for m in msgs[:16]) / (time.perf_counter() - t0) / 1e9
+    res["wire"] = wb
+
     # the reference's call shape
     args = type("Args", (), {"federated_optimizer": "FedAvg"})()
     times = []
