@@ -594,6 +594,76 @@ const Variant kVariants[] = {
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // ---------------------------------------------------------------------------
+// Coordinate-wise median (the reference's "wise_median" defense:
+// core/security/defense/coordinate_wise_median_defense.py:24-32, i.e.
+// torch.median(stack, dim=-1).values: the LOWER median, element (K-1)/2 of the
+// sorted column; any NaN in the column makes the result that NaN).
+//
+// One lane per parameter element holds the column's K values in registers
+// (KMAX >= K slots).  The column is padded with -inf / +inf so that its lower
+// median always lands at the network's fixed middle slot (KMAX-1)/2; a
+// Batcher odd-even merge sorting network is then fully unrolled at compile
+// time, and since only that one output slot is used, the compiler deletes
+// every comparator that does not feed it.  Loads are 4 B per lane (256 B per
+// wave instruction), all K of them independent and in flight together.
+
+__device__ __forceinline__ void cmpx(float& a, float& b) {
+  const float lo = fminf(a, b), hi = fmaxf(a, b);
+  a = lo;
+  b = hi;
+}
+
+template <int N>
+__device__ __forceinline__ void oem_sort(float (&a)[N]) {
+#pragma unroll
+  for (int p = 1; p < N; p += p)
+#pragma unroll
+    for (int k = p; k > 0; k /= 2)
+#pragma unroll
+      for (int j = k % p; j + k < N; j += k + k)
+#pragma unroll
+        for (int i = 0; i < k; ++i)
+          if (i + j + k < N && (i + j) / (p + p) == (i + j + k) / (p + p)) cmpx(a[i + j], a[i + j + k]);
+}
+
+template <int KMAX, int BS>
+__global__ __launch_bounds__(BS) void median_kernel(const float* const* __restrict__ src, int K, int64_t N,
+                                                    float* __restrict__ out) {
+  const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;
+  if (e >= N) return;
+  const int below = (KMAX - 1) / 2 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
+  float v[KMAX];
+#pragma unroll
+  for (int c = 0; c < KMAX; ++c) {
+    if (c < K) {
+      v[c] = __builtin_nontemporal_load(src[c] + e);
+    } else {
+      v[c] = (c - K < below) ? -__builtin_huge_valf() : __builtin_huge_valf();
+    }
+  }
+  // torch returns the first NaN of the column (client order) if there is one
+  float nan_v = 0.f;
+  bool has_nan = false;
+#pragma unroll
+  for (int c = 0; c < KMAX; ++c) {
+    const bool n = (c < K) && __builtin_isnan(v[c]);
+    nan_v = (n && !has_nan) ? v[c] : nan_v;
+    has_nan = has_nan || n;
+  }
+  oem_sort<KMAX>(v);
+  out[e] = has_nan ? nan_v : v[(KMAX - 1) / 2];
+}
+
+template <int KMAX>
+int launch_median(const float* const* src, int K, int64_t N, float* out, hipStream_t st) {
+  constexpr int BS = 256;
+  const int64_t grid = (N + BS - 1) / BS;
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N too large");
+  hipLaunchKernelGGL((median_kernel<KMAX, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
+  return check_launch("fedagg_median_f32");
+}
+
+// ---------------------------------------------------------------------------
 // FedOpt SGD(+momentum) epilogue.
 
 __global__ __launch_bounds__(kBlock) void fedopt_sgd_kernel(float* __restrict__ p, float* __restrict__ mom,
@@ -786,6 +856,21 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
     go(PtrW<float>{d_w});
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
+}
+
+int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_out, uint32_t flags,
+                      fedagg_stream_t stream) {
+  (void)flags;
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K must be >= 1 and N >= 0");
+  if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  if (K <= 8) return launch_median<8>(d_src, K, N, d_out, st);
+  if (K <= 16) return launch_median<16>(d_src, K, N, d_out, st);
+  if (K <= 32) return launch_median<32>(d_src, K, N, d_out, st);
+  if (K <= 64) return launch_median<64>(d_src, K, N, d_out, st);
+  if (K <= 128) return launch_median<128>(d_src, K, N, d_out, st);
+  return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K > 128 clients is not supported yet");
 }
 
 int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs, const int64_t* nbytes, int32_t n,

@@ -6,11 +6,15 @@ aggregate -> on_after_aggregation) and the default subclass of
 python/fedml/ml/aggregator/default_aggregator.py:12-23.
 
 ``aggregate`` routes to fedml_amd.agg_operator.FedMLAggOperator.agg, the GPU
-implementation of the reference's operator.  The reference's optional hooks
-(FHE, differential privacy, attacks, defenses, contribution assessment) are
-outside this build's scope: with them disabled (FedML's default) the hooks are
-the identity, exactly as in the reference; enabling one raises
-NotImplementedError instead of silently aggregating without it.
+implementation of the reference's operator.  Two of FedML's defenses are
+reductions over the client axis and run on the GPU too (fedml_amd.defense):
+``defense_type`` "wise_median" (on aggregation) and "trimmed_mean" (before
+aggregation), dispatched exactly as FedMLDefender does
+(core/security/fedml_defender.py:131-171).  The other optional hooks (FHE,
+differential privacy, attacks, other defenses, contribution assessment) are
+outside this build's scope: disabled (FedML's default) they are the identity,
+as in the reference; enabling one raises NotImplementedError instead of
+silently aggregating without it.
 
 INTEGRATION.md shows the two-line subclass a FedML maintainer adds to route
 FedML's own ServerAggregator through this operator.
@@ -21,9 +25,10 @@ from abc import ABC, abstractmethod
 from collections import OrderedDict
 from typing import List, Tuple
 
+from . import defense as dfn
 from .agg_operator import FedMLAggOperator
 
-_UNSUPPORTED_FLAGS = ("enable_fhe", "enable_dp", "enable_defense", "enable_attack", "enable_contribution")
+_UNSUPPORTED_FLAGS = ("enable_fhe", "enable_dp", "enable_attack", "enable_contribution")
 
 
 def _check_flags(args) -> None:
@@ -32,6 +37,16 @@ def _check_flags(args) -> None:
             raise NotImplementedError(
                 f"args.{flag} is set: FedML's {flag[7:]} hooks are not part of fedml_amd; "
                 "use FedML's own ServerAggregator for that round")
+    if getattr(args, "enable_defense", False):
+        dt = str(getattr(args, "defense_type", "")).strip()
+        if dt not in dfn.SUPPORTED:
+            raise NotImplementedError(f"defense_type {dt!r}: fedml_amd runs {dfn.SUPPORTED} on the GPU")
+
+
+def _defense(args):
+    if not getattr(args, "enable_defense", False):
+        return None
+    return str(args.defense_type).strip()
 
 
 class ServerAggregator(ABC):
@@ -60,12 +75,19 @@ class ServerAggregator(ABC):
         pass
 
     def on_before_aggregation(self, raw_client_model_or_grad_list: List[Tuple[float, OrderedDict]]):
-        """server_aggregator.py:44-73 with FHE/DP/attack/defense disabled."""
+        """server_aggregator.py:44-73 (FHE/DP/attacks disabled); the trimmed-mean
+        defense filters the list here (fedml_defender.py:134-161)."""
         client_idxs = [i for i in range(len(raw_client_model_or_grad_list))]
-        return raw_client_model_or_grad_list, client_idxs
+        if _defense(self.args) == dfn.DEFENSE_TRIMMED_MEAN:
+            raw_client_model_or_grad_list = dfn.trimmed_mean_before_aggregation(
+                raw_client_model_or_grad_list, self.args.beta)
+        return raw_client_model_or_grad_list, client_idxs  # no client is flagged malicious
 
     def aggregate(self, raw_client_model_or_grad_list: List[Tuple[float, OrderedDict]]):
-        """server_aggregator.py:75-88: FedMLAggOperator.agg(self.args, list)."""
+        """server_aggregator.py:75-88: the median defense replaces the operator
+        (fedml_defender.py:163-174), otherwise FedMLAggOperator.agg."""
+        if _defense(self.args) == dfn.DEFENSE_WISE_MEDIAN:
+            return dfn.coordinate_wise_median(raw_client_model_or_grad_list, getattr(self.args, "fedagg_device", None))
         return FedMLAggOperator.agg(self.args, raw_client_model_or_grad_list)
 
     def on_after_aggregation(self, aggregated_model_or_grad: OrderedDict) -> OrderedDict:

@@ -156,6 +156,17 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w,
                                int32_t first_step, uint32_t flags,
                                fedagg_stream_t stream);
 
+/* ---- Robust aggregation --------------------------------------------------- */
+
+/* Coordinate-wise median over K fp32 clients (the "wise_median" defense,
+ * core/security/defense/coordinate_wise_median_defense.py:24-32:
+ * torch.median(stack, dim=-1).values): out[e] = the LOWER median (sorted
+ * element (K-1)/2) of {src_i[e]}; if the column holds a NaN, the first NaN in
+ * client order.  K <= 128.  Where +0.0 and -0.0 tie at the median the sign of
+ * the zero returned may differ from torch's (nth_element order). */
+int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N,
+                      float* d_out, uint32_t flags, fedagg_stream_t stream);
+
 /* ---- Host ingest helper -------------------------------------------------- */
 
 /* HOST-side gather of n host buffers into one host buffer (normally pinned

@@ -300,3 +300,64 @@ def fedopt_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: Seque
         else:
             out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)
     return out
+
+
+# --------------------------------------------------------------------------
+# Robust aggregation (core/security/defense)
+
+
+def _is_weight_param(k: str) -> bool:
+    """core/security/common/utils.py:16-21."""
+    return "running_mean" not in k and "running_var" not in k and "num_batches_tracked" not in k
+
+
+def lower_median_cols(stack: np.ndarray) -> np.ndarray:
+    """torch.median(x, dim=-1).values for x = stack.T ([M, K] -> [M]): element
+    (K-1)//2 of each sorted column; a column with a NaN yields its first NaN
+    (ATen's median: find_if(isnan) before nth_element)."""
+    K = stack.shape[0]
+    srt = np.sort(stack, axis=0)  # NaNs sort last; they are overridden below
+    med = srt[(K - 1) // 2].astype(stack.dtype)
+    isn = np.isnan(stack)
+    anyn = isn.any(axis=0)
+    if anyn.any():
+        first = np.argmax(isn, axis=0)
+        med[anyn] = stack[first[anyn], np.nonzero(anyn)[0]]
+    return med
+
+
+def coordinate_wise_median(raw_grad_list):
+    """CoordinateWiseMedianDefense.defend_on_aggregation
+    (coordinate_wise_median_defense.py:18-44), including its walk over ALL of
+    client 0's keys (misaligned for models with BN buffers -> RuntimeError)."""
+    vecs = []
+    for n, params in raw_grad_list:
+        parts = [to_np(v).ravel() for k, v in params.items() if _is_weight_param(k)]
+        if not parts:
+            raise RuntimeError("torch.cat(): expected a non-empty list of Tensors")
+        vecs.append(np.concatenate([p.astype(np.float32) for p in parts]))
+    med = torch.from_numpy(lower_median_cols(np.stack(vecs)))
+    index = 0
+    (num0, averaged_params) = raw_grad_list[0]
+    for k, params in list(averaged_params.items()):
+        averaged_params[k] = med[index:index + params.numel()].view(params.size())
+        index += params.numel()
+    return averaged_params
+
+
+def trimmed_mean(model_list, trimmed_num):
+    """common/utils.py:213-228 (scores are the sample counts; stable sort)."""
+    temp = sorted([(n, g, n) for n, g in model_list], key=lambda t: t[2])
+    temp = temp[trimmed_num: len(model_list) - trimmed_num]
+    return [(t[0], t[1]) for t in temp]
+
+
+def defended_agg(args, raw_grad_list):
+    """FedMLDefender flow for the two reduction defenses (fedml_defender.py:131-171)."""
+    if args.defense_type == "wise_median":
+        return coordinate_wise_median(raw_grad_list)
+    if args.defense_type == "trimmed_mean":
+        if args.beta > 1 / 2 or args.beta < 0:
+            raise ValueError("the bound of beta is [0, 1/2)")
+        return agg(args, trimmed_mean(raw_grad_list, int(args.beta * len(raw_grad_list))))
+    raise NotImplementedError(args.defense_type)

@@ -191,3 +191,36 @@ def spec_json(spec) -> str:
 
 def clone_raw(raw):
     return copy.deepcopy(raw)
+
+
+# Robust aggregation (core/security/defense): run through the reference's own
+# CoordinateWiseMedianDefense / CoordinateWiseTrimmedMeanDefense (+ FedAvg).
+DEFENSE_CASES: List[Dict[str, Any]] = []
+
+
+def _def(name, defense, K, keys, seed, **kw):
+    DEFENSE_CASES.append(dict(name=name, defense=defense, optimizer="FedAvg", K=K, keys=keys, seed=seed, **kw))
+
+
+for _k in (1, 2, 3, 4, 5, 8, 32):
+    _def(f"median_cnn_web_k{_k}", "wise_median", _k, _model_keys("cnn_web"), seed=100 + _k)
+for _k in (17, 64, 100, 128):
+    _def(f"median_ragged_k{_k}", "wise_median", _k, [k for k in RAGGED_F32 if k[0] != "e"], seed=120 + _k)
+_def("median_specials_k5", "wise_median", 5, [["x", [64], F32]], seed=130, specials=True)
+_def("median_specials_k8", "wise_median", 8, [["x", [64], F32]], seed=131, specials=True)
+_def("median_resnet_mini_k3", "wise_median", 3, RESNET_MINI, seed=132, expect_error=True)  # misaligned walk
+_def("trimmed_k10_b01", "trimmed_mean", 10, RESNET_MINI, seed=140, beta=0.1,
+     sample_nums=[50, 10, 10, 70, 30, 90, 20, 60, 40, 80])
+_def("trimmed_k10_b02_ties", "trimmed_mean", 10, RAGGED_F32[:4], seed=141, beta=0.2,
+     sample_nums=[5, 5, 1, 9, 9, 5, 2, 9, 1, 5])
+_def("trimmed_k7_b0", "trimmed_mean", 7, RAGGED_F32[:4], seed=142, beta=0.0)
+_def("trimmed_bad_beta", "trimmed_mean", 4, RAGGED_F32[:2], seed=143, beta=0.6, expect_error=True)
+
+
+class DefenseArgs(Args):
+    def __init__(self, spec):
+        super().__init__(spec)
+        self.enable_defense = True
+        self.defense_type = spec["defense"]
+        if "beta" in spec:
+            self.beta = spec["beta"]

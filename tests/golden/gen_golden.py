@@ -52,6 +52,18 @@ def import_reference():
     return FedMLAggOperator, FedOptAggregator
 
 
+def import_defenses():
+    for name, path in [("fedml.core.security", f"{REF}/core/security"),
+                       ("fedml.core.security.defense", f"{REF}/core/security/defense"),
+                       ("fedml.core.security.common", f"{REF}/core/security/common")]:
+        m = types.ModuleType(name)
+        m.__path__ = [path]
+        sys.modules[name] = m
+    from fedml.core.security.defense.coordinate_wise_median_defense import CoordinateWiseMedianDefense
+    from fedml.core.security.defense.coordinate_wise_trimmed_mean_defense import CoordinateWiseTrimmedMeanDefense
+    return CoordinateWiseMedianDefense, CoordinateWiseTrimmedMeanDefense
+
+
 def tensor_bytes(t: torch.Tensor) -> np.ndarray:
     t = t.detach().cpu().contiguous()
     if t.dtype == torch.bfloat16:
@@ -68,7 +80,7 @@ def save(name: str, meta: dict, arrays: dict) -> None:
     np.savez_compressed(os.path.join(OUT_DIR, f"{name}.npz"), meta=np.array(json.dumps(meta)), **payload)
 
 
-def run_agg_case(FedMLAggOperator, spec):
+def run_agg_case(FedMLAggOperator, spec, aggregate=None):
     raw = cases.build_inputs(spec)
     sha = fingerprint(raw)
     client0_before = OrderedDict((k, t.clone()) for k, t in raw[0][1].items())
@@ -76,7 +88,7 @@ def run_agg_case(FedMLAggOperator, spec):
     meta = {"spec": spec, "in_sha256": sha, "error": None}
     arrays = {}
     try:
-        res = FedMLAggOperator.agg(cases.Args(spec), raw)
+        res = aggregate(raw) if aggregate is not None else FedMLAggOperator.agg(cases.Args(spec), raw)
     except Exception as e:  # the reference's own error behaviour is part of the contract
         meta["error"] = type(e).__name__
         save(spec["name"], meta, arrays)
@@ -150,6 +162,19 @@ def main():
         print("wrote", spec["name"])
     for spec in cases.FEDOPT_CASES:
         run_fedopt_case(FedOptAggregator, spec)
+        print("wrote", spec["name"])
+    Median, Trimmed = import_defenses()
+    for spec in cases.DEFENSE_CASES:
+        args = cases.DefenseArgs(spec)
+        if spec["defense"] == "wise_median":
+            # FedMLDefender.defend_on_aggregation -> CoordinateWiseMedianDefense (fedml_defender.py:163-171)
+            def agg(raw, args=args):
+                return Median(args).defend_on_aggregation(raw, FedMLAggOperator.agg, None)
+        else:
+            # defend_before_aggregation -> trimmed list, then the base FedAvg operator
+            def agg(raw, args=args):
+                return FedMLAggOperator.agg(args, Trimmed(args).defend_before_aggregation(raw, None))
+        run_agg_case(FedMLAggOperator, spec, aggregate=agg)
         print("wrote", spec["name"])
 
 

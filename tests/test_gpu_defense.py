@@ -1,0 +1,85 @@
+"""GPU parity of the robust-aggregation defenses against the reference's own
+CoordinateWiseMedianDefense / CoordinateWiseTrimmedMeanDefense (golden)."""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+import cases
+import golden_util as gu
+from fedml_amd import defense as dfn
+from fedml_amd import kernels as kn
+from fedml_amd.server_aggregator import MI355XServerAggregator
+from oracle import fedavg_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(spec, raw):
+    args = cases.DefenseArgs(spec)
+    agg = MI355XServerAggregator(torch.nn.Linear(1, 1), args)
+    lst, idxs = agg.on_before_aggregation(raw)
+    assert idxs == list(range(len(raw)))
+    return agg.on_after_aggregation(agg.aggregate(lst))
+
+
+@pytest.mark.parametrize("device_inputs", [False, True])
+@pytest.mark.parametrize("name", [c["name"] for c in cases.DEFENSE_CASES])
+def test_defense_matches_reference(name, device_inputs, cuda_device):
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw = cases.build_inputs(spec)
+    if device_inputs:
+        raw = [(n, OrderedDict((k, t.to(cuda_device)) for k, t in d.items())) for n, d in raw]
+    if meta["error"]:
+        with pytest.raises(Exception) as ei:
+            _run(spec, raw)
+        assert type(ei.value).__name__ == meta["error"]
+        return
+    res = _run(spec, raw)
+    for t in res.values():
+        assert t.is_cuda == device_inputs
+    gu.assert_groups(OrderedDict((k, t.cpu()) for k, t in res.items()), meta, arrays, name)
+
+
+@pytest.mark.parametrize("K", [1, 2, 7, 8, 9, 16, 33, 64, 65, 100, 127, 128])
+def test_median_kernel_vs_oracle(K, cuda_device):
+    """Every KMAX bucket and padding split, with duplicates and infinities."""
+    N = 20_011
+    g = torch.Generator(device=cuda_device).manual_seed(K)
+    rows = torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125
+    rows[:, :7] = float("inf")
+    rows[:, 7:9] = -float("inf")
+    rows[K // 2, 100:110] = float("nan")
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, device=cuda_device)
+    dfn.median_f32(d_ptrs, K, N, out)
+    exp = orc.lower_median_cols(rows.cpu().numpy())
+    gu.assert_same(out.cpu(), torch.from_numpy(exp), f"median K={K}")
+
+
+def test_median_headline_shape_sampled(cuda_device):
+    """128 clients x 25.6M fp32: 200,000 random columns vs the oracle."""
+    K, N = 128, 25_610_152
+    g = torch.Generator(device=cuda_device).manual_seed(3)
+    rows = torch.empty((K, (N + 63) // 64 * 64), device=cuda_device)
+    for i in range(K):
+        rows[i].normal_(0.0, 0.05, generator=g)
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, device=cuda_device)
+    dfn.median_f32(d_ptrs, K, N, out)
+    idx = torch.randint(0, N, (200_000,), generator=torch.Generator().manual_seed(2)).to(cuda_device)
+    exp = orc.lower_median_cols(rows[:, idx].cpu().numpy())
+    gu.assert_same(out[idx].cpu(), torch.from_numpy(exp), "median headline")
+
+
+def test_median_rejects_too_many_clients(cuda_device):
+    from fedml_amd import _native as nat
+
+    rows = torch.zeros(129, 64, device=cuda_device)
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(129)], cuda_device)
+    with pytest.raises(nat.FedAggNativeError):
+        dfn.median_f32(d_ptrs, 129, 64, torch.empty(64, device=cuda_device))
