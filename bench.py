@@ -62,6 +62,8 @@ def parse():
                     help="bf16/f16 accumulation: torch's per-op chain (bit-exact) or fp32")
     ap.add_argument("--fedopt", action="store_true",
                     help="1 GPU: FedOpt server step fused into the reduction (SGD lr=1.0, momentum 0.9; config 5)")
+    ap.add_argument("--op", default="fedavg", choices=["fedavg", "median"],
+                    help="1 GPU: the reduction measured (median = the wise_median defense kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -179,6 +181,21 @@ def main():
         n_launch = 1
         server.aggregate()  # first step (no momentum read) happens before timing
         dom_bytes = server.algorithmic_bytes()
+    elif a.op == "median":
+        from fedml_amd import defense as dfn
+
+        gd = bucket.groups[dom_dt]
+        med_out = torch.empty(gd.padded, dtype=torch.float32, device=dev)
+
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record()
+            dfn.median_f32(gd.d_ptrs, K, gd.length, med_out)
+            if ev is not None:
+                ev[1].record()
+
+        n_launch = 1
+        dom_bytes = K * gd.length * 4 + gd.length * 4
     elif mode == "single":
         outs = bucket.new_outputs()
         w = bucket.weights(ns_local)
@@ -282,7 +299,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": ("reduce_kernel<OpF32,SgdEpi> (FedAvg+SGD fused)" if server is not None else
+            "kernel": ("median_kernel<128>" if a.op == "median" else
+                       "reduce_kernel<OpF32,SgdEpi> (FedAvg+SGD fused)" if server is not None else
                        f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step"),
             "alg_bytes_per_step": dom_bytes,
             "kernel_ms_per_step": round(kern_ms, 4),

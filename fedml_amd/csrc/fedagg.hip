@@ -203,6 +203,42 @@ struct OpSumI32 {
   static __device__ __forceinline__ out_t fin(acc_t a) { return static_cast<int32_t>(a); }
 };
 
+// Secure aggregation over a finite field (LightSecAgg, core/mpc/lightsecagg.py).
+// numpy int64 semantics: adds wrap, np.mod is a floor modulo (sign of p).
+__device__ __forceinline__ int64_t floor_mod(int64_t a, int64_t p) {
+  int64_t r = a % p;
+  if (r != 0 && ((r < 0) != (p < 0))) r += p;
+  return r;
+}
+__device__ __forceinline__ int64_t wrap_add(int64_t a, int64_t b) {
+  return static_cast<int64_t>(static_cast<uint64_t>(a) + static_cast<uint64_t>(b));
+}
+
+// aggregate_models_in_finite (:134-148): w = x_0 ; w = (w + x_i) mod p.  The
+// "weight" operand carries p.  Field elements (0 <= a, b < p) take the
+// conditional-subtract path; anything else the exact 64-bit floor modulo.
+struct OpSumModI64 {
+  using in_t = int64_t; using out_t = int64_t; using acc_t = int64_t; using w_t = int64_t;
+  static __device__ __forceinline__ acc_t first(in_t x, w_t) { return x; }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t p) {
+    if (p > 0 && static_cast<uint64_t>(a) < static_cast<uint64_t>(p) &&
+        static_cast<uint64_t>(x) < static_cast<uint64_t>(p) && p <= (int64_t(1) << 62)) {
+      const int64_t s2 = a + x;
+      return s2 >= p ? s2 - p : s2;
+    }
+    return floor_mod(wrap_add(a, x), p);
+  }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return a; }
+};
+
+// Plain wrapping int64 sum (the first half of aggregate_model_reconstruction).
+struct OpWrapSumI64 {
+  using in_t = int64_t; using out_t = int64_t; using acc_t = int64_t; using w_t = int64_t;
+  static __device__ __forceinline__ acc_t first(in_t x, w_t) { return x; }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t) { return wrap_add(a, x); }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return a; }
+};
+
 // ---------------------------------------------------------------------------
 // 16-byte packs.
 
@@ -252,6 +288,11 @@ template <class T>
 struct PtrW {
   const T* p;
   __device__ __forceinline__ T operator[](int i) const { return p ? p[i] : T(0); }
+};
+template <class T>
+struct ConstW {  // one value for every client (the field prime of the mod-p sum)
+  T v;
+  __device__ __forceinline__ T operator[](int) const { return v; }
 };
 constexpr int kInlineK = 256;
 template <class T>
@@ -336,6 +377,39 @@ struct SgdEpi {
     p[e] = step1(p[e], a, &mb);
     if (mom) mom[e] = mb;
   }
+};
+
+// LightSecAgg model reconstruction epilogue
+// (cross_silo/lightsecagg/lsa_fedml_aggregator.py:139-166 with
+// core/mpc/lightsecagg.py:157-182): on the wrapping int64 client sum
+//   m = (sum - mask) mod p ; v = m > (p-1)/2 ? m - p : m   (my_q_inv, float64)
+//   out = fl32( fl32(v / 2^q) * fl32(w) )   (torch.Tensor(...) then * (1/K))
+struct LsaEpi {
+  const int64_t* mask;
+  float* out;
+  int64_t p;
+  double inv_scale;  // 2^-q (exact)
+  float w;
+  static constexpr int E = 2;
+  struct Pre {
+    Pack<int64_t, 2> m;
+  };
+  __device__ __forceinline__ Pre pre(int64_t off) const { return {load_pack<int64_t, true>(mask + off)}; }
+  __device__ __forceinline__ float one_value(int64_t acc, int64_t mk) const {
+    const int64_t m = floor_mod(wrap_add(acc, -mk), p);
+    // flag = X_q - (p-1)/2 > 0, computed by numpy in float64
+    const double xq = static_cast<double>(m);
+    const double v = (xq - (static_cast<double>(p) - 1.0) / 2.0 > 0.0) ? xq - static_cast<double>(p) : xq;
+    const float f = static_cast<float>(v * inv_scale);  // exact scale, then RNE to fp32
+    return f * w;
+  }
+  __device__ __forceinline__ void pack(int64_t off, const int64_t (&acc)[E], const Pre& pr) const {
+    float o[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) o[e] = one_value(acc[e], pr.m.v[e]);
+    store_pack<float, E>(out + off, o);
+  }
+  __device__ __forceinline__ void one(int64_t e, int64_t acc) const { out[e] = one_value(acc, mask[e]); }
 };
 
 // Scalar path: one element at a time, identical arithmetic.  Used for the
@@ -524,6 +598,33 @@ int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t
   if (blocks_for<OP>(N) < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
   return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS, WS>(s, w, K, N, o, al, st, name);
+}
+
+// Any epilogue / weight source, shipped or small-tensor tiles by size.
+template <class OP, class EPI, class WS, int U, int V, bool NT, int BS>
+int launch_epi_cfg(const Seg<OP>& s, const EPI& epi, const WS& w, int32_t K, bool aligned, hipStream_t st,
+                   const char* name) {
+  constexpr int E = 16 / sizeof(typename OP::in_t);
+  const int64_t grid = ((s.numel + E - 1) / E + int64_t(BS) * V - 1) / (int64_t(BS) * V);
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, std::string(name) + ": N too large");
+  if (aligned) {
+    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, true, BS, EPI, WS>), dim3(unsigned(grid)), dim3(BS), 0, st, s, epi,
+                       w, K);
+  } else {
+    hipLaunchKernelGGL((reduce_kernel<OP, U, V, NT, false, BS, EPI, WS>), dim3(unsigned(grid)), dim3(BS), 0, st, s,
+                       epi, w, K);
+  }
+  return check_launch(name);
+}
+
+template <class OP, class EPI, class WS>
+int launch_epi(const Seg<OP>& s, const EPI& epi, const WS& w, int32_t K, bool aligned, hipStream_t st,
+               const char* name) {
+  if (blocks_for<OP>(s.numel) < kSmallBelowBlocks)
+    return launch_epi_cfg<OP, EPI, WS, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS>(s, epi, w, K, aligned,
+                                                                                            st, name);
+  return launch_epi_cfg<OP, EPI, WS, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS>(s, epi, w, K, aligned, st,
+                                                                                      name);
 }
 
 // Weights passed in the kernel arguments (flags & FEDAGG_HOST_WEIGHTS): w is a
@@ -856,6 +957,31 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
     go(PtrW<float>{d_w});
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
+}
+
+int fedagg_sum_mod_i64(const int64_t* const* d_src, int32_t K, int64_t N, int64_t p, int64_t* d_out,
+                       uint32_t flags, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_sum_mod_i64: K must be >= 1 and N >= 0");
+  if (p <= 0) return set_error(FEDAGG_EINVAL, "fedagg_sum_mod_i64: the prime must be positive");
+  if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_sum_mod_i64: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  Seg<OpSumModI64> s{d_src, N};
+  return launch_epi<OpSumModI64>(s, StoreEpi<OpSumModI64>{d_out}, ConstW<int64_t>{p}, K,
+                                 (flags & FEDAGG_ALIGNED16) != 0, reinterpret_cast<hipStream_t>(stream),
+                                 "fedagg_sum_mod_i64");
+}
+
+int fedagg_lsa_reconstruct_f32(const int64_t* const* d_src, int32_t K, int64_t N, const int64_t* d_mask, int64_t p,
+                               int32_t q_bits, float w, float* d_out, uint32_t flags, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_lsa_reconstruct_f32: K must be >= 1 and N >= 0");
+  if (p <= 0 || q_bits < 0 || q_bits > 62)
+    return set_error(FEDAGG_EINVAL, "fedagg_lsa_reconstruct_f32: need p > 0 and 0 <= q_bits <= 62");
+  if (!d_src || !d_mask || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_lsa_reconstruct_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  Seg<OpWrapSumI64> s{d_src, N};
+  LsaEpi epi{d_mask, d_out, p, ldexp(1.0, -q_bits), w};
+  return launch_epi<OpWrapSumI64>(s, epi, ConstW<int64_t>{0}, K, (flags & FEDAGG_ALIGNED16) != 0,
+                                  reinterpret_cast<hipStream_t>(stream), "fedagg_lsa_reconstruct_f32");
 }
 
 int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_out, uint32_t flags,

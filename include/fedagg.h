@@ -167,6 +167,27 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w,
 int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N,
                       float* d_out, uint32_t flags, fedagg_stream_t stream);
 
+/* Secure aggregation in a finite field (LightSecAgg), numpy int64 semantics:
+ * wrapping adds, floor modulo.  p > 0.
+ *
+ * fedagg_sum_mod_i64 replaces aggregate_models_in_finite
+ * (core/mpc/lightsecagg.py:134-148): out = x_0; out = (out + x_i) mod p.
+ *
+ * fedagg_lsa_reconstruct_f32 replaces the per-key loop of
+ * LightSecAggAggregator.aggregate_model_reconstruction
+ * (cross_silo/lightsecagg/lsa_fedml_aggregator.py:139-166) with
+ * transform_finite_to_tensor / my_q_inv (lightsecagg.py:157-182):
+ *   m = (Σ_i x_i − mask) mod p;  v = m > (p−1)/2 ? m − p : m  (float64);
+ *   out = fl32( fl32(v / 2^q_bits) · w )   with w = fl32(1 / K_active).
+ * d_mask is the decoded aggregate mask laid out like the client rows. */
+int fedagg_sum_mod_i64(const int64_t* const* d_src, int32_t K, int64_t N,
+                       int64_t p, int64_t* d_out, uint32_t flags,
+                       fedagg_stream_t stream);
+int fedagg_lsa_reconstruct_f32(const int64_t* const* d_src, int32_t K, int64_t N,
+                               const int64_t* d_mask, int64_t p, int32_t q_bits,
+                               float w, float* d_out, uint32_t flags,
+                               fedagg_stream_t stream);
+
 /* ---- Host ingest helper -------------------------------------------------- */
 
 /* HOST-side gather of n host buffers into one host buffer (normally pinned

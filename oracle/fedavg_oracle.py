@@ -361,3 +361,41 @@ def defended_agg(args, raw_grad_list):
             raise ValueError("the bound of beta is [0, 1/2)")
         return agg(args, trimmed_mean(raw_grad_list, int(args.beta * len(raw_grad_list))))
     raise NotImplementedError(args.defense_type)
+
+
+# --------------------------------------------------------------------------
+# LightSecAgg field arithmetic
+
+
+def finite_sum(weights_finite, p):
+    """core/mpc/lightsecagg.py:134-148: w = x_0 ; w = (w + x_i) mod p (numpy
+    int64: wrapping add, floor modulo)."""
+    out = OrderedDict((k, np.array(v, dtype=np.int64, copy=True)) for k, v in weights_finite[0].items())
+    for k in out:
+        for d in weights_finite[1:]:
+            with np.errstate(over="ignore"):
+                out[k] = np.mod(out[k] + d[k], p)
+    return out
+
+
+def lsa_reconstruct(dicts, mask, p, q_bits):
+    """lsa_fedml_aggregator.py:139-166 with lightsecagg.py:157-182 given the
+    decoded aggregate mask (d, 1)."""
+    out = OrderedDict()
+    pos = 0
+    K = len(dicts)
+    for k in dicts[0]:
+        s = np.array(dicts[0][k], dtype=np.int64, copy=True)
+        for d in dicts[1:]:
+            with np.errstate(over="ignore"):
+                s = s + d[k]
+        n = s.size
+        with np.errstate(over="ignore"):
+            s = s - np.asarray(mask).reshape(-1)[pos:pos + n].reshape(s.shape)
+        pos += n
+        xq = np.mod(s, p)
+        v = np.where(xq.astype(np.float64) - (p - 1) / 2 > 0, xq.astype(np.float64) - float(p),
+                     xq.astype(np.float64)) / float(2 ** q_bits)
+        t = torch.from_numpy(np.asarray(v, dtype=np.float64).astype(np.float32).reshape(v.shape if v.ndim else (1,)))
+        out[k] = t * (1 / K)
+    return out

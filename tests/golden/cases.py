@@ -224,3 +224,36 @@ class DefenseArgs(Args):
         self.defense_type = spec["defense"]
         if "beta" in spec:
             self.beta = spec["beta"]
+
+
+# LightSecAgg field arithmetic (core/mpc/lightsecagg.py, cross_silo/lightsecagg)
+SECAGG_KEYS = [[k, s, I64] for k, s, _ in RESNET_MINI]
+SECAGG_CASES: List[Dict[str, Any]] = [
+    dict(name="lsa_finite_sum_k1", kind="finite_sum", K=1, p=32749, seed=200),
+    dict(name="lsa_finite_sum_k5", kind="finite_sum", K=5, p=32749, seed=201),
+    dict(name="lsa_finite_sum_k16", kind="finite_sum", K=16, p=2 ** 31 - 1, seed=202),
+    dict(name="lsa_finite_sum_wild_k4", kind="finite_sum", K=4, p=32749, seed=203, wild=True),
+    dict(name="lsa_reconstruct_k2", kind="reconstruct", K=2, p=32749, q=10, seed=210),
+    dict(name="lsa_reconstruct_k5", kind="reconstruct", K=5, p=32749, q=10, seed=211),
+    dict(name="lsa_reconstruct_k16_big", kind="reconstruct", K=16, p=2 ** 31 - 1, q=16, seed=212),
+]
+
+
+def secagg_inputs(spec):
+    """(list of K OrderedDicts of int64 numpy arrays, aggregate_mask (d, 1))."""
+    import numpy as np
+
+    rng = np.random.default_rng(spec["seed"])
+    p = spec["p"]
+    dicts = []
+    for _ in range(spec["K"]):
+        d = OrderedDict()
+        for k, s, _ in SECAGG_KEYS:
+            if spec.get("wild"):
+                d[k] = rng.integers(-3 * p, 3 * p, size=s, dtype=np.int64)
+            else:
+                d[k] = rng.integers(0, p, size=s, dtype=np.int64)
+        dicts.append(d)
+    dim = sum(int(np.prod(s)) for _, s, _ in SECAGG_KEYS)
+    mask = rng.integers(0, p, size=(dim, 1), dtype=np.int64)
+    return dicts, mask

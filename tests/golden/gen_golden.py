@@ -155,6 +155,41 @@ def run_fedopt_case(FedOptAggregator, spec):
     save(spec["name"], meta, arrays)
 
 
+def run_secagg_case(spec):
+    """The reference's own aggregate_models_in_finite / aggregate_model_reconstruction."""
+    for name, path in [("fedml.core.mpc", f"{REF}/core/mpc"), ("fedml.cross_silo", f"{REF}/cross_silo"),
+                       ("fedml.cross_silo.lightsecagg", f"{REF}/cross_silo/lightsecagg")]:
+        m = types.ModuleType(name)
+        m.__path__ = [path]
+        sys.modules.setdefault(name, m)
+    sys.modules.setdefault("fedml.mlops", types.ModuleType("fedml.mlops"))
+    sys.modules["fedml"].mlops = sys.modules["fedml.mlops"]
+    from fedml.core.mpc.lightsecagg import aggregate_models_in_finite, model_dimension
+    from fedml.cross_silo.lightsecagg.lsa_fedml_aggregator import LightSecAggAggregator
+
+    dicts, mask = cases.secagg_inputs(spec)
+    meta = {"spec": spec, "error": None, "tuple": False}
+    arrays = {}
+    if spec["kind"] == "finite_sum":
+        out = aggregate_models_in_finite(dicts, spec["p"])
+        res = OrderedDict((k, torch.from_numpy(np.asarray(v))) for k, v in out.items())
+    else:
+        agg = object.__new__(LightSecAggAggregator)
+        agg.model_dict = {i: d for i, d in enumerate(dicts)}
+        agg.dimensions, _ = model_dimension(OrderedDict((k, torch.from_numpy(v)) for k, v in dicts[0].items()))
+        agg.prime_number = spec["p"]
+        agg.precision_parameter = spec["q"]
+        agg.aggregate_mask_reconstruction = lambda active: mask
+        agg.set_global_model_params = lambda params: None
+        res = agg.aggregate_model_reconstruction(list(range(spec["K"])), list(range(spec["K"])))
+    meta["outputs"] = []
+    for k, t in res.items():
+        arrays[f"o0:{k}"] = tensor_bytes(t)
+        meta["outputs"].append({"group": 0, "key": k, "dtype": str(t.dtype).replace("torch.", ""),
+                                "shape": list(t.shape), "is_client0_tensor": False})
+    save(spec["name"], meta, arrays)
+
+
 def main():
     FedMLAggOperator, FedOptAggregator = import_reference()
     for spec in cases.CASES:
@@ -175,6 +210,9 @@ def main():
             def agg(raw, args=args):
                 return FedMLAggOperator.agg(args, Trimmed(args).defend_before_aggregation(raw, None))
         run_agg_case(FedMLAggOperator, spec, aggregate=agg)
+        print("wrote", spec["name"])
+    for spec in cases.SECAGG_CASES:
+        run_secagg_case(spec)
         print("wrote", spec["name"])
 
 
