@@ -247,13 +247,24 @@ struct alignas(16) Pack {
   T v[E];
 };
 
+// Client rows arrive through pointer tables, which hipcc cannot prove are
+// global memory: without the cast it issues FLAT loads, which also count on
+// lgkmcnt and so get waited for together with the scalar loads of the next
+// client pointers.  All device pointers here are global (hipMalloc / torch).
+template <class T>
+__device__ __forceinline__ const T __attribute__((address_space(1)))* as_global(const T* p) {
+  return (const T __attribute__((address_space(1)))*)(p);
+}
+
 template <class T, bool NT>
 __device__ __forceinline__ Pack<T, 16 / sizeof(T)> load_pack(const T* p) {
+  typedef const u32x4 __attribute__((address_space(1)))* gvec;
+  const gvec g = (gvec)(p);
   u32x4 r;
   if constexpr (NT) {
-    r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    r = __builtin_nontemporal_load(g);
   } else {
-    r = *reinterpret_cast<const u32x4*>(p);
+    r = *g;
   }
   Pack<T, 16 / sizeof(T)> o;
   __builtin_memcpy(&o, &r, 16);
@@ -416,14 +427,13 @@ struct LsaEpi {
 // ragged tail of a tensor and for unaligned pointers.
 template <class OP, class EPI, class WS>
 __device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, const WS& w, int K, int64_t e) {
-  using w_t = typename OP::w_t;
   constexpr int SU = 16;  // clients in flight per lane: tiny tensors are latency-bound
-  typename OP::acc_t acc = OP::first(s.src[0][e], w[0]);
+  typename OP::acc_t acc = OP::first(as_global(s.src[0])[e], w[0]);
   int c = 1;
   for (; c + SU <= K; c += SU) {
     typename OP::in_t x[SU];
 #pragma unroll
-    for (int u = 0; u < SU; ++u) x[u] = s.src[c + u][e];
+    for (int u = 0; u < SU; ++u) x[u] = as_global(s.src[c + u])[e];
 #pragma unroll
     for (int u = 0; u < SU; ++u) acc = OP::step(acc, x[u], w[c + u]);
   }
@@ -431,7 +441,7 @@ __device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, 
     typename OP::in_t x[SU - 1];
 #pragma unroll
     for (int u = 0; u < SU - 1; ++u)
-      if (c + u < K) x[u] = s.src[c + u][e];
+      if (c + u < K) x[u] = as_global(s.src[c + u])[e];
 #pragma unroll
     for (int u = 0; u < SU - 1; ++u)
       if (c + u < K) acc = OP::step(acc, x[u], w[c + u]);
@@ -735,13 +745,9 @@ __global__ __launch_bounds__(BS) void median_kernel(const float* const* __restri
   const int below = (KMAX - 1) / 2 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
   float v[KMAX];
 #pragma unroll
-  for (int c = 0; c < KMAX; ++c) {
-    if (c < K) {
-      v[c] = __builtin_nontemporal_load(src[c] + e);
-    } else {
-      v[c] = (c - K < below) ? -__builtin_huge_valf() : __builtin_huge_valf();
-    }
-  }
+  for (int c = 0; c < KMAX; ++c)
+    v[c] = (c < K) ? __builtin_nontemporal_load(as_global(src[c]) + e)
+                   : ((c - K < below) ? -__builtin_huge_valf() : __builtin_huge_valf());
   // torch returns the first NaN of the column (client order) if there is one
   float nan_v = 0.f;
   bool has_nan = false;
