@@ -215,6 +215,8 @@ def main():
         def step(ev=None):
             for dt, agg in aggs.items():
                 agg.aggregate(w, events=ev if dt == dom_dt else None)
+                if dt in (torch.bfloat16, torch.float16):
+                    agg.shard_in_model_dtype()  # the one rounding of a 16-bit model, after the exchange
 
         n_launch = len(aggs[dom_dt].bounds)
         gd = bucket.groups[dom_dt]

@@ -36,6 +36,7 @@ SIGNATURES = {
     "fedagg_wsum_bf16": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _I32, _U32, _P]),
     "fedagg_wsum_bf16_f32out": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _U32, _P]),
     "fedagg_wsum_f16": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _I32, _U32, _P]),
+    "fedagg_round_f32": (ctypes.c_int, [_I32, _P, _I64, _P, _P]),
     "fedagg_wsum_f64": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _U32, _P]),
     "fedagg_wsum_i64_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _U32, _P]),
     "fedagg_sum": (ctypes.c_int, [_I32, _P, _I32, _I64, _P, _U32, _P]),

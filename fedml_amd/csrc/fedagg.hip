@@ -771,6 +771,18 @@ int launch_median(const float* const* src, int K, int64_t N, float* out, hipStre
 }
 
 // ---------------------------------------------------------------------------
+// fp32 -> bf16 / f16 rounding of a reduced shard (the client-axis multi-GPU
+// mode accumulates bf16 clients in fp32 and rounds once, after the exchange).
+
+template <bool BF16>
+__global__ __launch_bounds__(kBlock) void round_f32_kernel(const float* __restrict__ in, uint16_t* __restrict__ out,
+                                                           int64_t n) {
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+    out[i] = BF16 ? f32_to_bf16(in[i]) : f32_to_f16(in[i]);
+}
+
+// ---------------------------------------------------------------------------
 // FedOpt SGD(+momentum) epilogue.
 
 __global__ __launch_bounds__(kBlock) void fedopt_sgd_kernel(float* __restrict__ p, float* __restrict__ mom,
@@ -963,6 +975,21 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
     go(PtrW<float>{d_w});
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
+}
+
+int fedagg_round_f32(int32_t dtype, const float* d_in, int64_t N, void* d_out, fedagg_stream_t stream) {
+  if (N < 0 || (N > 0 && (!d_in || !d_out))) return set_error(FEDAGG_EINVAL, "fedagg_round_f32: bad argument");
+  if (dtype != FEDAGG_DT_BF16 && dtype != FEDAGG_DT_F16)
+    return set_error(FEDAGG_EINVAL, "fedagg_round_f32: dtype must be FEDAGG_DT_BF16 or FEDAGG_DT_F16");
+  if (N == 0) return FEDAGG_OK;
+  const int64_t want = (N + kBlock - 1) / kBlock;
+  const unsigned grid = unsigned(want < 8192 ? want : 8192);
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == FEDAGG_DT_BF16)
+    hipLaunchKernelGGL(round_f32_kernel<true>, dim3(grid), dim3(kBlock), 0, st, d_in, (uint16_t*)d_out, N);
+  else
+    hipLaunchKernelGGL(round_f32_kernel<false>, dim3(grid), dim3(kBlock), 0, st, d_in, (uint16_t*)d_out, N);
+  return check_launch("fedagg_round_f32");
 }
 
 int fedagg_sum_mod_i64(const int64_t* const* d_src, int32_t K, int64_t N, int64_t p, int64_t* d_out,

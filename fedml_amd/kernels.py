@@ -183,3 +183,12 @@ def wsum_fedopt_sgd(d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int, par
     nat.check(nat.lib().fedagg_wsum_fedopt_sgd_f32(
         d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), mom.data_ptr() if mom is not None else None,
         float(lr), float(momentum), int(first_step), flags, nat.stream_handle()), "wsum_fedopt_sgd_f32")
+
+
+def round_f32(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """fp32 -> bf16/f16 (RNE) on the device, in libfedagg (fedagg_round_f32)."""
+    _require_cuda(x, "round_f32")
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    nat.check(nat.lib().fedagg_round_f32(_DT_CODE[dtype], x.data_ptr(), x.numel(), out.data_ptr(),
+                                         nat.stream_handle()), "round_f32")
+    return out

@@ -151,6 +151,13 @@ class ClientAxisAggregator:
                 dst.copy_(src)
         return self.shard
 
+    def shard_in_model_dtype(self) -> torch.Tensor:
+        """This rank's shard rounded once to the rows' dtype (bf16/f16 models);
+        fp32 rows return the fp32 shard itself."""
+        if self.dtype in (torch.bfloat16, torch.float16) and self.on_gpu:
+            return kn.round_f32(self.shard, self.dtype)
+        return self.shard
+
     def gather_full(self) -> torch.Tensor:
         """Reassemble the full [length] result on every rank (all-gather of the
         shards; used by tests and when the model must be replicated)."""

@@ -81,6 +81,13 @@ int fedagg_wsum_bf16_f32out(const uint16_t* const* d_src, const float* d_w,
                             int32_t K, int64_t N, float* d_out,
                             uint32_t flags, fedagg_stream_t stream);
 
+/* Round an fp32 vector to bf16 or f16 (RNE; NaN -> torch's canonical NaN for
+ * bf16): the final step of the client-axis multi-GPU mode for 16-bit models,
+ * whose per-GPU partials and reduce-scatter are fp32.  dtype is
+ * FEDAGG_DT_BF16 or FEDAGG_DT_F16 (defined below). */
+int fedagg_round_f32(int32_t dtype, const float* d_in, int64_t N, void* d_out,
+                     fedagg_stream_t stream);
+
 /* fp16 clients -> fp16 average; acc_mode as for bf16. */
 int fedagg_wsum_f16(const uint16_t* const* d_src, const float* d_w, int32_t K,
                     int64_t N, uint16_t* d_out, int32_t acc_mode,

@@ -273,3 +273,15 @@ def test_put_encoded_matches_reference(name, pinned, cuda_device):
     res = bucket.aggregate()
     for k, e in gu.expected_groups(meta, arrays)[0].items():
         gu.assert_same(res[k].cpu(), e, f"{name}[{k}]")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_round_f32_matches_torch_rounding(dtype, cuda_device):
+    x = torch.randn(100_003, device=cuda_device) * 1e3
+    x[:5] = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e-40, -0.0])
+    got = kn.round_f32(x, dtype).cpu()
+    if dtype == torch.bfloat16:
+        exp = torch.from_numpy(orc.f32_to_bf16_bits(x.cpu().numpy()).view(np.int16)).view(torch.bfloat16)
+    else:
+        exp = x.cpu().to(torch.float16)
+    gu.assert_same(got, exp, str(dtype))
