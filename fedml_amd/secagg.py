@@ -50,7 +50,8 @@ def _int64_layout(d: "OrderedDict") -> list:
 
 def _fill(bucket: ClientBucket, dicts: Sequence["OrderedDict"]) -> None:
     for i, d in enumerate(dicts):
-        bucket.put(i, {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in d.items()}, 1)
+        # np.ascontiguousarray would turn a 0-d key into shape (1,)
+        bucket.put(i, {k: torch.from_numpy(np.array(v, dtype=np.int64, order="C", copy=True)) for k, v in d.items()}, 1)
     bucket.sync_ingest()
 
 
