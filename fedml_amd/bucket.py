@@ -335,3 +335,4 @@ class ClientBucket:
         for key, _, _ in self.entries:
             res[key] = per_key[key]
         return res
+

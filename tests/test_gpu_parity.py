@@ -285,3 +285,4 @@ def test_round_f32_matches_torch_rounding(dtype, cuda_device):
     else:
         exp = x.cpu().to(torch.float16)
     gu.assert_same(got, exp, str(dtype))
+
