@@ -851,6 +851,18 @@ int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, c
 // C ABI
 // ===========================================================================
 
+namespace {
+template <class OP>
+int launch_multi(const void* const* d_src, void* const* d_out, const int64_t* d_numel, const int64_t* d_block_begin,
+                 int32_t T, const float* d_w, int32_t K, int64_t total_blocks, hipStream_t st) {
+  using C = Cfg<OP>;
+  hipLaunchKernelGGL((reduce_multi_kernel<OP, C::U, C::V, C::NT, C::BS>), dim3(unsigned(total_blocks)), dim3(C::BS),
+                     0, st, reinterpret_cast<const typename OP::in_t* const*>(d_src),
+                     reinterpret_cast<typename OP::out_t* const*>(d_out), d_numel, d_block_begin, T, d_w, K);
+  return check_launch("fedagg_wsum_multi");
+}
+}  // namespace
+
 extern "C" {
 
 int fedagg_wsum_f32(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float* d_out,
@@ -914,22 +926,49 @@ int fedagg_sum(int32_t dtype, const void* const* d_src, int32_t K, int64_t N, vo
 }
 
 int64_t fedagg_multi_blocks(int32_t dtype, int64_t numel) {
-  if (dtype != FEDAGG_DT_F32 || numel < 0) return -1;
-  return blocks_for<OpF32>(numel);
+  if (numel < 0) return -1;
+  switch (dtype) {
+    case FEDAGG_DT_F32: return blocks_for<OpF32>(numel);
+    case FEDAGG_DT_BF16: return blocks_for<OpBF16Ref>(numel);
+    case FEDAGG_DT_F16: return blocks_for<OpF16Ref>(numel);
+    case FEDAGG_DT_I64: return blocks_for<OpI64F32>(numel);
+    default: return -1;
+  }
+}
+
+
+int fedagg_wsum_multi(int32_t dtype, int32_t acc_mode, const void* const* d_src, void* const* d_out,
+                      const int64_t* d_numel, const int64_t* d_block_begin, int32_t T, const float* d_w, int32_t K,
+                      int64_t total_blocks, fedagg_stream_t stream) {
+  if (K < 1 || T < 1 || total_blocks < 0) return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi: bad sizes");
+  if (!d_src || !d_out || !d_numel || !d_block_begin || !d_w)
+    return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi: null pointer");
+  if (acc_mode != FEDAGG_ACC_REFERENCE && acc_mode != FEDAGG_ACC_FP32)
+    return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi: unknown acc_mode");
+  if (total_blocks == 0) return FEDAGG_OK;
+  if (total_blocks > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi: too many blocks");
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  const bool ref = acc_mode == FEDAGG_ACC_REFERENCE;
+  switch (dtype) {
+    case FEDAGG_DT_F32: return launch_multi<OpF32>(d_src, d_out, d_numel, d_block_begin, T, d_w, K, total_blocks, st);
+    case FEDAGG_DT_BF16:
+      return ref ? launch_multi<OpBF16Ref>(d_src, d_out, d_numel, d_block_begin, T, d_w, K, total_blocks, st)
+                 : launch_multi<OpBF16Acc32>(d_src, d_out, d_numel, d_block_begin, T, d_w, K, total_blocks, st);
+    case FEDAGG_DT_F16:
+      return ref ? launch_multi<OpF16Ref>(d_src, d_out, d_numel, d_block_begin, T, d_w, K, total_blocks, st)
+                 : launch_multi<OpF16Acc32>(d_src, d_out, d_numel, d_block_begin, T, d_w, K, total_blocks, st);
+    case FEDAGG_DT_I64:
+      return launch_multi<OpI64F32>(d_src, d_out, d_numel, d_block_begin, T, d_w, K, total_blocks, st);
+    default: return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi: unsupported dtype");
+  }
 }
 
 int fedagg_wsum_multi_f32(const float* const* d_src, float* const* d_out, const int64_t* d_numel,
                           const int64_t* d_block_begin, int32_t T, const float* d_w, int32_t K,
                           int64_t total_blocks, fedagg_stream_t stream) {
-  if (K < 1 || T < 1 || total_blocks < 0) return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi_f32: bad sizes");
-  if (!d_src || !d_out || !d_numel || !d_block_begin || !d_w)
-    return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi_f32: null pointer");
-  if (total_blocks == 0) return FEDAGG_OK;
-  if (total_blocks > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_multi_f32: too many blocks");
-  using C = Cfg<OpF32>;
-  hipLaunchKernelGGL((reduce_multi_kernel<OpF32, C::U, C::V, C::NT, C::BS>), dim3(unsigned(total_blocks)), dim3(C::BS), 0,
-                     reinterpret_cast<hipStream_t>(stream), d_src, d_out, d_numel, d_block_begin, T, d_w, K);
-  return check_launch("fedagg_wsum_multi_f32");
+  return fedagg_wsum_multi(FEDAGG_DT_F32, FEDAGG_ACC_REFERENCE, reinterpret_cast<const void* const*>(d_src),
+                           reinterpret_cast<void* const*>(d_out), d_numel, d_block_begin, T, d_w, K, total_blocks,
+                           stream);
 }
 
 int fedagg_fedopt_sgd_f32(float* d_param, float* d_mom, const float* d_avg, int64_t N, float lr, float momentum,

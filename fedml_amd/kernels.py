@@ -9,8 +9,11 @@ non-CUDA tensors raise.
 from __future__ import annotations
 
 import ctypes
+import functools
+import operator
 from typing import List, Sequence
 
+import numpy as np
 import torch
 
 from . import _native as nat
@@ -28,9 +31,12 @@ def _require_cuda(t: torch.Tensor, what: str) -> None:
 
 
 def upload_i64(values: Sequence[int], device: torch.device) -> torch.Tensor:
-    host = torch.tensor(list(values), dtype=torch.int64)
+    arr = np.asarray(values, dtype=np.int64)  # ~2x faster than torch.tensor(list) on 40k pointers
     if torch.cuda.is_available():
-        host = host.pin_memory()
+        host = torch.empty(arr.shape, dtype=torch.int64, pin_memory=True)
+        host.numpy()[...] = arr
+    else:
+        host = torch.from_numpy(arr)
     return host.to(device, non_blocking=True)
 
 
@@ -74,7 +80,7 @@ def weights_for(values: Sequence[float], dtype: torch.dtype, device: torch.devic
 
 
 def aligned16(ptrs: Sequence[int]) -> bool:
-    return all((p & 15) == 0 for p in ptrs)
+    return (functools.reduce(operator.or_, ptrs, 0) & 15) == 0
 
 
 def wsum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int,
@@ -131,16 +137,26 @@ def wsum_tensors(tensors: Sequence[torch.Tensor], weights: Sequence[float], out:
     wsum_ptrs(dtype, d_ptrs, d_w, len(tensors), tensors[0].numel(), out, aligned16(ptrs), acc_mode)
 
 
-class MultiF32Plan:
-    """Segment table for the one-launch multi-tensor fp32 kernel
-    (fedagg_wsum_multi_f32): T keys, each with K client pointers."""
+_MULTI_DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16, torch.float16: nat.DT_F16,
+             torch.int64: nat.DT_I64}
+MULTI_DTYPES = tuple(_MULTI_DT)
 
-    def __init__(self, numels: Sequence[int]):
+
+class MultiPlan:
+    """Segment table for the one-launch multi-tensor kernel (fedagg_wsum_multi):
+    T keys of one dtype, each with K client pointers.  int64 keys produce
+    float32 outputs (the reference's int64 * float promotion)."""
+
+    def __init__(self, numels: Sequence[int], dtype: torch.dtype = torch.float32, acc_mode: int = 0):
+        if dtype not in _MULTI_DT:
+            raise TypeError(f"MultiPlan: unsupported dtype {dtype}")
         lib = nat.lib()
+        self.dt = _MULTI_DT[dtype]
+        self.acc_mode = int(acc_mode)
         self.numels = [int(n) for n in numels]
         begin = [0]
         for n in self.numels:
-            nb = lib.fedagg_multi_blocks(nat.DT_F32, n)
+            nb = lib.fedagg_multi_blocks(self.dt, n)
             if nb < 0:
                 raise ValueError("bad numel")
             begin.append(begin[-1] + nb)
@@ -152,14 +168,22 @@ class MultiF32Plan:
         """src_ptrs is the flattened [T][K] table.  Returns the device tables,
         which must stay referenced until the launch has been enqueued."""
         T = len(self.numels)
-        d_src = upload_i64(src_ptrs, device)
-        d_out = upload_i64(out_ptrs, device)
-        d_numel = upload_i64(self.numels, device)
-        d_begin = upload_i64(self.block_begin, device)
-        nat.check(nat.lib().fedagg_wsum_multi_f32(d_src.data_ptr(), d_out.data_ptr(), d_numel.data_ptr(),
-                                                  d_begin.data_ptr(), T, d_w.data_ptr(), K, self.total_blocks,
-                                                  nat.stream_handle()), "wsum_multi_f32")
-        return [d_src, d_out, d_numel, d_begin]
+        if len(src_ptrs) != T * K or len(out_ptrs) != T:
+            raise ValueError("MultiPlan.launch: table sizes do not match the plan")
+        # numels and block starts travel in one upload, pointers in another
+        d_meta = upload_i64(self.numels + self.block_begin, device)
+        d_tab = upload_i64(list(src_ptrs) + list(out_ptrs), device)
+        nat.check(nat.lib().fedagg_wsum_multi(self.dt, self.acc_mode, d_tab.data_ptr(), d_tab.data_ptr() + 8 * T * K,
+                                              d_meta.data_ptr(), d_meta.data_ptr() + 8 * T, T, d_w.data_ptr(), K,
+                                              self.total_blocks, nat.stream_handle()), "wsum_multi")
+        return [d_meta, d_tab]
+
+
+class MultiF32Plan(MultiPlan):
+    """fp32 MultiPlan (kept for callers of the fp32-only entry point)."""
+
+    def __init__(self, numels: Sequence[int]):
+        super().__init__(numels, torch.float32)
 
 
 def fedopt_sgd(param: torch.Tensor, mom: torch.Tensor | None, avg: torch.Tensor, lr: float, momentum: float,

@@ -129,9 +129,14 @@ int fedagg_sum(int32_t dtype, const void* const* d_src, int32_t K, int64_t N,
  * becomes a segment table).  d_src is a [T][K] device pointer table, d_out a
  * [T] device pointer table, d_numel a [T] device int64 array, and
  * d_block_begin a [T+1] device int64 prefix array of workgroup offsets that the
- * host computed with fedagg_multi_blocks() for the same numels.
- * Supported dtype codes: FEDAGG_DT_F32 only (other dtypes go key by key). */
+ * host computed with fedagg_multi_blocks() for the same dtype and numels.
+ * fedagg_wsum_multi takes FEDAGG_DT_F32, _BF16, _F16 (acc_mode as for
+ * fedagg_wsum_bf16; outputs keep the dtype) or _I64 (float32 outputs). */
 int64_t fedagg_multi_blocks(int32_t dtype, int64_t numel);
+int fedagg_wsum_multi(int32_t dtype, int32_t acc_mode, const void* const* d_src,
+                      void* const* d_out, const int64_t* d_numel,
+                      const int64_t* d_block_begin, int32_t T, const float* d_w,
+                      int32_t K, int64_t total_blocks, fedagg_stream_t stream);
 int fedagg_wsum_multi_f32(const float* const* d_src, float* const* d_out,
                           const int64_t* d_numel, const int64_t* d_block_begin,
                           int32_t T, const float* d_w, int32_t K,

@@ -115,6 +115,21 @@ def test_resnet50_multi_tensor_vs_oracle(cuda_device):
         gu.assert_same(res[k].cpu(), exp[k], k)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_resnet50_low_precision_multi_tensor_vs_oracle(dtype, cuda_device):
+    """ResNet-50 key shapes held in bf16/f16 as separate device tensors: one
+    multi-tensor launch for the float keys (bf16/f16 reference chain), one for
+    the 53 int64 keys (fp32 outputs); bit-exact against the oracle."""
+    entries = [(k, s, dtype if dt == torch.float32 else dt) for k, s, dt in shapes.resnet50()]
+    raw = host_clients(entries, 5, seed=11, round_idx=1)
+    args = type("A", (), {"federated_optimizer": "FedAvg"})()
+    exp = orc.agg(args, copy.deepcopy(raw))
+    res = ao.FedMLAggOperator.agg(args, _to_device(raw, cuda_device))
+    for k in exp:
+        assert res[k].dtype == exp[k].dtype, k
+        gu.assert_same(res[k].cpu(), exp[k], k)
+
+
 def test_unaligned_views_take_scalar_path(cuda_device):
     """Tensors that are views at odd element offsets (not 16-byte aligned)."""
     K, N = 5, 4099

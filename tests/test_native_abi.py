@@ -51,7 +51,11 @@ def test_argument_validation_without_gpu(lib):
     assert lib.fedagg_wsum_f32(None, None, 4, -1, None, 0, None) == -1
     assert lib.fedagg_wsum_bf16(1, 1, 2, 10, 1, 7, 1, None) == -1
     assert lib.fedagg_sum(99, 1, 2, 10, 1, 0, None) == -1
-    assert lib.fedagg_multi_blocks(1, 100) == -1
+    assert lib.fedagg_multi_blocks(nat.DT_F64, 100) == -1
+    assert lib.fedagg_multi_blocks(nat.DT_F32, -1) == -1
+    assert lib.fedagg_wsum_multi(nat.DT_F64, 0, 1, 1, 1, 1, 1, 1, 2, 1, None) == -1
+    assert lib.fedagg_wsum_multi(nat.DT_BF16, 5, 1, 1, 1, 1, 1, 1, 2, 1, None) == -1
+    assert lib.fedagg_wsum_multi(nat.DT_F32, 0, None, 1, 1, 1, 1, 1, 2, 1, None) == -1
     assert lib.fedagg_version() == 1
     assert lib.fedagg_num_variants() > 0
 
@@ -65,6 +69,17 @@ def test_multi_block_plan(lib):
     per_block = 4096 // (plan.block_begin[3] - plan.block_begin[2])
     assert per_block >= 1024
     assert plan.total_blocks == plan.block_begin[-1]
+
+
+@pytest.mark.parametrize("dtype,elems_per_block", [(torch.float32, 4096), (torch.bfloat16, 8192),
+                                                     (torch.float16, 8192), (torch.int64, 2048)])
+def test_multi_plan_dtypes(lib, dtype, elems_per_block):
+    from fedml_amd.kernels import MultiPlan
+
+    plan = MultiPlan([0, 1, elems_per_block, elems_per_block + 1, 10 * elems_per_block], dtype)
+    assert plan.block_begin == [0, 0, 1, 2, 4, 14]
+    with pytest.raises(TypeError):
+        MultiPlan([1], torch.float64)
 
 
 def test_no_cpu_fallback():
