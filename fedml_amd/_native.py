@@ -44,6 +44,9 @@ SIGNATURES = {
     "fedagg_wsum_multi_f32": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _I32, _I64, _P]),
     "fedagg_wsum_multi": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P, _I32, _P, _I32, _I64, _P]),
     "fedagg_fedopt_sgd_f32": (ctypes.c_int, [_P, _P, _P, _I64, _F, _F, _I32, _P]),
+    "fedagg_adam_scalars": (ctypes.c_int, [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                          _I64, _P]),
+    "fedagg_wsum_fedopt_adam_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _I32, _U32, _P]),
     "fedagg_wsum_fedopt_sgd_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _F, _F, _I32, _U32, _P]),
     "fedagg_median_f32": (ctypes.c_int, [_P, _I32, _I64, _P, _U32, _P]),
     "fedagg_sum_mod_i64": (ctypes.c_int, [_P, _I32, _I64, _I64, _P, _U32, _P]),

@@ -26,6 +26,8 @@ HIPCC_FLAGS = [
     "-ffp-contract=off",
     # torch's CPU kernels keep fp32 denormals; so do we.
     "-fno-gpu-flush-denormals-to-zero",
+    # IEEE division and sqrt (server Adam step); the HIP default, stated here
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-fPIC",
     "-shared",
     "-Wall",

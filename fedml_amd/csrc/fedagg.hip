@@ -31,6 +31,7 @@
 //   fp64 * float        : fl64(x * w)
 
 #include <hip/hip_runtime.h>
+#include <cmath>
 
 #include <stdint.h>
 #include <string.h>
@@ -387,6 +388,64 @@ struct SgdEpi {
     float mb = (mom && !first) ? mom[e] : 0.f;
     p[e] = step1(p[e], a, &mb);
     if (mom) mom[e] = mb;
+  }
+};
+
+// Fused server Adam step (sp/fedopt/fedopt_api.py:121-130 with torch.optim.Adam's
+// single-tensor CPU path, amsgrad off, weight_decay 0).  Per element, with the
+// host-computed fp32 scalars of fedagg_adam_scalars():
+//   g = p_old - avg
+//   m = lerp(m, g, w1)          torch's vectorised lerp: one fma
+//   v = fma(fl(c2*g), g, fl(v*beta2))   mul_(beta2).addcmul_(g, g, value=c2)
+//   p = p_old + fl(nss*m) / (fl(sqrt(v) / bc2s) + eps)   addcdiv_, no fma
+struct AdamEpi {
+  float* p;
+  float* m;
+  float* v;
+  float w1, beta2, c2, bc2s, eps, nss;
+  int first;  // exp_avg / exp_avg_sq are zero before torch's first step: skip their loads
+  static constexpr int E = 4;
+  struct Pre {
+    Pack<float, 4> p, m, v;
+  };
+  __device__ __forceinline__ Pre pre(int64_t off) const {
+    Pre r;
+    r.p = load_pack<float, true>(p + off);
+    r.m = {};
+    r.v = {};
+    if (!first) {
+      r.m = load_pack<float, true>(m + off);
+      r.v = load_pack<float, true>(v + off);
+    }
+    return r;
+  }
+  __device__ __forceinline__ float step1(float po, float avg, float* mm, float* vv) const {
+    const float g = po - avg;
+    const float d = g - *mm;
+    *mm = __builtin_fabsf(w1) < 0.5f ? __builtin_fmaf(w1, d, *mm) : __builtin_fmaf(w1 - 1.0f, d, g);
+    const float vb = *vv * beta2;
+    *vv = __builtin_fmaf(c2 * g, g, vb);
+    const float denom = __builtin_sqrtf(*vv) / bc2s + eps;
+    return po + (nss * *mm) / denom;
+  }
+  __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E], const Pre& pr) const {
+    float po[E], mo[E], vo[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      mo[e] = pr.m.v[e];
+      vo[e] = pr.v.v[e];
+      po[e] = step1(pr.p.v[e], acc[e], &mo[e], &vo[e]);
+    }
+    store_pack<float, E>(p + off, po);
+    store_pack<float, E>(m + off, mo);
+    store_pack<float, E>(v + off, vo);
+  }
+  __device__ __forceinline__ void one(int64_t e, float a) const {
+    float mm = first ? 0.f : m[e];
+    float vv = first ? 0.f : v[e];
+    p[e] = step1(p[e], a, &mm, &vv);
+    m[e] = mm;
+    v[e] = vv;
   }
 };
 
@@ -1014,6 +1073,58 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
     go(PtrW<float>{d_w});
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
+}
+
+int fedagg_adam_scalars(double lr, double beta1, double beta2, double eps, int64_t step, float* out6) {
+  if (!out6 || step < 1) return set_error(FEDAGG_EINVAL, "fedagg_adam_scalars: step must be >= 1");
+  // the double-precision scalar chain of torch.optim.adam._single_tensor_adam;
+  // Python's ** is C pow(), so bias_correction2 ** 0.5 is pow(x, 0.5), not sqrt
+  const double t = double(step);
+  const double bc1 = 1.0 - std::pow(beta1, t);
+  const double bc2 = 1.0 - std::pow(beta2, t);
+  const double step_size = lr / bc1;
+  out6[0] = float(1.0 - beta1);         // lerp_ weight
+  out6[1] = float(beta2);               // mul_
+  out6[2] = float(1.0 - beta2);         // addcmul_ value
+  out6[3] = float(std::pow(bc2, 0.5));  // bias_correction2_sqrt
+  out6[4] = float(eps);                 // add_
+  out6[5] = float(-step_size);          // addcdiv_ value
+  return FEDAGG_OK;
+}
+
+int fedagg_wsum_fedopt_adam_f32(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float* d_param,
+                                float* d_exp_avg, float* d_exp_avg_sq, const float* scalars6, int32_t first_step,
+                                uint32_t flags, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adam_f32: K must be >= 1 and N >= 0");
+  if (!d_src || !d_w || !d_param || !d_exp_avg || !d_exp_avg_sq || !scalars6)
+    return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adam_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  using C = Cfg<OpF32>;
+  const int64_t grid = blocks_for<OpF32>(N);
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adam_f32: N too large");
+  Seg<OpF32> s{d_src, N};
+  AdamEpi epi{d_param, d_exp_avg, d_exp_avg_sq, scalars6[0], scalars6[1], scalars6[2],
+              scalars6[3], scalars6[4], scalars6[5], first_step};
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  auto go = [&](const auto& w) {
+    using WS = std::decay_t<decltype(w)>;
+    if (flags & FEDAGG_ALIGNED16) {
+      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
+                         dim3(C::BS), 0, st, s, epi, w, K);
+    } else {
+      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
+                         dim3(C::BS), 0, st, s, epi, w, K);
+    }
+  };
+  if (flags & FEDAGG_HOST_WEIGHTS) {
+    InlW<float> iw;
+    if (!inline_weights<float>(d_w, K, &iw))
+      return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adam_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
+    go(iw);
+  } else {
+    go(PtrW<float>{d_w});
+  }
+  return check_launch("fedagg_wsum_fedopt_adam_f32");
 }
 
 int fedagg_round_f32(int32_t dtype, const float* d_in, int64_t N, void* d_out, fedagg_stream_t stream) {

@@ -13,9 +13,16 @@ Mirrors the server side of python/fedml/simulation/mpi/fedopt/FedOptAggregator.p
       buffers (BatchNorm running stats, num_batches_tracked) take the
       average, int64 ones truncated by load_state_dict's copy_ (:126-130).
 
-Supported server optimizer: "sgd" (OptRepo name, optrepo.py:10), with or
-without momentum — the optimizers the MPI aggregator can build (it passes
-`momentum=` to the constructor).  Parameters are fp32.
+Supported server optimizers (OptRepo names, optrepo.py:10); parameters are fp32:
+  "sgd"   with or without momentum — what the MPI aggregator builds (it passes
+          `momentum=` to the constructor, :49-54).
+  "adam"  torch.optim.Adam with its defaults and lr=server_lr, as the SP
+          FedOptAPI builds it (sp/fedopt/fedopt_api.py:78-85; the MPI aggregator
+          cannot: Adam rejects `momentum=`).  server_momentum is ignored.  The
+          step is fused like SGD's (fedagg_wsum_fedopt_adam_f32); exp_avg and
+          exp_avg_sq are bit-identical to torch's CPU Adam, the parameters
+          differ only where torch's CPU sqrt is not correctly rounded
+          (tests/test_gpu_fedopt.py).
 
 Device layout: the round's updates sit in a ClientBucket; the global model
 and the momentum buffers are flat fp32 vectors with the bucket's fp32 layout.
@@ -39,10 +46,15 @@ class FedOptServer:
     def __init__(self, global_state: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],
                  worker_num: int, server_optimizer: str = "sgd", server_lr: float = 1.0,
                  server_momentum: float = 0.0, device=None):
-        if server_optimizer.lower() != "sgd":
-            raise NotImplementedError(f"server_optimizer {server_optimizer!r}: only 'sgd' (with momentum) is fused")
+        self.optimizer = server_optimizer.lower()
+        if self.optimizer not in ("sgd", "adam"):
+            raise NotImplementedError(f"server_optimizer {server_optimizer!r}: 'sgd' (with momentum) and 'adam' "
+                                      "are fused")
         self.lr = float(server_lr)
-        self.momentum = float(server_momentum)
+        self.momentum = float(server_momentum) if self.optimizer == "sgd" else 0.0
+        # torch.optim.Adam defaults (sp/fedopt/fedopt_api.py:79-85 passes lr only)
+        self.betas, self.eps = (0.9, 0.999), 1e-8
+        self.step_count = 0
         self.worker_num = worker_num
         self.param_names = list(param_names)
         self.bucket = ClientBucket(global_state, worker_num, device)
@@ -62,6 +74,9 @@ class FedOptServer:
                 if k in self.bucket.int_keys:
                     self._int_state[k] = t.detach().to(self.device).clone()
             self.mom = torch.zeros_like(self.global_flat[torch.float32]) if (f32 and self.momentum) else None
+            adam = f32 and self.optimizer == "adam"
+            self.exp_avg = torch.zeros_like(self.global_flat[torch.float32]) if adam else None
+            self.exp_avg_sq = torch.zeros_like(self.global_flat[torch.float32]) if adam else None
         self.first_step = True
         self._views: Optional["OrderedDict[str, torch.Tensor]"] = None
         self.runs: List[Tuple[bool, int, int]] = self._runs(f32) if f32 else []
@@ -111,10 +126,16 @@ class FedOptServer:
             self.bucket.sync_ingest()
             w32 = kn.weights_for(weights, torch.float32, self.device)  # by value for K <= 256
             f32 = self.global_flat.get(torch.float32)
+            step = self.step_count + 1
+            sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step) \
+                if self.optimizer == "adam" else None
             if events is not None:
                 events[0].record()
             for (is_param, lo, hi), d_ptrs in zip(self.runs, self.run_ptrs):
-                if is_param:
+                if is_param and sc is not None:
+                    kn.wsum_fedopt_adam(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
+                                        self.exp_avg_sq[lo:hi], sc, self.first_step, True)
+                elif is_param:
                     kn.wsum_fedopt_sgd(d_ptrs, w32, K, hi - lo, f32[lo:hi],
                                        self.mom[lo:hi] if self.mom is not None else None,
                                        self.lr, self.momentum, self.first_step, True)
@@ -132,7 +153,49 @@ class FedOptServer:
                 g, j = self.bucket.where[k]
                 t.reshape(-1).copy_(self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]])
         self.first_step = False
+        self.step_count += 1
         return self.get_global_model_params()
+
+    # ---- optimizer state (the reference's opt.state_dict() round trip) ------
+
+    def _param_slices(self):
+        for key in self.param_names:
+            g, j = self.bucket.where[key]
+            yield key, g.offsets[j], g.numels[j], g.shapes[j]
+
+    def optimizer_state(self) -> Dict[str, object]:
+        """Per named parameter, the state torch's optimizer would hold after the
+        same rounds: {"step": n, <buffer>: {name: tensor}} with buffer
+        "momentum_buffer" (sgd with momentum) or "exp_avg" / "exp_avg_sq"
+        (adam).  Copies; for checkpointing and parity checks."""
+        out: Dict[str, object] = {"step": self.step_count}
+        bufs = {"momentum_buffer": self.mom} if self.optimizer == "sgd" else \
+            {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
+        for name, flat in bufs.items():
+            if flat is None or self.step_count == 0:
+                continue
+            out[name] = OrderedDict((k, flat[o:o + n].view(shape).clone()) for k, o, n, shape in self._param_slices())
+        return out
+
+    def load_optimizer_state(self, state: Dict[str, object]) -> None:
+        """Inverse of optimizer_state() (resume, or the state a torch optimizer
+        holds: the next aggregate() continues from it)."""
+        step = int(state.get("step", 0))
+        bufs = {"momentum_buffer": self.mom} if self.optimizer == "sgd" else \
+            {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
+        with torch.cuda.device(self.device):
+            for name, flat in bufs.items():
+                if flat is None:
+                    continue
+                src = state.get(name)
+                if src is None:
+                    if step:
+                        raise KeyError(f"optimizer state at step {step} lacks {name!r}")
+                    continue
+                for k, o, n, _ in self._param_slices():
+                    flat[o:o + n].copy_(src[k].detach().reshape(-1))
+        self.step_count = step
+        self.first_step = step == 0
 
     def get_global_model_params(self) -> "OrderedDict[str, torch.Tensor]":
         """Views of the persistent global vectors (built once; they track every
@@ -157,6 +220,11 @@ class FedOptServer:
         for is_param, lo, hi in self.runs:
             n = hi - lo
             tot += K * n * 4
-            tot += (2 * n * 4 + (2 * n * 4 if self.mom is not None and not self.first_step else
-                                 (n * 4 if self.mom is not None else 0))) if is_param else n * 4
+            if not is_param:
+                tot += n * 4
+            elif self.optimizer == "adam":  # p read+write, exp_avg / exp_avg_sq written (+ read after step 1)
+                tot += 2 * n * 4 + (4 if not self.first_step else 2) * n * 4
+            else:
+                tot += 2 * n * 4 + (2 * n * 4 if self.mom is not None and not self.first_step else
+                                    (n * 4 if self.mom is not None else 0))
         return tot

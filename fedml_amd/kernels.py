@@ -209,6 +209,28 @@ def wsum_fedopt_sgd(d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int, par
         float(lr), float(momentum), int(first_step), flags, nat.stream_handle()), "wsum_fedopt_sgd_f32")
 
 
+def adam_scalars(lr: float, beta1: float, beta2: float, eps: float, step: int) -> "ctypes.Array":
+    """The six fp32 scalars of one torch Adam step (fedagg_adam_scalars), as a
+    host array to pass to wsum_fedopt_adam."""
+    out = (ctypes.c_float * 6)()
+    nat.check(nat.lib().fedagg_adam_scalars(float(lr), float(beta1), float(beta2), float(eps), int(step),
+                                            ctypes.addressof(out)), "adam_scalars")
+    return out
+
+
+def wsum_fedopt_adam(d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int, param: torch.Tensor,
+                     exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, scalars: "ctypes.Array", first_step: bool,
+                     aligned: bool) -> None:
+    """FedAvg of K fp32 sources fused with the server Adam step: param, exp_avg
+    and exp_avg_sq (flat, N elements each) are updated in place."""
+    _require_cuda(param, "wsum_fedopt_adam")
+    ok = aligned and all((t.data_ptr() & 15) == 0 for t in (param, exp_avg, exp_avg_sq))
+    flags = (nat.FEDAGG_ALIGNED16 if ok else 0) | (nat.FEDAGG_HOST_WEIGHTS if isinstance(d_w, HostWeights) else 0)
+    nat.check(nat.lib().fedagg_wsum_fedopt_adam_f32(
+        d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+        ctypes.addressof(scalars), int(first_step), flags, nat.stream_handle()), "wsum_fedopt_adam_f32")
+
+
 def round_f32(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """fp32 -> bf16/f16 (RNE) on the device, in libfedagg (fedagg_round_f32)."""
     _require_cuda(x, "round_f32")

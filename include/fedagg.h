@@ -168,6 +168,24 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w,
                                int32_t first_step, uint32_t flags,
                                fedagg_stream_t stream);
 
+/* Server Adam (torch.optim.Adam defaults: amsgrad off, weight_decay 0) fused
+ * with the FedAvg of K fp32 clients, one pass.  Replaces the server step of
+ * simulation/sp/fedopt/fedopt_api.py:121-130 (_set_model_global_grads, then
+ * opt.step() with OptRepo "adam", lr=server_lr).  d_exp_avg / d_exp_avg_sq are
+ * the optimizer state (N floats each, zero before the first step; with
+ * first_step != 0 they are only written).  scalars6 is host memory filled by
+ * fedagg_adam_scalars() for the step number (1-based) about to be taken.
+ * Per element: g = p - avg; m = lerp(m, g, 1-beta1); v = v*beta2 + (1-beta2)*g*g;
+ * p += (-lr/bc1)*m / (sqrt(v)/sqrt(bc2) + eps), rounded as torch's CPU kernels
+ * round (lerp and addcmul fused, addcdiv not); sqrt is correctly rounded. */
+int fedagg_adam_scalars(double lr, double beta1, double beta2, double eps,
+                        int64_t step, float* out6);
+int fedagg_wsum_fedopt_adam_f32(const float* const* d_src, const float* d_w,
+                                int32_t K, int64_t N, float* d_param,
+                                float* d_exp_avg, float* d_exp_avg_sq,
+                                const float* scalars6, int32_t first_step,
+                                uint32_t flags, fedagg_stream_t stream);
+
 /* ---- Robust aggregation --------------------------------------------------- */
 
 /* Coordinate-wise median over K fp32 clients (the "wise_median" defense,

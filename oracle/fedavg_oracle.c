@@ -139,3 +139,24 @@ void oracle_fedopt_sgd_f32(float* p, float* buf, const float* avg, int64_t N, fl
     p[e] = fmaf(b, neg_lr, po);
   }
 }
+
+/* torch.optim.Adam, single-tensor CPU path (torch/optim/adam.py
+ * _single_tensor_adam), the moment updates of one step:
+ *   g = p - avg                          fedopt_api.py:160 parameter.grad
+ *   m.lerp_(g, w1)                       ATen lerp: |w1| < 0.5 ? fma(w1, g-m, m)
+ *                                                   : fma(w1-1, g-m, g)
+ *   v.mul_(beta2).addcmul_(g, g, c2)     fma(fl(c2*g), g, fl(v*beta2))
+ * (fusion measured against torch 2.10's CPU kernels, vector body and scalar
+ * tail).  The parameter update needs torch's own sqrt and is done by the
+ * caller (fedavg_oracle.fedopt_adam). */
+void oracle_adam_moments_f32(const float* p, const float* avg, float* m, float* v, int64_t N, float w1, float beta2,
+                             float c2) {
+  const int small = fabsf(w1) < 0.5f;
+  for (int64_t e = 0; e < N; ++e) {
+    const float g = p[e] - avg[e];
+    const float d = g - m[e];
+    m[e] = small ? fmaf(w1, d, m[e]) : fmaf(w1 - 1.0f, d, g);
+    const float vb = v[e] * beta2;
+    v[e] = fmaf(c2 * g, g, vb);
+  }
+}

@@ -231,6 +231,7 @@ def clib() -> ctypes.CDLL:
             "oracle_sum_bf16": [P, I, L, P],
             "oracle_sum_i64": [P, I, L, P],
             "oracle_fedopt_sgd_f32": [P, P, P, L, F, F, I],
+            "oracle_adam_moments_f32": [P, P, P, P, L, F, F, F],
         }.items():
             fn = getattr(lib, name)
             fn.restype = None
@@ -277,6 +278,65 @@ def fedopt_sgd(p_old: np.ndarray, avg: np.ndarray, buf: np.ndarray | None, lr: f
     clib().oracle_fedopt_sgd_f32(p.ctypes.data, b.ctypes.data, a.ctypes.data, p.size, float(lr),
                                  float(momentum), int(first))
     return p, (b if momentum != 0 else None)
+
+
+def adam_scalars(lr: float, beta1: float, beta2: float, eps: float, step: int) -> Tuple[float, ...]:
+    """The double-precision scalars of torch's _single_tensor_adam for 1-based
+    `step`, each as the fp32 value the CPU kernel receives: (lerp weight, beta2,
+    addcmul value, bias_correction2 ** 0.5, eps, -step_size)."""
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    vals = (1 - beta1, beta2, 1 - beta2, bc2 ** 0.5, eps, -(lr / bc1))
+    return tuple(float(np.float32(v)) for v in vals)
+
+
+def fedopt_adam(p_old: np.ndarray, avg: np.ndarray, m: np.ndarray | None, v: np.ndarray | None, lr: float,
+                step: int, betas=(0.9, 0.999), eps: float = 1e-8, sqrt: str = "torch"
+                ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """One server Adam step on one named parameter (sp/fedopt/fedopt_api.py:121-130,
+    grad = p_old - avg as _set_model_global_grads :155-160).  Returns (p, m, v).
+
+    sqrt="torch" uses torch's CPU sqrt, which is what the reference's
+    exp_avg_sq.sqrt() runs (on this image an MKL VML routine that is NOT
+    correctly rounded: ~0.6% of fp32 results are 1 ulp off); sqrt="ieee" uses
+    the correctly rounded sqrt the GPU kernel computes."""
+    w1, b2, c2, bc2s, epsf, nss = (np.float32(x) for x in adam_scalars(lr, betas[0], betas[1], eps, step))
+    p = np.ascontiguousarray(p_old, dtype=np.float32).reshape(-1).copy()
+    a = np.ascontiguousarray(avg, dtype=np.float32).reshape(-1)
+    mm = np.zeros_like(p) if m is None else np.ascontiguousarray(m, dtype=np.float32).reshape(-1).copy()
+    vv = np.zeros_like(p) if v is None else np.ascontiguousarray(v, dtype=np.float32).reshape(-1).copy()
+    clib().oracle_adam_moments_f32(p.ctypes.data, a.ctypes.data, mm.ctypes.data, vv.ctypes.data, p.size,
+                                   float(w1), float(b2), float(c2))
+    if sqrt == "torch":
+        s = torch.from_numpy(vv).sqrt().numpy()
+    elif sqrt == "ieee":
+        s = np.sqrt(vv)
+    else:
+        raise ValueError(sqrt)
+    denom = (s / bc2s) + epsf  # (exp_avg_sq.sqrt() / bias_correction2_sqrt).add_(eps)
+    p = (p + (nss * mm) / denom).astype(np.float32)  # addcdiv_: self + (value * t1) / t2
+    return p, mm, vv
+
+
+def fedopt_adam_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str], raw_grad_list,
+                      lr: float, state: Dict[str, Tuple[np.ndarray, np.ndarray]], step: int,
+                      sqrt: str = "torch") -> "OrderedDict[str, torch.Tensor]":
+    """One FedOptAPI round with server_optimizer="adam" (fedopt_api.py:121-130):
+    FedAvg, Adam on named parameters (state carries exp_avg / exp_avg_sq across
+    rounds, step is 1-based), averaged values for buffers."""
+    class _A:
+        federated_optimizer = "FedAvg"
+    avg = agg(_A(), raw_grad_list)
+    out = OrderedDict()
+    for k, t_old in global_sd.items():
+        if k in param_names:
+            m, v = state.get(k, (None, None))
+            p, m, v = fedopt_adam(to_np(t_old).ravel(), to_np(avg[k]).ravel(), m, v, lr, step, sqrt=sqrt)
+            state[k] = (m, v)
+            out[k] = torch.from_numpy(p).reshape(t_old.shape)
+        else:
+            out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)
+    return out
 
 
 def fedopt_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],

@@ -102,6 +102,20 @@ FEDOPT_MODEL = [
     ["2.weight", [3, 5], F32], ["2.bias", [3], F32],
 ]
 FEDOPT_PARAMS = ["0.weight", "0.bias", "1.weight", "1.bias", "2.weight", "2.bias"]
+# Server Adam (sp/fedopt/fedopt_api.py, OptRepo "adam", lr only): a wider model
+# so the fixtures cover torch's AVX-512 vector body as well as its scalar tails.
+ADAM_MODEL = [
+    ["0.weight", [40, 64], F32], ["0.bias", [40], F32],
+    ["1.weight", [40], F32], ["1.bias", [40], F32], ["1.running_mean", [40], F32], ["1.running_var", [40], F32],
+    ["1.num_batches_tracked", [], I64],
+    ["2.weight", [10, 40], F32], ["2.bias", [10], F32],
+]
+FEDOPT_MODELS = {"small": FEDOPT_MODEL, "adam": ADAM_MODEL}
+FEDOPT_ADAM_CASES = [
+    dict(name="fedopt_adam_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=93),
+    dict(name="fedopt_adam_lr1", K=3, rounds=3, lr=1.0, model="adam", seed=94),
+    dict(name="fedopt_adam_lr1e-3_small", K=5, rounds=5, lr=0.001, model="small", seed=95),
+]
 FEDOPT_CASES = [
     dict(name="fedopt_sgd_m09_lr1", K=4, rounds=3, lr=1.0, momentum=0.9, seed=90),
     dict(name="fedopt_sgd_m09_lr1e-3", K=4, rounds=3, lr=0.001, momentum=0.9, seed=91),
@@ -166,13 +180,14 @@ class Args:
 
 
 def fedopt_global_init(spec):
-    raw = host_clients(_entries(FEDOPT_MODEL), 1, spec["seed"])
+    raw = host_clients(_entries(FEDOPT_MODELS[spec.get("model", "small")]), 1, spec["seed"])
     return raw[0][1]
 
 
 def fedopt_round_inputs(spec, global_sd, r):
     """Clients of round r: global + small noise (fresh objects)."""
-    noise = host_clients(_entries(FEDOPT_MODEL), spec["K"], spec["seed"] * 100 + r, round_idx=r)
+    noise = host_clients(_entries(FEDOPT_MODELS[spec.get("model", "small")]), spec["K"], spec["seed"] * 100 + r,
+                         round_idx=r)
     out = []
     for n, d in noise:
         nd = OrderedDict()

@@ -1,6 +1,6 @@
 """Generate golden vectors by running the REFERENCE aggregator (CPU container).
 
-    python tests/golden/gen_golden.py
+    python tests/golden/gen_golden.py [case-name-prefix ...]
 
 Imports FedML's own code from /root/reference/python (read-only) through
 namespace-package stubs, so only the modules on the aggregation path load:
@@ -155,6 +155,80 @@ def run_fedopt_case(FedOptAggregator, spec):
     save(spec["name"], meta, arrays)
 
 
+def import_sp_fedopt():
+    """sp/fedopt/fedopt_api.py's FedOptAPI (its trainer factory import is stubbed:
+    only _aggregate / _set_model_global_grads / _instanciate_opt are used)."""
+    for name, path in [("fedml.simulation.sp", f"{REF}/simulation/sp"),
+                       ("fedml.simulation.sp.fedopt", f"{REF}/simulation/sp/fedopt")]:
+        m = types.ModuleType(name)
+        m.__path__ = [path]
+        sys.modules.setdefault(name, m)
+    if "fedml.ml.trainer" not in sys.modules:  # its __init__ pulls in every trainer
+        m = types.ModuleType("fedml.ml.trainer")
+        m.__path__ = []
+        sys.modules["fedml.ml.trainer"] = m
+    tc = types.ModuleType("fedml.ml.trainer.trainer_creator")
+    tc.create_model_trainer = None
+    sys.modules["fedml.ml.trainer.trainer_creator"] = tc
+    from fedml.simulation.sp.fedopt.fedopt_api import FedOptAPI
+    return FedOptAPI
+
+
+def run_fedopt_adam_case(FedOptAPI, spec):
+    """The server half of FedOptAPI.train (fedopt_api.py:121-130) with
+    server_optimizer="adam": _aggregate, then zero_grad / state_dict /
+    _set_model_global_grads / _instanciate_opt / load_state_dict / step, each the
+    reference's own method.  Clients are the synthetic updates of cases.py."""
+    ent = cases.FEDOPT_MODELS[spec["model"]]
+    dims = [ent[0][1][1], ent[0][1][0], ent[7][1][0]]
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(dims[0], dims[1]), torch.nn.BatchNorm1d(dims[1]),
+                                torch.nn.Linear(dims[1], dims[2]))
+    model.load_state_dict(cases.fedopt_global_init(spec))
+
+    class Trainer:
+        def __init__(self, m):
+            self.model = m
+
+        def get_model_params(self):
+            return self.model.state_dict()
+
+        def set_model_params(self, sd):
+            self.model.load_state_dict(sd)
+
+    class A:
+        server_optimizer = "adam"
+        server_lr = spec["lr"]
+
+    api = object.__new__(FedOptAPI)
+    api.args = A()
+    api.model_trainer = Trainer(model)
+    api._instanciate_opt()
+    meta = {"spec": spec, "rounds": [], "param_names": cases.FEDOPT_PARAMS}
+    arrays = {}
+    for k, t in cases.fedopt_global_init(spec).items():
+        arrays[f"init:{k}"] = tensor_bytes(t)
+    gsd = OrderedDict((k, t.clone()) for k, t in model.state_dict().items())
+    for r in range(spec["rounds"]):
+        raw = cases.fedopt_round_inputs(spec, gsd, r)
+        meta["rounds"].append({"in_sha256": fingerprint(raw)})
+        w_avg = api._aggregate(raw)
+        api.opt.zero_grad()
+        opt_state = api.opt.state_dict()
+        api._set_model_global_grads(w_avg)
+        api._instanciate_opt()
+        api.opt.load_state_dict(opt_state)
+        api.opt.step()
+        gsd = OrderedDict((k, t.detach().clone()) for k, t in model.state_dict().items())
+        for k, t in gsd.items():
+            arrays[f"r{r}:{k}"] = tensor_bytes(t)
+        st = api.opt.state_dict()["state"]
+        for j, name in enumerate(cases.FEDOPT_PARAMS):
+            arrays[f"r{r}:exp_avg:{name}"] = tensor_bytes(st[j]["exp_avg"])
+            arrays[f"r{r}:exp_avg_sq:{name}"] = tensor_bytes(st[j]["exp_avg_sq"])
+    save(spec["name"], meta, arrays)
+
+
 def run_secagg_case(spec):
     """The reference's own aggregate_models_in_finite / aggregate_model_reconstruction."""
     for name, path in [("fedml.core.mpc", f"{REF}/core/mpc"), ("fedml.cross_silo", f"{REF}/cross_silo"),
@@ -190,16 +264,24 @@ def run_secagg_case(spec):
     save(spec["name"], meta, arrays)
 
 
-def main():
+def main(only=()):
+    """only: case-name prefixes to regenerate (default: every case)."""
+    def want(spec):
+        return not only or any(spec["name"].startswith(p) for p in only)
+
     FedMLAggOperator, FedOptAggregator = import_reference()
-    for spec in cases.CASES:
+    for spec in filter(want, cases.CASES):
         run_agg_case(FedMLAggOperator, spec)
         print("wrote", spec["name"])
-    for spec in cases.FEDOPT_CASES:
+    for spec in filter(want, cases.FEDOPT_CASES):
         run_fedopt_case(FedOptAggregator, spec)
         print("wrote", spec["name"])
+    FedOptAPI = import_sp_fedopt()
+    for spec in filter(want, cases.FEDOPT_ADAM_CASES):
+        run_fedopt_adam_case(FedOptAPI, spec)
+        print("wrote", spec["name"])
     Median, Trimmed = import_defenses()
-    for spec in cases.DEFENSE_CASES:
+    for spec in filter(want, cases.DEFENSE_CASES):
         args = cases.DefenseArgs(spec)
         if spec["defense"] == "wise_median":
             # FedMLDefender.defend_on_aggregation -> CoordinateWiseMedianDefense (fedml_defender.py:163-171)
@@ -211,10 +293,10 @@ def main():
                 return FedMLAggOperator.agg(args, Trimmed(args).defend_before_aggregation(raw, None))
         run_agg_case(FedMLAggOperator, spec, aggregate=agg)
         print("wrote", spec["name"])
-    for spec in cases.SECAGG_CASES:
+    for spec in filter(want, cases.SECAGG_CASES):
         run_secagg_case(spec)
         print("wrote", spec["name"])
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -4,6 +4,7 @@ from __future__ import annotations
 
 from collections import OrderedDict
 
+import numpy as np
 import pytest
 import torch
 
@@ -70,3 +71,113 @@ def test_fedopt_lora_layout_is_one_launch(cuda_device):
     sd = OrderedDict((k, torch.zeros(s)) for k, s, _ in ents)
     server = FedOptServer(sd, list(sd.keys()), 4, "sgd", 1.0, 0.9, cuda_device)
     assert len(server.runs) == 1 and server.runs[0][0]
+
+
+def _golden_state(arrays, r, names):
+    """Torch's Adam state after round r (r = -1: before the first step)."""
+    if r < 0:
+        return {"step": 0}
+    st = {"step": r + 1, "exp_avg": OrderedDict(), "exp_avg_sq": OrderedDict()}
+    for k in names:
+        st["exp_avg"][k] = torch.from_numpy(arrays[f"r{r}:exp_avg:{k}"].copy())
+        st["exp_avg_sq"][k] = torch.from_numpy(arrays[f"r{r}:exp_avg_sq:{k}"].copy())
+    return st
+
+
+def _bits(t: torch.Tensor):
+    return t.detach().cpu().contiguous().reshape(-1).view(torch.int32)
+
+
+@pytest.mark.parametrize("spec", cases.FEDOPT_ADAM_CASES, ids=lambda s: s["name"])
+def test_fedopt_adam_matches_reference(spec, cuda_device):
+    """Each round of FedOptAPI's server Adam, started from the reference's own
+    state of the previous round (parameters and optimizer moments):
+      - exp_avg / exp_avg_sq and every buffer: bit-identical to torch;
+      - parameters: bit-identical to the oracle with a correctly rounded sqrt,
+        and within 1 ulp(p) + 2^-21 |step| of torch, whose CPU sqrt (MKL VML)
+        is not correctly rounded — the only source of difference."""
+    meta, arrays = gu.load(spec["name"])
+    names = cases.FEDOPT_PARAMS
+    init = cases.fedopt_global_init(spec)
+    prev = OrderedDict((k, gu.to_tensor(arrays[f"init:{k}"], str(t.dtype).replace("torch.", ""), t.shape))
+                       for k, t in init.items())
+    exact = total = 0
+    for r in range(spec["rounds"]):
+        server = FedOptServer(prev, names, spec["K"], "adam", spec["lr"], 0.0, cuda_device)
+        server.load_optimizer_state(_golden_state(arrays, r - 1, names))
+        raw = cases.fedopt_round_inputs(spec, prev, r)
+        assert fingerprint(raw) == meta["rounds"][r]["in_sha256"]
+        for i, (n, d) in enumerate(raw):
+            server.add_local_trained_result(i, d, n)
+        out = OrderedDict((k, t.cpu().clone()) for k, t in server.aggregate().items())
+        st = server.optimizer_state()
+        assert st["step"] == r + 1
+        gold = _golden_state(arrays, r, names)
+        for k in names:
+            gu.assert_same(st["exp_avg"][k].cpu(), gold["exp_avg"][k].reshape(st["exp_avg"][k].shape), f"r{r} m {k}")
+            gu.assert_same(st["exp_avg_sq"][k].cpu(), gold["exp_avg_sq"][k].reshape(st["exp_avg_sq"][k].shape),
+                           f"r{r} v {k}")
+        # oracle, same inputs, IEEE sqrt: bit-exact
+        ostate = {k: (_golden_state(arrays, r - 1, names)["exp_avg"][k].numpy(),
+                      _golden_state(arrays, r - 1, names)["exp_avg_sq"][k].numpy()) for k in names} if r else {}
+        exp = orc.fedopt_adam_round(prev, names, raw, spec["lr"], ostate, r + 1, sqrt="ieee")
+        for k, t in out.items():
+            gu.assert_same(t, exp[k], f"r{r} oracle {k}")
+            e = gu.to_tensor(arrays[f"r{r}:{k}"], str(t.dtype).replace("torch.", ""), t.shape)
+            if k in names:
+                step = (e.double() - prev[k].double()).abs()
+                tol = torch.from_numpy(np.spacing(np.abs(e.numpy()))).double() + step * 2.0 ** -21
+                assert ((t.double() - e.double()).abs() <= tol).all(), f"r{r} {k}"
+                exact += int((_bits(t) == _bits(e)).sum())
+                total += t.numel()
+            else:
+                gu.assert_same(t, e, f"r{r} {k}")
+        prev = OrderedDict((k, gu.to_tensor(arrays[f"r{r}:{k}"], str(t.dtype).replace("torch.", ""), t.shape))
+                           for k, t in init.items())
+    assert exact >= 0.98 * total, (exact, total)
+
+
+def test_fused_adam_vs_oracle_large(cuda_device):
+    """Fused Adam at LoRA scale with a ragged tail, 3 rounds, every element
+    bit-exact against the C oracle (IEEE sqrt): moments and parameters."""
+    K, N = 16, 262_147
+    g = torch.Generator(device=cuda_device).manual_seed(9)
+    rows = torch.randn(K, (N + 63) // 64 * 64, generator=g, device=cuda_device) * 0.02
+    p = torch.randn(N, generator=g, device=cuda_device) * 0.02
+    m = torch.zeros(N, device=cuda_device)
+    v = torch.zeros(N, device=cuda_device)
+    ws = [(i + 1.0) for i in range(K)]
+    ws = [w / sum(ws) for w in ws]
+    d_w = kn.upload_f32(ws, cuda_device)
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    hp, hm, hv = p.cpu().numpy(), None, None
+    for r in range(3):
+        avg = orc.wsum([rows[i, :N].cpu() for i in range(K)], ws).numpy()
+        kn.wsum_fedopt_adam(d_ptrs, kn.weights_for(ws, torch.float32, cuda_device), K, N, p, m, v,
+                            kn.adam_scalars(0.01, 0.9, 0.999, 1e-8, r + 1), r == 0, True)
+        hp, hm, hv = orc.fedopt_adam(hp, avg, hm, hv, 0.01, r + 1, sqrt="ieee")
+        gu.assert_same(m.cpu(), torch.from_numpy(hm), f"r{r} exp_avg")
+        gu.assert_same(v.cpu(), torch.from_numpy(hv), f"r{r} exp_avg_sq")
+        gu.assert_same(p.cpu(), torch.from_numpy(hp), f"r{r} param")
+        rows.mul_(1.01)
+    assert d_w.numel() == K
+
+
+def test_optimizer_state_round_trip(cuda_device):
+    spec = cases.FEDOPT_ADAM_CASES[0]
+    init = cases.fedopt_global_init(spec)
+    a = FedOptServer(init, cases.FEDOPT_PARAMS, spec["K"], "adam", spec["lr"], 0.0, cuda_device)
+    gsd = init
+    for r in range(2):
+        for i, (n, d) in enumerate(cases.fedopt_round_inputs(spec, gsd, r)):
+            a.add_local_trained_result(i, d, n)
+        gsd = OrderedDict((k, t.cpu().clone()) for k, t in a.aggregate().items())
+    b = FedOptServer(gsd, cases.FEDOPT_PARAMS, spec["K"], "adam", spec["lr"], 0.0, cuda_device)
+    b.load_optimizer_state(a.optimizer_state())
+    raw = cases.fedopt_round_inputs(spec, gsd, 2)
+    for s in (a, b):
+        for i, (n, d) in enumerate(raw):
+            s.add_local_trained_result(i, d, n)
+    oa, ob = a.aggregate(), b.aggregate()
+    for k in oa:
+        gu.assert_same(oa[k].cpu(), ob[k].cpu(), k)
