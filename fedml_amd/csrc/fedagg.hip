@@ -405,18 +405,17 @@ struct AdamEpi {
   float w1, beta2, c2, bc2s, eps, nss;
   int first;  // exp_avg / exp_avg_sq are zero before torch's first step: skip their loads
   static constexpr int E = 4;
+  // p_old and exp_avg are prefetched before the client loop like SgdEpi's
+  // operands; exp_avg_sq is loaded in the epilogue (a third prefetched pack
+  // per V takes the kernel past 128 VGPRs: occupancy 3 instead of 4).
   struct Pre {
-    Pack<float, 4> p, m, v;
+    Pack<float, 4> p, m;
   };
   __device__ __forceinline__ Pre pre(int64_t off) const {
     Pre r;
     r.p = load_pack<float, true>(p + off);
     r.m = {};
-    r.v = {};
-    if (!first) {
-      r.m = load_pack<float, true>(m + off);
-      r.v = load_pack<float, true>(v + off);
-    }
+    if (!first) r.m = load_pack<float, true>(m + off);
     return r;
   }
   __device__ __forceinline__ float step1(float po, float avg, float* mm, float* vv) const {
@@ -430,10 +429,12 @@ struct AdamEpi {
   }
   __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E], const Pre& pr) const {
     float po[E], mo[E], vo[E];
+    Pack<float, 4> vp = {};
+    if (!first) vp = load_pack<float, true>(v + off);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       mo[e] = pr.m.v[e];
-      vo[e] = pr.v.v[e];
+      vo[e] = vp.v[e];
       po[e] = step1(pr.p.v[e], acc[e], &mo[e], &vo[e]);
     }
     store_pack<float, E>(p + off, po);
@@ -590,6 +591,17 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi, c
 template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI = StoreEpi<OP>,
           class WS = PtrW<typename OP::w_t>>
 __global__ __launch_bounds__(BS) void reduce_kernel(Seg<OP> s, EPI epi, WS w, int K) {
+  reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, int64_t(blockIdx.x) * BS * V);
+}
+
+// Reduction fused with the server Adam epilogue (AdamEpi): the
+// prefetched optimizer operands sit in VGPRs across the client loop; cap the
+// kernel at 128 VGPRs so 4 waves per SIMD stay resident (the epilogue
+// otherwise lands at 130 and 3 waves; SgdEpi fits without the cap, and
+// spills with it).
+template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI, class WS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void reduce_fused_kernel(
+    Seg<OP> s, EPI epi, WS w, int K) {
   reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, int64_t(blockIdx.x) * BS * V);
 }
 
@@ -1109,10 +1121,10 @@ int fedagg_wsum_fedopt_adam_f32(const float* const* d_src, const float* d_w, int
   auto go = [&](const auto& w) {
     using WS = std::decay_t<decltype(w)>;
     if (flags & FEDAGG_ALIGNED16) {
-      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
+      hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
                          dim3(C::BS), 0, st, s, epi, w, K);
     } else {
-      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
+      hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
                          dim3(C::BS), 0, st, s, epi, w, K);
     }
   };
