@@ -39,6 +39,7 @@
 #include <string>
 #include <thread>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "../../include/fedagg.h"
@@ -784,10 +785,15 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 // One lane per parameter element holds the column's K values in registers
 // (KMAX >= K slots).  The column is padded with -inf / +inf so that its lower
 // median always lands at the network's fixed middle slot (KMAX-1)/2; a
-// Batcher odd-even merge sorting network is then fully unrolled at compile
-// time, and since only that one output slot is used, the compiler deletes
-// every comparator that does not feed it.  Loads are 4 B per lane (256 B per
-// wave instruction), all K of them independent and in flight together.
+// pairwise sorting network is then fully unrolled at compile time, and since
+// only that one output slot is used, the compiler deletes every comparator
+// that does not feed it.  Loads are 4 B per lane (256 B per wave
+// instruction), all K of them independent and in flight together.  K == KMAX
+// (e.g. 128 clients) gets a kernel with no padding logic at all.
+//
+// VALU per element at K = 128 (gfx950 ISA): 2,017 v_min/v_max (+61 fused
+// min3/max3), 128 NaN compares; ~3,470 with the earlier Batcher network,
+// per-client 64-bit addressing and in-line first-NaN tracking.
 
 __device__ __forceinline__ void cmpx(float& a, float& b) {
   const float lo = fminf(a, b), hi = fmaxf(a, b);
@@ -795,40 +801,120 @@ __device__ __forceinline__ void cmpx(float& a, float& b) {
   b = hi;
 }
 
+// Parberry's pairwise sorting network on N slots, generated at compile time.
+// Pruned to the one output slot the median needs, it keeps 2,011 min/max at
+// N = 128 where Batcher's odd-even merge sort keeps 2,299 (same 1,471
+// comparators before pruning; the pairwise network's last stages feed fewer
+// slots).
+struct CmpPair {
+  int a, b;
+};
 template <int N>
-__device__ __forceinline__ void oem_sort(float (&a)[N]) {
-#pragma unroll
-  for (int p = 1; p < N; p += p)
-#pragma unroll
-    for (int k = p; k > 0; k /= 2)
-#pragma unroll
-      for (int j = k % p; j + k < N; j += k + k)
-#pragma unroll
-        for (int i = 0; i < k; ++i)
-          if (i + j + k < N && (i + j) / (p + p) == (i + j + k) / (p + p)) cmpx(a[i + j], a[i + j + k]);
+struct PairwiseNet {
+  // emit(a, b) for every comparator in network order; returns the count
+  template <class F>
+  static constexpr int walk(F emit) {
+    int m = 0;
+    int a = 1;
+    for (; a < N; a *= 2) {
+      int b = a, c = 0;
+      while (b < N) {
+        emit(m++, b - a, b);
+        ++b;
+        c = (c + 1) % a;
+        if (c == 0) b += a;
+      }
+    }
+    a /= 4;
+    for (int e = 1; a > 0; a /= 2, e = e * 2 + 1) {
+      for (int d = e; d > 0; d /= 2) {
+        int b = (d + 1) * a, c = 0;
+        while (b < N) {
+          emit(m++, b - d * a, b);
+          ++b;
+          c = (c + 1) % a;
+          if (c == 0) b += a;
+        }
+      }
+    }
+    return m;
+  }
+  static constexpr int M = walk([](int, int, int) {});
+  struct Table {
+    CmpPair p[M > 0 ? M : 1];
+  };
+  static constexpr Table make() {
+    Table t{};
+    walk([&t](int m, int x, int y) { t.p[m] = CmpPair{x, y}; });
+    return t;
+  }
+  static constexpr Table table = make();
+};
+
+template <int N, int I>
+__device__ __forceinline__ void net_cmp(float (&v)[N]) {
+  constexpr int A = PairwiseNet<N>::table.p[I].a, B = PairwiseNet<N>::table.p[I].b;
+  cmpx(v[A], v[B]);
+}
+template <int N, int... I>
+__device__ __forceinline__ void net_apply(float (&v)[N], std::integer_sequence<int, I...>) {
+  (net_cmp<N, I>(v), ...);
+}
+template <int N>
+__device__ __forceinline__ void pairwise_sort(float (&v)[N]) {
+  net_apply<N>(v, std::make_integer_sequence<int, PairwiseNet<N>::M>{});
 }
 
-template <int KMAX, int BS>
+template <int KMAX, bool FULL, int BS, bool PRIO = false>
 __global__ __launch_bounds__(BS) void median_kernel(const float* const* __restrict__ src, int K, int64_t N,
                                                     float* __restrict__ out) {
   const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;
   if (e >= N) return;
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // issue this wave's loads ahead of others' sorting
+  if constexpr (FULL) K = KMAX;  // K == KMAX: no padding, no per-client conditions
+  // The host guarantees N * 4 < 2^32: a 32-bit byte offset on each
+  // wave-uniform row base lets every load use the SGPR-base + VGPR-offset
+  // form, with no per-client 64-bit address arithmetic on the VALU.
+  const uint32_t boff = uint32_t(e) * 4u;
   const int below = (KMAX - 1) / 2 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
   float v[KMAX];
-#pragma unroll
-  for (int c = 0; c < KMAX; ++c)
-    v[c] = (c < K) ? __builtin_nontemporal_load(as_global(src[c]) + e)
-                   : ((c - K < below) ? -__builtin_huge_valf() : __builtin_huge_valf());
-  // torch returns the first NaN of the column (client order) if there is one
-  float nan_v = 0.f;
   bool has_nan = false;
 #pragma unroll
   for (int c = 0; c < KMAX; ++c) {
-    const bool n = (c < K) && __builtin_isnan(v[c]);
-    nan_v = (n && !has_nan) ? v[c] : nan_v;
-    has_nan = has_nan || n;
+    // Keep at most 16 row pointers live in SGPRs: without the barrier the
+    // scheduler hoists all K pointer loads to the top and spills them.
+    if (c % 16 == 0 && c) __builtin_amdgcn_sched_barrier(0);
+    // Padded slots (c >= K) load client K-1's element again (a cache hit on
+    // the line just requested) and select the pad value: no branches, so the
+    // pointer loads batch and nothing spills.
+    const int ci = (FULL || c < K) ? c : K - 1;
+    const auto row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
+    const float x =
+        __builtin_nontemporal_load(reinterpret_cast<const float __attribute__((address_space(1)))*>(row + boff));
+    // torch returns the first NaN of the column (client order) if there is
+    // one.  The common case pays one compare per client (on x itself, which
+    // also keeps CodeGenPrepare from turning the select below into a branch
+    // around a single-use load).
+    has_nan |= __builtin_isnan(x);
+    if constexpr (FULL)
+      v[c] = x;
+    else
+      v[c] = (c < K) ? x : ((c - K < below) ? -__builtin_huge_valf() : __builtin_huge_valf());
   }
-  oem_sort<KMAX>(v);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  // The search runs only in waves holding a NaN column (skipped on an empty
+  // exec mask otherwise).
+  float nan_v = 0.f;
+  if (has_nan) {
+    bool found = false;
+#pragma unroll
+    for (int c = 0; c < KMAX; ++c) {
+      const bool n = (FULL || c < K) && !found && __builtin_isnan(v[c]);
+      nan_v = n ? v[c] : nan_v;
+      found = found || n;
+    }
+  }
+  pairwise_sort<KMAX>(v);
   out[e] = has_nan ? nan_v : v[(KMAX - 1) / 2];
 }
 
@@ -837,7 +923,10 @@ int launch_median(const float* const* src, int K, int64_t N, float* out, hipStre
   constexpr int BS = 256;
   const int64_t grid = (N + BS - 1) / BS;
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N too large");
-  hipLaunchKernelGGL((median_kernel<KMAX, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
+  if (K == KMAX)
+    hipLaunchKernelGGL((median_kernel<KMAX, true, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
+  else
+    hipLaunchKernelGGL((median_kernel<KMAX, false, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
   return check_launch("fedagg_median_f32");
 }
 
@@ -1185,11 +1274,16 @@ int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_
   if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K must be >= 1 and N >= 0");
   if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: null pointer");
   if (N == 0) return FEDAGG_OK;
+  // the kernel addresses rows with 32-bit byte offsets
+  if (N > (int64_t(1) << 30)) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N > 2^30 elements per row");
   auto st = reinterpret_cast<hipStream_t>(stream);
   if (K <= 8) return launch_median<8>(d_src, K, N, d_out, st);
   if (K <= 16) return launch_median<16>(d_src, K, N, d_out, st);
+  if (K <= 24) return launch_median<24>(d_src, K, N, d_out, st);
   if (K <= 32) return launch_median<32>(d_src, K, N, d_out, st);
+  if (K <= 48) return launch_median<48>(d_src, K, N, d_out, st);
   if (K <= 64) return launch_median<64>(d_src, K, N, d_out, st);
+  if (K <= 96) return launch_median<96>(d_src, K, N, d_out, st);
   if (K <= 128) return launch_median<128>(d_src, K, N, d_out, st);
   return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K > 128 clients is not supported yet");
 }

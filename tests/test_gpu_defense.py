@@ -45,9 +45,10 @@ def test_defense_matches_reference(name, device_inputs, cuda_device):
     gu.assert_groups(OrderedDict((k, t.cpu()) for k, t in res.items()), meta, arrays, name)
 
 
-@pytest.mark.parametrize("K", [1, 2, 7, 8, 9, 16, 33, 64, 65, 100, 127, 128])
+@pytest.mark.parametrize("K", [1, 2, 7, 8, 9, 16, 17, 24, 33, 48, 64, 65, 96, 97, 100, 127, 128])
 def test_median_kernel_vs_oracle(K, cuda_device):
-    """Every KMAX bucket and padding split, with duplicates and infinities."""
+    """Every KMAX bucket (full and padded kernels), with duplicates and
+    infinities."""
     N = 20_011
     g = torch.Generator(device=cuda_device).manual_seed(K)
     rows = torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 TAG=${1:-r01}
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_${TAG}.log 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread> gpurun_out/pytest_gpu_${TAG}.log 2>&1 \
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 \
  && timeout -k 10 600 python bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err \
  && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" \
