@@ -131,13 +131,73 @@ def _cached_bucket(layout, K: int, device: torch.device, acc: str) -> ClientBuck
     return b
 
 
+def _walker():
+    """The native dict walker (csrc/walker.cpp), or None if it is not built;
+    without it the Python walk below does the same job, slower."""
+    global _WALKER
+    if _WALKER is False:
+        try:
+            import importlib.util
+            import os
+
+            from . import build as fbuild
+
+            spec = importlib.util.spec_from_file_location("_fedagg_walker", fbuild.WALKER_OUT)
+            if spec is None or not os.path.exists(fbuild.WALKER_OUT):
+                raise ImportError(fbuild.WALKER_OUT)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            _WALKER = mod
+        except (ImportError, OSError):
+            _WALKER = None
+    return _WALKER
+
+
+_WALKER = False
+_CODE_DT = {nat.DT_F32: torch.float32, nat.DT_BF16: torch.bfloat16, nat.DT_F16: torch.float16,
+            nat.DT_I64: torch.int64}
+
+
+def _reduce_device_walked(walked, dicts, keys, weights, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
+    """Every key a contiguous, 16-byte aligned device tensor of one device
+    (what the native walker verified): one multi-tensor launch per dtype with
+    the walker's pointer tables, no per-tensor Python work."""
+    dev_idx, codes, numels, tables = walked
+    device = torch.device("cuda", dev_idx)
+    K = len(dicts)
+    d0 = dicts[0]
+    results: Dict[str, torch.Tensor] = {}
+    by_code: Dict[int, Tuple[List[int], List[int]]] = OrderedDict()
+    with torch.cuda.device(device):
+        for k, code in zip(keys, codes):
+            out = torch.empty(d0[k].shape, dtype=torch.float32 if code == nat.DT_I64 else _CODE_DT[code],
+                              device=device)
+            results[k] = out
+            ns, ops = by_code.setdefault(code, ([], []))
+            ns.append(out.numel())
+            ops.append(out.data_ptr())
+        if any(p & 15 for _, ops in by_code.values() for p in ops):
+            return None  # the caching allocator never does this; take the general path if it ever does
+        w32 = kn.upload_f32(weights, device)
+        for code, (ns, ops) in by_code.items():
+            kn.MultiPlan(ns, _CODE_DT[code], acc_mode).launch(tables[code], ops, w32, K, device)
+    return OrderedDict((k, results[k]) for k in keys)
+
+
 def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights: Sequence[float], args
                     ) -> "OrderedDict[str, torch.Tensor]":
     """avg[k] = Σ_i fl(p_i[k] · w_i) in client order for every key (the FedAvg
     inner loops, agg_operator.py:36-44), on the GPU.  Returns results on the
     inputs' device."""
-    per_key = _gather(dicts, keys)
     acc_mode = _acc_mode(args)
+    w = _walker()
+    if w is not None and keys:
+        walked = w.walk(list(dicts), list(keys))
+        if walked is not None:
+            res = _reduce_device_walked(walked, dicts, keys, weights, acc_mode)
+            if res is not None:
+                return res
+    per_key = _gather(dicts, keys)
     K = len(dicts)
     results: Dict[str, torch.Tensor] = {}
     host_keys = [k for k in keys if not per_key[k][0].is_cuda]

@@ -10,11 +10,14 @@ import os
 import shutil
 import subprocess
 import sys
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "fedagg.hip")
 OUT_DIR = os.path.join(HERE, "lib")
 OUT = os.path.join(OUT_DIR, "libfedagg.so")
+WALKER_SRC = os.path.join(HERE, "csrc", "walker.cpp")
+WALKER_OUT = os.path.join(OUT_DIR, "_fedagg_walker" + sysconfig.get_config_var("EXT_SUFFIX"))
 ARCH = os.environ.get("FEDAGG_ARCH", "gfx950")
 
 HIPCC_FLAGS = [
@@ -48,7 +51,32 @@ def needs_rebuild() -> bool:
     return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps if os.path.exists(d))
 
 
+def build_walker(force: bool = False, verbose: bool = False) -> str:
+    """The host-side dict walker (csrc/walker.cpp): a CPython module built
+    against torch's headers with the system C++ compiler (no device code)."""
+    if not force and os.path.exists(WALKER_OUT) and \
+            os.path.getmtime(WALKER_OUT) >= max(os.path.getmtime(WALKER_SRC), os.path.getmtime(__file__)):
+        return WALKER_OUT
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    os.makedirs(OUT_DIR, exist_ok=True)
+    tmp = WALKER_OUT + ".tmp"
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I" + sysconfig.get_paths()["include"],
+           *("-I" + d for d in ce.include_paths()), WALKER_SRC,
+           *("-L" + d for d in ce.library_paths()), "-ltorch_python", "-ltorch", "-lc10",
+           *("-Wl,-rpath," + d for d in ce.library_paths()), "-o", tmp]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, WALKER_OUT)
+    return WALKER_OUT
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    build_walker(force=force, verbose=verbose)
     if not force and not needs_rebuild():
         return OUT
     os.makedirs(OUT_DIR, exist_ok=True)

@@ -163,16 +163,24 @@ class MultiPlan:
         self.block_begin = begin
         self.total_blocks = begin[-1]
 
-    def launch(self, src_ptrs: List[int], out_ptrs: List[int], d_w: torch.Tensor, K: int,
+    def launch(self, src_ptrs, out_ptrs: List[int], d_w: torch.Tensor, K: int,
                device: torch.device) -> List[torch.Tensor]:
-        """src_ptrs is the flattened [T][K] table.  Returns the device tables,
-        which must stay referenced until the launch has been enqueued."""
+        """src_ptrs is the flattened [T][K] table (a list of ints, or an int64
+        numpy array / bytes as the native dict walker produces it).  Returns
+        the device tables, which must stay referenced until the launch has
+        been enqueued."""
         T = len(self.numels)
+        if isinstance(src_ptrs, (bytes, bytearray)):
+            src_ptrs = np.frombuffer(src_ptrs, dtype=np.int64)
         if len(src_ptrs) != T * K or len(out_ptrs) != T:
             raise ValueError("MultiPlan.launch: table sizes do not match the plan")
         # numels and block starts travel in one upload, pointers in another
         d_meta = upload_i64(self.numels + self.block_begin, device)
-        d_tab = upload_i64(list(src_ptrs) + list(out_ptrs), device)
+        if isinstance(src_ptrs, np.ndarray):
+            tab = np.concatenate([src_ptrs.astype(np.int64, copy=False), np.asarray(out_ptrs, dtype=np.int64)])
+        else:
+            tab = list(src_ptrs) + list(out_ptrs)
+        d_tab = upload_i64(tab, device)
         nat.check(nat.lib().fedagg_wsum_multi(self.dt, self.acc_mode, d_tab.data_ptr(), d_tab.data_ptr() + 8 * T * K,
                                               d_meta.data_ptr(), d_meta.data_ptr() + 8 * T, T, d_w.data_ptr(), K,
                                               self.total_blocks, nat.stream_handle()), "wsum_multi")

@@ -130,6 +130,34 @@ def test_resnet50_low_precision_multi_tensor_vs_oracle(dtype, cuda_device):
         gu.assert_same(res[k].cpu(), exp[k], k)
 
 
+def test_native_walker_takes_device_dicts(cuda_device):
+    """Device-resident dicts go through the native walker's pointer tables;
+    anything irregular (here a non-contiguous client tensor) falls back to the
+    Python walk, with the same result."""
+    from fedml_amd import _native as nat
+
+    w = ao._walker()
+    assert w is not None
+    entries = shapes.resnet50()
+    raw = _to_device(host_clients(entries, 3, seed=2, round_idx=1), cuda_device)
+    walked = w.walk([d for _, d in raw], list(raw[0][1].keys()))
+    assert walked is not None
+    dev, codes, numels, tables = walked
+    assert dev == cuda_device.index or dev == 0
+    assert set(tables) == {nat.DT_F32, nat.DT_I64}
+    assert len(tables[nat.DT_F32]) == 8 * 3 * codes.count(nat.DT_F32)
+    assert numels == [int(torch.Size(s).numel()) for _, s, _ in entries]
+    args = type("A", (), {"federated_optimizer": "FedAvg"})()
+    exp = orc.agg(args, [(n, OrderedDict((k, t.cpu()) for k, t in d.items())) for n, d in raw])
+    k = "fc.weight"
+    t = raw[1][1][k]
+    raw[1][1][k] = t.t().contiguous().t()  # same values, not contiguous
+    assert w.walk([d for _, d in raw], list(raw[0][1].keys())) is None
+    res = ao.FedMLAggOperator.agg(args, raw)
+    for key in exp:
+        gu.assert_same(res[key].cpu(), exp[key], key)
+
+
 def test_unaligned_views_take_scalar_path(cuda_device):
     """Tensors that are views at odd element offsets (not 16-byte aligned)."""
     K, N = 5, 4099

@@ -172,3 +172,25 @@ def test_host_unpack_scatters_exactly(lib):
                                   (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*sizes), n, 8) == 0
     for d, off in zip(dsts, offs):
         assert np.array_equal(d, src[off:off + d.size])
+
+
+def test_dict_walker_builds_and_declines_host_inputs():
+    """The native dict walker (csrc/walker.cpp) only ever takes the all-device
+    fast path; host tensors and missing keys return None so the Python walk
+    handles them (and raises the reference's KeyError)."""
+    from fedml_amd import agg_operator as ao
+
+    w = ao._walker()
+    assert w is not None, "build the walker: python -m fedml_amd.build"
+    assert w.walk([OrderedDict(a=torch.ones(3))], ["a"]) is None
+    assert w.walk([OrderedDict(a=torch.ones(3))], ["b"]) is None
+    assert w.walk([], ["a"]) is None
+    assert w.walk([OrderedDict(a=1)], ["a"]) is None
+
+    class Custom(dict):
+        def __getitem__(self, k):  # overridden lookup: never walked natively
+            return super().__getitem__(k)
+
+    assert w.walk([Custom(a=torch.ones(3))], ["a"]) is None
+    with pytest.raises(TypeError):
+        w.walk([OrderedDict()], [["unhashable"]])

@@ -16,6 +16,7 @@ import time
 from collections import OrderedDict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import torch  # noqa: E402
 
@@ -59,7 +60,11 @@ def main():
         if r:
             times.append((t1 - t0, t2 - t0))
             gpu.append(e0.elapsed_time(e1))
-    res = {"K": a.K, "tensors": a.K * len(ents),
+    # host-side breakdown of the native-walker path (agg_operator._reduce_device_walked)
+    import agg_breakdown  # noqa: F401  (tools/agg_breakdown.py)
+
+    bd = agg_breakdown.breakdown([(raw[0][0], OrderedDict(c0))] + raw[1:], a.reps)
+    res = {"K": a.K, "tensors": a.K * len(ents), "breakdown_ms": bd,
            "host_enqueue_ms_median": sorted(t[0] for t in times)[len(times) // 2] * 1e3,
            "wall_to_done_ms_median": sorted(t[1] for t in times)[len(times) // 2] * 1e3,
            "gpu_window_ms_median": sorted(gpu)[len(gpu) // 2]}
