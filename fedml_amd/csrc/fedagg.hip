@@ -646,6 +646,15 @@ template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; st
 struct SmallCfg { static constexpr int U = 16, V = 1, BS = 64; static constexpr bool NT = true; };
 constexpr int64_t kSmallBelowBlocks = 1024;  // shipped-tile workgroups below which SmallCfg is used
 
+// Mid-sized launches (1,024 to 4,096 tiles: every tile resident at once or
+// nearly so) stream one client at a time per lane (56 VGPRs instead of 94).
+// tools/tune_wsum.py and tools/adam_probe.py on MI355X: 64 x 4.19M (config 5)
+// FedAvg 0.160 vs 0.171 ms, fused SGD 0.168 vs 0.177 ms, fused Adam 0.175 vs
+// 0.197 ms; 128 x 4.19M 0.317 vs 0.348 ms; 128 x 16.8M 1.271 vs 1.298 ms.  At
+// config 3 (6,253 tiles) U4V4 stays ahead (2.047 vs 2.067 ms).
+struct MidCfg { static constexpr int U = 1, V = 4, BS = 256; static constexpr bool NT = true; };
+constexpr int64_t kMidUpToBlocks = 4096;
+
 template <class OP>
 int64_t blocks_for(int64_t numel) {
   constexpr int E = 16 / sizeof(typename OP::in_t);
@@ -677,8 +686,11 @@ int launch_uvn(const typename OP::in_t* const* src, const WS& w, int32_t K, int6
 template <class OP, class WS>
 int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t N, typename OP::out_t* o, bool al,
               hipStream_t st, const char* name) {
-  if (blocks_for<OP>(N) < kSmallBelowBlocks)
+  const int64_t blocks = blocks_for<OP>(N);
+  if (blocks < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
+  if (blocks <= kMidUpToBlocks)
+    return launch_uvn<OP, MidCfg::U, MidCfg::V, MidCfg::NT, MidCfg::BS, WS>(s, w, K, N, o, al, st, name);
   return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS, WS>(s, w, K, N, o, al, st, name);
 }
 
@@ -702,9 +714,12 @@ int launch_epi_cfg(const Seg<OP>& s, const EPI& epi, const WS& w, int32_t K, boo
 template <class OP, class EPI, class WS>
 int launch_epi(const Seg<OP>& s, const EPI& epi, const WS& w, int32_t K, bool aligned, hipStream_t st,
                const char* name) {
-  if (blocks_for<OP>(s.numel) < kSmallBelowBlocks)
+  const int64_t blocks = blocks_for<OP>(s.numel);
+  if (blocks < kSmallBelowBlocks)
     return launch_epi_cfg<OP, EPI, WS, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS>(s, epi, w, K, aligned,
                                                                                             st, name);
+  if (blocks <= kMidUpToBlocks)
+    return launch_epi_cfg<OP, EPI, WS, MidCfg::U, MidCfg::V, MidCfg::NT, MidCfg::BS>(s, epi, w, K, aligned, st, name);
   return launch_epi_cfg<OP, EPI, WS, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS>(s, epi, w, K, aligned, st,
                                                                                       name);
 }
@@ -773,6 +788,8 @@ const Variant kVariants[] = {
     {"U4V4", variant_fn<4, 4, false, 256>},
     {"U4V4nt_p4", persistent_fn<4, 4, 256, 4>},   {"U4V4nt_p5", persistent_fn<4, 4, 256, 5>},
     {"U4V4nt_p8", persistent_fn<4, 4, 256, 8>},   {"U4V2nt_p8", persistent_fn<4, 2, 256, 8>},
+    {"U1V4nt", variant_fn<1, 4, true, 256>},      {"U1V2nt", variant_fn<1, 2, true, 256>},
+    {"U2V2nt", variant_fn<2, 2, true, 256>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -1012,6 +1029,35 @@ int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, c
 // ===========================================================================
 
 namespace {
+// FedAvg fused with a server-optimizer epilogue (SgdEpi / AdamEpi): the tile
+// configuration by size, as launch_ws picks it for plain FedAvg.  FUSED_CAP
+// selects reduce_fused_kernel (capped at 128 VGPRs for Adam's operands).
+template <bool FUSED_CAP, class C, class EPI, class WS>
+void launch_fused_cfg(const Seg<OpF32>& s, const EPI& epi, const WS& w, int32_t K, bool aligned, hipStream_t st) {
+  const int64_t grid = ((s.numel + 3) / 4 + int64_t(C::BS) * C::V - 1) / (int64_t(C::BS) * C::V);
+  const dim3 g{unsigned(grid)}, b{unsigned(C::BS)};
+  if (FUSED_CAP) {
+    if (aligned)
+      hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, EPI, WS>), g, b, 0, st, s, epi, w, K);
+    else
+      hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, EPI, WS>), g, b, 0, st, s, epi, w,
+                         K);
+  } else {
+    if (aligned)
+      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, EPI, WS>), g, b, 0, st, s, epi, w, K);
+    else
+      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, EPI, WS>), g, b, 0, st, s, epi, w, K);
+  }
+}
+
+template <bool FUSED_CAP, class EPI, class WS>
+void launch_fused(const Seg<OpF32>& s, const EPI& epi, const WS& w, int32_t K, bool aligned, hipStream_t st) {
+  if (blocks_for<OpF32>(s.numel) <= kMidUpToBlocks)
+    launch_fused_cfg<FUSED_CAP, MidCfg>(s, epi, w, K, aligned, st);
+  else
+    launch_fused_cfg<FUSED_CAP, Cfg<OpF32>>(s, epi, w, K, aligned, st);
+}
+
 template <class OP>
 int launch_multi(const void* const* d_src, void* const* d_out, const int64_t* d_numel, const int64_t* d_block_begin,
                  int32_t T, const float* d_w, int32_t K, int64_t total_blocks, hipStream_t st) {
@@ -1149,29 +1195,19 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
   if (!d_src || !d_w || !d_param || (momentum != 0.0f && !d_mom))
     return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: null pointer");
   if (N == 0) return FEDAGG_OK;
-  using C = Cfg<OpF32>;
   const int64_t grid = blocks_for<OpF32>(N);
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: N too large");
   Seg<OpF32> s{d_src, N};
   SgdEpi epi{d_param, momentum != 0.0f ? d_mom : nullptr, -lr, momentum, first_step};
   auto st = reinterpret_cast<hipStream_t>(stream);
-  auto go = [&](const auto& w) {
-    using WS = std::decay_t<decltype(w)>;
-    if (flags & FEDAGG_ALIGNED16) {
-      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, SgdEpi, WS>), dim3(unsigned(grid)),
-                         dim3(C::BS), 0, st, s, epi, w, K);
-    } else {
-      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, SgdEpi, WS>), dim3(unsigned(grid)),
-                         dim3(C::BS), 0, st, s, epi, w, K);
-    }
-  };
+  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
   if (flags & FEDAGG_HOST_WEIGHTS) {
     InlW<float> iw;
     if (!inline_weights<float>(d_w, K, &iw))
       return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
-    go(iw);
+    launch_fused<false>(s, epi, iw, K, aligned, st);
   } else {
-    go(PtrW<float>{d_w});
+    launch_fused<false>(s, epi, PtrW<float>{d_w}, K, aligned, st);
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
 }
@@ -1200,30 +1236,20 @@ int fedagg_wsum_fedopt_adam_f32(const float* const* d_src, const float* d_w, int
   if (!d_src || !d_w || !d_param || !d_exp_avg || !d_exp_avg_sq || !scalars6)
     return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adam_f32: null pointer");
   if (N == 0) return FEDAGG_OK;
-  using C = Cfg<OpF32>;
   const int64_t grid = blocks_for<OpF32>(N);
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adam_f32: N too large");
   Seg<OpF32> s{d_src, N};
   AdamEpi epi{d_param, d_exp_avg, d_exp_avg_sq, scalars6[0], scalars6[1], scalars6[2],
               scalars6[3], scalars6[4], scalars6[5], first_step};
   auto st = reinterpret_cast<hipStream_t>(stream);
-  auto go = [&](const auto& w) {
-    using WS = std::decay_t<decltype(w)>;
-    if (flags & FEDAGG_ALIGNED16) {
-      hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
-                         dim3(C::BS), 0, st, s, epi, w, K);
-    } else {
-      hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, AdamEpi, WS>), dim3(unsigned(grid)),
-                         dim3(C::BS), 0, st, s, epi, w, K);
-    }
-  };
+  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
   if (flags & FEDAGG_HOST_WEIGHTS) {
     InlW<float> iw;
     if (!inline_weights<float>(d_w, K, &iw))
       return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adam_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
-    go(iw);
+    launch_fused<true>(s, epi, iw, K, aligned, st);
   } else {
-    go(PtrW<float>{d_w});
+    launch_fused<true>(s, epi, PtrW<float>{d_w}, K, aligned, st);
   }
   return check_launch("fedagg_wsum_fedopt_adam_f32");
 }

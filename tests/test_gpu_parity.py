@@ -192,6 +192,24 @@ def test_headline_shape_sampled_columns(dtype, cuda_device):
     gu.assert_same(out[idx].cpu(), exp, f"headline {dtype}")
 
 
+@pytest.mark.parametrize("dtype,N", [(torch.float32, 4_194_305), (torch.float32, 16_777_216),
+                                     (torch.bfloat16, 8_388_613), (torch.float16, 8_390_000)])
+def test_mid_size_tiles_vs_oracle(dtype, N, cuda_device):
+    """Launches of 1,025..4,096 tiles take the one-client-per-step tile
+    configuration (MidCfg); every element checked against the oracle,
+    including the ragged tail."""
+    K = 9
+    g = torch.Generator(device=cuda_device).manual_seed(N % 1000)
+    rows = (torch.randn((K, N), generator=g, device=cuda_device) * 0.05).to(dtype)
+    ns = [int(v) for v in np.random.default_rng(N % 97).integers(100, 1001, K)]
+    ws = [n / sum(ns) for n in ns]
+    out = torch.empty(N, dtype=dtype, device=cuda_device)
+    kn.wsum_tensors([rows[i] for i in range(K)], ws, out)
+    host = rows.cpu()
+    exp = orc.wsum([host[i] for i in range(K)], ws)
+    gu.assert_same(out.cpu(), exp, f"mid {dtype} {N}")
+
+
 def test_bf16_fp32_accumulate_tolerance(cuda_device):
     """fedagg_low_precision_acc='fp32': within one bf16 rounding of the exact
     (fp64) weighted mean, |err| <= 2^-8 * |Σ w_i p_i| + 2^-133 (one final RNE)."""
