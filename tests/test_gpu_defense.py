@@ -77,10 +77,45 @@ def test_median_headline_shape_sampled(cuda_device):
     gu.assert_same(out[idx].cpu(), torch.from_numpy(exp), "median headline")
 
 
+@pytest.mark.parametrize("K", [129, 200, 255, 256, 257, 512, 700, 1024])
+def test_median_radix_kernel_vs_oracle(K, cuda_device):
+    """More than 128 clients (LDS tile + radix select): every KCAP bucket and a
+    ragged last tile, with duplicates, infinities, NaN columns and -0.0."""
+    N = 3_001
+    g = torch.Generator(device=cuda_device).manual_seed(K)
+    rows = torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125
+    rows[:, 17:29] = torch.randn(K, 12, generator=g, device=cuda_device)  # distinct values
+    rows[:, :7] = float("inf")
+    rows[:, 7:9] = -float("inf")
+    rows[K // 2, 100:110] = float("nan")
+    rows[K - 1, 105:115] = -float("nan")
+    rows[:, 200:203] = -0.0
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, device=cuda_device)
+    dfn.median_f32(d_ptrs, K, N, out)
+    exp = orc.lower_median_cols(rows.cpu().numpy())
+    gu.assert_same(out.cpu(), torch.from_numpy(exp), f"median K={K}")
+
+
+def test_median_radix_large_sampled(cuda_device):
+    """512 clients x 4M fp32 (the config-4 client count): 100,000 random
+    columns plus the ragged tail against the oracle."""
+    K, N = 512, 4_000_037
+    g = torch.Generator(device=cuda_device).manual_seed(5)
+    rows = torch.randn((K, N), generator=g, device=cuda_device) * 0.05
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, device=cuda_device)
+    dfn.median_f32(d_ptrs, K, N, out)
+    idx = torch.cat([torch.randint(0, N, (100_000,), generator=torch.Generator().manual_seed(4)),
+                     torch.arange(N - 40, N)]).to(cuda_device)
+    exp = orc.lower_median_cols(rows[:, idx].cpu().numpy())
+    gu.assert_same(out[idx].cpu(), torch.from_numpy(exp), "median K=512 sampled")
+
+
 def test_median_rejects_too_many_clients(cuda_device):
     from fedml_amd import _native as nat
 
-    rows = torch.zeros(129, 64, device=cuda_device)
-    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(129)], cuda_device)
+    rows = torch.zeros(1025, 64, device=cuda_device)
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(1025)], cuda_device)
     with pytest.raises(nat.FedAggNativeError):
-        dfn.median_f32(d_ptrs, 129, 64, torch.empty(64, device=cuda_device))
+        dfn.median_f32(d_ptrs, 1025, 64, torch.empty(64, device=cuda_device))

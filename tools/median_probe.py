@@ -75,6 +75,29 @@ def main():
         ms = statistics.median(res[name])
         summary[name] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
                          "compute_only_ms": round(statistics.median(res_c[name]), 4)}
+    # more than 128 clients: the product entry point (LDS tile + radix select)
+    del rows, tab, same, out
+    torch.cuda.empty_cache()
+    from fedml_amd import defense as dfn
+
+    N2 = 4_000_000
+    for K2 in (256, 512, 1024):
+        rows = torch.randn((K2, N2), device=dev) * 0.05
+        tab = kn.upload_i64([rows[i].data_ptr() for i in range(K2)], dev)
+        out = torch.empty(N2, device=dev)
+        dfn.median_f32(tab, K2, N2, out)
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dfn.median_f32(tab, K2, N2, out)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        ms = statistics.median(ts)
+        summary[f"radix_K{K2}_N{N2}"] = {"ms": round(ms, 4), "GBps": round((K2 + 1) * N2 * 4 / ms / 1e6, 1)}
+        del rows, tab, out
+        torch.cuda.empty_cache()
     print(json.dumps(summary, indent=1))
     os.makedirs("gpurun_out", exist_ok=True)
     json.dump(summary, open("gpurun_out/median_probe.json", "w"), indent=1)
