@@ -60,9 +60,9 @@ def parse():
     ap.add_argument("--chunks", type=int, default=8, help="client mode: reduce-scatter pipeline depth")
     ap.add_argument("--acc", default="reference", choices=["reference", "fp32"],
                     help="bf16/f16 accumulation: torch's per-op chain (bit-exact) or fp32")
-    ap.add_argument("--fedopt", nargs="?", const="sgd", default=None, choices=["sgd", "adam"],
+    ap.add_argument("--fedopt", nargs="?", const="sgd", default=None, choices=["sgd", "adam", "adagrad"],
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
-                         "or Adam lr=1.0 with torch defaults)")
+                         "or Adam / Adagrad lr=1.0 with torch defaults)")
     ap.add_argument("--op", default="fedavg", choices=["fedavg", "median"],
                     help="1 GPU: the reduction measured (median = the wise_median defense kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -290,8 +290,8 @@ def main():
             "elements_per_client": n_elems,
             "layout": "ClientBucket rows [K, L] per dtype, 256-B aligned rows",
             "low_precision_acc": a.acc,
-            "server_step": ({"sgd": "SGD lr=1.0 momentum=0.9 fused", "adam": "Adam lr=1.0 betas=(0.9,0.999) fused"}
-                            [a.fedopt] if server is not None else None),
+            "server_step": ({"sgd": "SGD lr=1.0 momentum=0.9 fused", "adam": "Adam lr=1.0 betas=(0.9,0.999) fused",
+                             "adagrad": "Adagrad lr=1.0 eps=1e-10 fused"}[a.fedopt] if server is not None else None),
             "parallelism": {"single": "1 GPU", "client": f"client-axis x{world}, RCCL reduce-scatter, "
                                                          f"{a.chunks}-chunk pipeline",
                             "param": f"parameter-axis x{world}, no collective"}[mode],
@@ -304,7 +304,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "kernel": ("median_kernel<128>" if a.op == "median" else
-                       ("reduce_fused_kernel<OpF32,AdamEpi>" if a.fedopt == "adam" else "reduce_kernel<OpF32,SgdEpi>")
+                       ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adagrad": "reduce_kernel<OpF32,AdagradEpi>"}
+                        .get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>"))
                        + " (FedAvg+server step fused)"
                        if server is not None else
                        f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step"),

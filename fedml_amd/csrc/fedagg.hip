@@ -451,6 +451,47 @@ struct AdamEpi {
   }
 };
 
+// Fused server Adagrad step (sp/fedopt/fedopt_api.py:121-130 with
+// torch.optim.Adagrad's single-tensor CPU path: weight_decay 0,
+// initial_accumulator_value 0 before the first step).  Per element:
+//   g = p_old - avg
+//   sum = fma(g, g, sum)                  addcmul_(g, g, value=1), fused
+//   p = p_old + fl(neg_clr * g) / (sqrt(sum) + eps)   addcdiv_, not fused
+// neg_clr = -lr / (1 + (step-1) * lr_decay) as fp32 (host side).
+struct AdagradEpi {
+  float* p;
+  float* sum;
+  float neg_clr, eps;
+  static constexpr int E = 4;
+  struct Pre {
+    Pack<float, 4> p, s;
+  };
+  __device__ __forceinline__ Pre pre(int64_t off) const {
+    return {load_pack<float, true>(p + off), load_pack<float, true>(sum + off)};
+  }
+  __device__ __forceinline__ float step1(float po, float avg, float* ss) const {
+    const float g = po - avg;
+    *ss = __builtin_fmaf(g, g, *ss);
+    const float std_ = __builtin_sqrtf(*ss) + eps;
+    return po + (neg_clr * g) / std_;
+  }
+  __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E], const Pre& pr) const {
+    float po[E], so[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      so[e] = pr.s.v[e];
+      po[e] = step1(pr.p.v[e], acc[e], &so[e]);
+    }
+    store_pack<float, E>(p + off, po);
+    store_pack<float, E>(sum + off, so);
+  }
+  __device__ __forceinline__ void one(int64_t e, float a) const {
+    float ss = sum[e];
+    p[e] = step1(p[e], a, &ss);
+    sum[e] = ss;
+  }
+};
+
 // LightSecAgg model reconstruction epilogue
 // (cross_silo/lightsecagg/lsa_fedml_aggregator.py:139-166 with
 // core/mpc/lightsecagg.py:157-182): on the wrapping int64 client sum
@@ -1381,6 +1422,29 @@ int fedagg_wsum_fedopt_adam_f32(const float* const* d_src, const float* d_w, int
     launch_fused<true>(s, epi, PtrW<float>{d_w}, K, aligned, st);
   }
   return check_launch("fedagg_wsum_fedopt_adam_f32");
+}
+
+int fedagg_wsum_fedopt_adagrad_f32(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float* d_param,
+                                   float* d_sum, float clr, float eps, uint32_t flags, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adagrad_f32: K must be >= 1 and N >= 0");
+  if (!d_src || !d_w || !d_param || !d_sum)
+    return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adagrad_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  const int64_t grid = blocks_for<OpF32>(N);
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adagrad_f32: N too large");
+  Seg<OpF32> s{d_src, N};
+  AdagradEpi epi{d_param, d_sum, -clr, eps};
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
+  if (flags & FEDAGG_HOST_WEIGHTS) {
+    InlW<float> iw;
+    if (!inline_weights<float>(d_w, K, &iw))
+      return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adagrad_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
+    launch_fused<false>(s, epi, iw, K, aligned, st);
+  } else {
+    launch_fused<false>(s, epi, PtrW<float>{d_w}, K, aligned, st);
+  }
+  return check_launch("fedagg_wsum_fedopt_adagrad_f32");
 }
 
 int fedagg_round_f32(int32_t dtype, const float* d_in, int64_t N, void* d_out, fedagg_stream_t stream) {

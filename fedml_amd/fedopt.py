@@ -23,6 +23,11 @@ Supported server optimizers (OptRepo names, optrepo.py:10); parameters are fp32:
           exp_avg_sq are bit-identical to torch's CPU Adam, the parameters
           differ only where torch's CPU sqrt is not correctly rounded
           (tests/test_gpu_fedopt.py).
+  "adagrad" torch.optim.Adagrad with its defaults (lr_decay 0, eps 1e-10,
+          initial_accumulator_value 0) and lr=server_lr, the SP FedOptAPI's
+          construction again (FedAdagrad).  Fused like Adam's
+          (fedagg_wsum_fedopt_adagrad_f32); state_sum is bit-identical to
+          torch's, parameters carry the same sqrt caveat.
 
 Device layout: the round's updates sit in a ClientBucket; the global model
 and the momentum buffers are flat fp32 vectors with the bucket's fp32 layout.
@@ -47,13 +52,14 @@ class FedOptServer:
                  worker_num: int, server_optimizer: str = "sgd", server_lr: float = 1.0,
                  server_momentum: float = 0.0, device=None):
         self.optimizer = server_optimizer.lower()
-        if self.optimizer not in ("sgd", "adam"):
-            raise NotImplementedError(f"server_optimizer {server_optimizer!r}: 'sgd' (with momentum) and 'adam' "
-                                      "are fused")
+        if self.optimizer not in ("sgd", "adam", "adagrad"):
+            raise NotImplementedError(f"server_optimizer {server_optimizer!r}: 'sgd' (with momentum), 'adam' and "
+                                      "'adagrad' are fused")
         self.lr = float(server_lr)
         self.momentum = float(server_momentum) if self.optimizer == "sgd" else 0.0
-        # torch.optim.Adam defaults (sp/fedopt/fedopt_api.py:79-85 passes lr only)
-        self.betas, self.eps = (0.9, 0.999), 1e-8
+        # torch.optim.Adam / Adagrad defaults (sp/fedopt/fedopt_api.py:79-85 passes lr only)
+        self.betas, self.eps = (0.9, 0.999), (1e-10 if self.optimizer == "adagrad" else 1e-8)
+        self.lr_decay = 0.0
         self.step_count = 0
         self.worker_num = worker_num
         self.param_names = list(param_names)
@@ -77,6 +83,8 @@ class FedOptServer:
             adam = f32 and self.optimizer == "adam"
             self.exp_avg = torch.zeros_like(self.global_flat[torch.float32]) if adam else None
             self.exp_avg_sq = torch.zeros_like(self.global_flat[torch.float32]) if adam else None
+            adagrad = f32 and self.optimizer == "adagrad"
+            self.state_sum = torch.zeros_like(self.global_flat[torch.float32]) if adagrad else None
         self.first_step = True
         self._views: Optional["OrderedDict[str, torch.Tensor]"] = None
         self.runs: List[Tuple[bool, int, int]] = self._runs(f32) if f32 else []
@@ -131,8 +139,13 @@ class FedOptServer:
                 if self.optimizer == "adam" else None
             if events is not None:
                 events[0].record()
+            # torch's Adagrad: clr = lr / (1 + (step - 1) * lr_decay), in double
+            clr = self.lr / (1 + (step - 1) * self.lr_decay)
             for (is_param, lo, hi), d_ptrs in zip(self.runs, self.run_ptrs):
-                if is_param and sc is not None:
+                if is_param and self.optimizer == "adagrad":
+                    kn.wsum_fedopt_adagrad(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], clr, self.eps,
+                                           True)
+                elif is_param and sc is not None:
                     kn.wsum_fedopt_adam(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
                                         self.exp_avg_sq[lo:hi], sc, self.first_step, True)
                 elif is_param:
@@ -166,23 +179,29 @@ class FedOptServer:
     def optimizer_state(self) -> Dict[str, object]:
         """Per named parameter, the state torch's optimizer would hold after the
         same rounds: {"step": n, <buffer>: {name: tensor}} with buffer
-        "momentum_buffer" (sgd with momentum) or "exp_avg" / "exp_avg_sq"
-        (adam).  Copies; for checkpointing and parity checks."""
+        "momentum_buffer" (sgd with momentum), "exp_avg" / "exp_avg_sq"
+        (adam) or "sum" (adagrad).  Copies; for checkpointing and parity checks."""
         out: Dict[str, object] = {"step": self.step_count}
-        bufs = {"momentum_buffer": self.mom} if self.optimizer == "sgd" else \
-            {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
+        bufs = self._state_buffers()
         for name, flat in bufs.items():
-            if flat is None or self.step_count == 0:
+            if flat is None or (self.step_count == 0 and self.optimizer != "adagrad"):
                 continue
             out[name] = OrderedDict((k, flat[o:o + n].view(shape).clone()) for k, o, n, shape in self._param_slices())
         return out
+
+    def _state_buffers(self) -> Dict[str, Optional[torch.Tensor]]:
+        """torch's per-parameter state names -> our flat buffers."""
+        if self.optimizer == "sgd":
+            return {"momentum_buffer": self.mom}
+        if self.optimizer == "adagrad":
+            return {"sum": self.state_sum}  # exists from construction in torch (initial_accumulator_value)
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
 
     def load_optimizer_state(self, state: Dict[str, object]) -> None:
         """Inverse of optimizer_state() (resume, or the state a torch optimizer
         holds: the next aggregate() continues from it)."""
         step = int(state.get("step", 0))
-        bufs = {"momentum_buffer": self.mom} if self.optimizer == "sgd" else \
-            {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
+        bufs = self._state_buffers()
         with torch.cuda.device(self.device):
             for name, flat in bufs.items():
                 if flat is None:
@@ -191,6 +210,7 @@ class FedOptServer:
                 if src is None:
                     if step:
                         raise KeyError(f"optimizer state at step {step} lacks {name!r}")
+                    flat.zero_()  # a fresh optimizer's state
                     continue
                 for k, o, n, _ in self._param_slices():
                     flat[o:o + n].copy_(src[k].detach().reshape(-1))
@@ -224,6 +244,8 @@ class FedOptServer:
                 tot += n * 4
             elif self.optimizer == "adam":  # p read+write, exp_avg / exp_avg_sq written (+ read after step 1)
                 tot += 2 * n * 4 + (4 if not self.first_step else 2) * n * 4
+            elif self.optimizer == "adagrad":  # p and state_sum read and written
+                tot += 4 * n * 4
             else:
                 tot += 2 * n * 4 + (2 * n * 4 if self.mom is not None and not self.first_step else
                                     (n * 4 if self.mom is not None else 0))

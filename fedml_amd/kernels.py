@@ -239,6 +239,18 @@ def wsum_fedopt_adam(d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int, pa
         ctypes.addressof(scalars), int(first_step), flags, nat.stream_handle()), "wsum_fedopt_adam_f32")
 
 
+def wsum_fedopt_adagrad(d_ptrs: torch.Tensor, d_w, K: int, N: int, param: torch.Tensor, state_sum: torch.Tensor,
+                        clr: float, eps: float, aligned: bool) -> None:
+    """FedAvg of K fp32 sources fused with the server Adagrad step: param and
+    state_sum (flat, N elements each) are updated in place."""
+    _require_cuda(param, "wsum_fedopt_adagrad")
+    ok = aligned and all((t.data_ptr() & 15) == 0 for t in (param, state_sum))
+    flags = (nat.FEDAGG_ALIGNED16 if ok else 0) | (nat.FEDAGG_HOST_WEIGHTS if isinstance(d_w, HostWeights) else 0)
+    nat.check(nat.lib().fedagg_wsum_fedopt_adagrad_f32(
+        d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), state_sum.data_ptr(), float(clr), float(eps),
+        flags, nat.stream_handle()), "wsum_fedopt_adagrad_f32")
+
+
 def round_f32(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """fp32 -> bf16/f16 (RNE) on the device, in libfedagg (fedagg_round_f32)."""
     _require_cuda(x, "round_f32")

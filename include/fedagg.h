@@ -186,6 +186,21 @@ int fedagg_wsum_fedopt_adam_f32(const float* const* d_src, const float* d_w,
                                 const float* scalars6, int32_t first_step,
                                 uint32_t flags, fedagg_stream_t stream);
 
+/* Server Adagrad (torch.optim.Adagrad: weight_decay 0) fused with the FedAvg
+ * of K fp32 clients, one pass.  Replaces the server step of
+ * simulation/sp/fedopt/fedopt_api.py:121-130 with OptRepo "adagrad"
+ * (optrepo.py:10-38 builds torch.optim.Adagrad(params, lr=server_lr)).
+ * d_sum is the optimizer's state_sum (N floats; initial_accumulator_value,
+ * i.e. zeros, before the first step).  clr = lr / (1 + (step-1) * lr_decay),
+ * the step's learning rate as torch computes it in double (= lr for FedML).
+ * Per element: g = p - avg; sum = fma(g, g, sum);
+ * p = p + fl(-clr * g) / (sqrt(sum) + eps), rounded as torch's CPU kernels
+ * round (addcmul fused, addcdiv not); sqrt is correctly rounded. */
+int fedagg_wsum_fedopt_adagrad_f32(const float* const* d_src, const float* d_w,
+                                   int32_t K, int64_t N, float* d_param,
+                                   float* d_sum, float clr, float eps,
+                                   uint32_t flags, fedagg_stream_t stream);
+
 /* ---- Robust aggregation --------------------------------------------------- */
 
 /* Coordinate-wise median over K fp32 clients (the "wise_median" defense,

@@ -160,3 +160,16 @@ void oracle_adam_moments_f32(const float* p, const float* avg, float* m, float* 
     v[e] = fmaf(c2 * g, g, vb);
   }
 }
+
+/* Server Adagrad's accumulator (sp/fedopt/fedopt_api.py:121-130 with
+ * torch.optim.Adagrad, single-tensor CPU path): g = p - avg;
+ *   state_sum.addcmul_(g, g, value=1)    fma(g, g, sum)  (fl(1*g) = g)
+ * (measured against torch 2.10's CPU kernel, vector body and scalar tail).
+ * The parameter update needs torch's own sqrt and is done by the caller
+ * (fedavg_oracle.fedopt_adagrad). */
+void oracle_adagrad_sum_f32(const float* p, const float* avg, float* sum, int64_t N) {
+  for (int64_t e = 0; e < N; ++e) {
+    const float g = p[e] - avg[e];
+    sum[e] = fmaf(g, g, sum[e]);
+  }
+}

@@ -13,7 +13,8 @@ It restates, branch by branch, python/fedml/ml/aggregator/agg_operator.py:
                     FedDyn        :68-77   (unweighted, aliases client 0)
                     SCAFFOLD      :100-118 (overwrites with the last client)
                     Mime          :119-133
-and the FedOpt server step of simulation/mpi/fedopt/FedOptAggregator.py:81-130.
+and the FedOpt server step of simulation/mpi/fedopt/FedOptAggregator.py:81-130
+(SGD) and of sp/fedopt/fedopt_api.py:121-130 (Adam, Adagrad).
 
 Inputs and outputs are CPU torch tensors (the reference's own currency); all
 arithmetic is numpy in the tensor's opmath type with one IEEE rounding per
@@ -232,6 +233,7 @@ def clib() -> ctypes.CDLL:
             "oracle_sum_i64": [P, I, L, P],
             "oracle_fedopt_sgd_f32": [P, P, P, L, F, F, I],
             "oracle_adam_moments_f32": [P, P, P, P, L, F, F, F],
+            "oracle_adagrad_sum_f32": [P, P, P, L],
         }.items():
             fn = getattr(lib, name)
             fn.restype = None
@@ -333,6 +335,50 @@ def fedopt_adam_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: 
             m, v = state.get(k, (None, None))
             p, m, v = fedopt_adam(to_np(t_old).ravel(), to_np(avg[k]).ravel(), m, v, lr, step, sqrt=sqrt)
             state[k] = (m, v)
+            out[k] = torch.from_numpy(p).reshape(t_old.shape)
+        else:
+            out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)
+    return out
+
+
+def fedopt_adagrad(p_old: np.ndarray, avg: np.ndarray, acc: np.ndarray | None, lr: float, eps: float = 1e-10,
+                   sqrt: str = "torch") -> Tuple[np.ndarray, np.ndarray]:
+    """One server Adagrad step on one named parameter (torch.optim.Adagrad with
+    lr only, as sp/fedopt/fedopt_api.py:78-85 builds it; lr_decay 0 so the
+    step's clr is lr).  Returns (p, state_sum):
+      sum = fma(g, g, sum)                     addcmul_(g, g, value=1)
+      std = fl(sqrt(sum) + eps)                sqrt().add_(eps)
+      p   = fl(p + fl(fl(-clr * g) / std))     addcdiv_(g, std, value=-clr), not fused
+    sqrt as in fedopt_adam (torch's CPU sqrt is not correctly rounded)."""
+    p = np.ascontiguousarray(p_old, dtype=np.float32).reshape(-1).copy()
+    a = np.ascontiguousarray(avg, dtype=np.float32).reshape(-1)
+    ss = np.zeros_like(p) if acc is None else np.ascontiguousarray(acc, dtype=np.float32).reshape(-1).copy()
+    clib().oracle_adagrad_sum_f32(p.ctypes.data, a.ctypes.data, ss.ctypes.data, p.size)
+    g = (p - a).astype(np.float32)
+    if sqrt == "torch":
+        r = torch.from_numpy(ss).sqrt().numpy()
+    elif sqrt == "ieee":
+        r = np.sqrt(ss)
+    else:
+        raise ValueError(sqrt)
+    std = (r + np.float32(eps)).astype(np.float32)
+    p = (p + (np.float32(-lr) * g) / std).astype(np.float32)
+    return p, ss
+
+
+def fedopt_adagrad_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str], raw_grad_list,
+                         lr: float, state: Dict[str, np.ndarray], sqrt: str = "torch"
+                         ) -> "OrderedDict[str, torch.Tensor]":
+    """One FedOptAPI round with server_optimizer="adagrad" (fedopt_api.py:121-130):
+    FedAvg, Adagrad on named parameters (state carries state_sum across rounds),
+    averaged values for buffers."""
+    class _A:
+        federated_optimizer = "FedAvg"
+    avg = agg(_A(), raw_grad_list)
+    out = OrderedDict()
+    for k, t_old in global_sd.items():
+        if k in param_names:
+            p, state[k] = fedopt_adagrad(to_np(t_old).ravel(), to_np(avg[k]).ravel(), state.get(k), lr, sqrt=sqrt)
             out[k] = torch.from_numpy(p).reshape(t_old.shape)
         else:
             out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)

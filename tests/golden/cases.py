@@ -116,6 +116,12 @@ FEDOPT_ADAM_CASES = [
     dict(name="fedopt_adam_lr1", K=3, rounds=3, lr=1.0, model="adam", seed=94),
     dict(name="fedopt_adam_lr1e-3_small", K=5, rounds=5, lr=0.001, model="small", seed=95),
 ]
+# Server Adagrad (FedAdagrad; OptRepo "adagrad", lr only: lr_decay 0, eps 1e-10,
+# initial_accumulator_value 0)
+FEDOPT_ADAGRAD_CASES = [
+    dict(name="fedopt_adagrad_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=96, optimizer="adagrad"),
+    dict(name="fedopt_adagrad_lr1e-1_small", K=5, rounds=3, lr=0.1, model="small", seed=97, optimizer="adagrad"),
+]
 FEDOPT_CASES = [
     dict(name="fedopt_sgd_m09_lr1", K=4, rounds=3, lr=1.0, momentum=0.9, seed=90),
     dict(name="fedopt_sgd_m09_lr1e-3", K=4, rounds=3, lr=0.001, momentum=0.9, seed=91),

@@ -176,7 +176,7 @@ def import_sp_fedopt():
 
 def run_fedopt_adam_case(FedOptAPI, spec):
     """The server half of FedOptAPI.train (fedopt_api.py:121-130) with
-    server_optimizer="adam": _aggregate, then zero_grad / state_dict /
+    server_optimizer="adam" (or spec["optimizer"], e.g. "adagrad"): _aggregate, then zero_grad / state_dict /
     _set_model_global_grads / _instanciate_opt / load_state_dict / step, each the
     reference's own method.  Clients are the synthetic updates of cases.py."""
     ent = cases.FEDOPT_MODELS[spec["model"]]
@@ -197,7 +197,7 @@ def run_fedopt_adam_case(FedOptAPI, spec):
             self.model.load_state_dict(sd)
 
     class A:
-        server_optimizer = "adam"
+        server_optimizer = spec.get("optimizer", "adam")
         server_lr = spec["lr"]
 
     api = object.__new__(FedOptAPI)
@@ -224,8 +224,8 @@ def run_fedopt_adam_case(FedOptAPI, spec):
             arrays[f"r{r}:{k}"] = tensor_bytes(t)
         st = api.opt.state_dict()["state"]
         for j, name in enumerate(cases.FEDOPT_PARAMS):
-            arrays[f"r{r}:exp_avg:{name}"] = tensor_bytes(st[j]["exp_avg"])
-            arrays[f"r{r}:exp_avg_sq:{name}"] = tensor_bytes(st[j]["exp_avg_sq"])
+            for buf in (("sum",) if A.server_optimizer == "adagrad" else ("exp_avg", "exp_avg_sq")):
+                arrays[f"r{r}:{buf}:{name}"] = tensor_bytes(st[j][buf])
     save(spec["name"], meta, arrays)
 
 
@@ -277,7 +277,7 @@ def main(only=()):
         run_fedopt_case(FedOptAggregator, spec)
         print("wrote", spec["name"])
     FedOptAPI = import_sp_fedopt()
-    for spec in filter(want, cases.FEDOPT_ADAM_CASES):
+    for spec in filter(want, cases.FEDOPT_ADAM_CASES + cases.FEDOPT_ADAGRAD_CASES):
         run_fedopt_adam_case(FedOptAPI, spec)
         print("wrote", spec["name"])
     Median, Trimmed = import_defenses()

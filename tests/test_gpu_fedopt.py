@@ -163,6 +163,74 @@ def test_fused_adam_vs_oracle_large(cuda_device):
     assert d_w.numel() == K
 
 
+@pytest.mark.parametrize("spec", cases.FEDOPT_ADAGRAD_CASES, ids=lambda s: s["name"])
+def test_fedopt_adagrad_matches_reference(spec, cuda_device):
+    """Each round of FedOptAPI's server Adagrad, started from the reference's
+    own state of the previous round: state_sum and every buffer bit-identical
+    to torch; parameters bit-identical to the oracle with a correctly rounded
+    sqrt and within 1 ulp(p) + 2^-21 |step| of torch (CPU sqrt)."""
+    meta, arrays = gu.load(spec["name"])
+    names = cases.FEDOPT_PARAMS
+    init = cases.fedopt_global_init(spec)
+    prev = OrderedDict((k, gu.to_tensor(arrays[f"init:{k}"], str(t.dtype).replace("torch.", ""), t.shape))
+                       for k, t in init.items())
+    exact = total = 0
+    for r in range(spec["rounds"]):
+        server = FedOptServer(prev, names, spec["K"], "adagrad", spec["lr"], 0.0, cuda_device)
+        state = {"step": r}
+        if r:
+            state["sum"] = OrderedDict((k, torch.from_numpy(arrays[f"r{r - 1}:sum:{k}"].copy())) for k in names)
+        server.load_optimizer_state(state)
+        raw = cases.fedopt_round_inputs(spec, prev, r)
+        assert fingerprint(raw) == meta["rounds"][r]["in_sha256"]
+        for i, (n, d) in enumerate(raw):
+            server.add_local_trained_result(i, d, n)
+        out = OrderedDict((k, t.cpu().clone()) for k, t in server.aggregate().items())
+        st = server.optimizer_state()
+        assert st["step"] == r + 1
+        for k in names:
+            gold = torch.from_numpy(arrays[f"r{r}:sum:{k}"].copy()).reshape(st["sum"][k].shape)
+            gu.assert_same(st["sum"][k].cpu(), gold, f"r{r} sum {k}")
+        osum = {k: arrays[f"r{r - 1}:sum:{k}"].reshape(-1).copy() for k in names} if r else {}
+        exp = orc.fedopt_adagrad_round(prev, names, raw, spec["lr"], osum, sqrt="ieee")
+        for k, t in out.items():
+            gu.assert_same(t, exp[k], f"r{r} oracle {k}")
+            e = gu.to_tensor(arrays[f"r{r}:{k}"], str(t.dtype).replace("torch.", ""), t.shape)
+            if k in names:
+                step = (e.double() - prev[k].double()).abs()
+                tol = torch.from_numpy(np.spacing(np.abs(e.numpy()))).double() + step * 2.0 ** -21
+                assert ((t.double() - e.double()).abs() <= tol).all(), f"r{r} {k}"
+                exact += int((_bits(t) == _bits(e)).sum())
+                total += t.numel()
+            else:
+                gu.assert_same(t, e, f"r{r} {k}")
+        prev = OrderedDict((k, gu.to_tensor(arrays[f"r{r}:{k}"], str(t.dtype).replace("torch.", ""), t.shape))
+                           for k, t in init.items())
+    assert exact >= 0.98 * total, (exact, total)
+
+
+@pytest.mark.parametrize("N", [262_147, 5_000_011])
+def test_fused_adagrad_vs_oracle_large(N, cuda_device):
+    """Fused Adagrad with a ragged tail (small-tile and mid-tile launches),
+    3 rounds, every element bit-exact against the C oracle (IEEE sqrt)."""
+    K = 12
+    g = torch.Generator(device=cuda_device).manual_seed(N % 101)
+    rows = torch.randn(K, (N + 63) // 64 * 64, generator=g, device=cuda_device) * 0.02
+    p = torch.randn(N, generator=g, device=cuda_device) * 0.02
+    acc = torch.zeros(N, device=cuda_device)
+    ws = [(i + 2.0) for i in range(K)]
+    ws = [w / sum(ws) for w in ws]
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    hp, hs = p.cpu().numpy(), None
+    for r in range(3):
+        avg = orc.wsum([rows[i, :N].cpu() for i in range(K)], ws).numpy()
+        kn.wsum_fedopt_adagrad(d_ptrs, kn.weights_for(ws, torch.float32, cuda_device), K, N, p, acc, 0.1, 1e-10, True)
+        hp, hs = orc.fedopt_adagrad(hp, avg, hs, 0.1, sqrt="ieee")
+        gu.assert_same(acc.cpu(), torch.from_numpy(hs), f"r{r} sum")
+        gu.assert_same(p.cpu(), torch.from_numpy(hp), f"r{r} param")
+        rows.mul_(1.01)
+
+
 def test_optimizer_state_round_trip(cuda_device):
     spec = cases.FEDOPT_ADAM_CASES[0]
     init = cases.fedopt_global_init(spec)
