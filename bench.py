@@ -114,13 +114,14 @@ def cpu_baseline(entries, K: int, sample_elems: int) -> dict:
                       f"{r['median_s'] * 1e3:.1f} ms/aggregation"}
 
 
-def load_traffic(config: str, mode: str, world: int):
+def load_traffic(config: str, mode: str, world: int, variant: str = ""):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None.
+    variant: "" for FedAvg, else the fused server step or the robust op."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    key = f"{config}:{mode if world > 1 else 'single'}" + (f":{variant}" if variant else "")
     try:
-        d = json.load(open(path))
-        return d.get(f"{config}:{mode if world > 1 else 'single'}", {}).get("bytes_per_launch")
+        return json.load(open(path)).get(key, {}).get("bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -269,7 +270,7 @@ def main():
 
     ms_per_step = elapsed / a.steps * 1e3
     value = world * K * n_elems / (elapsed / a.steps)
-    traffic = load_traffic(a.config, mode, world)
+    traffic = load_traffic(a.config, mode, world, a.fedopt or ("" if a.op == "fedavg" else a.op))
     line = {
         "metric": METRIC,
         "value": value,
