@@ -21,6 +21,7 @@
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <exception>
 #include <vector>
 
 namespace {
@@ -48,10 +49,21 @@ bool plain_lookup(PyObject* d) {
 //   numels[t] : elements of key t
 //   tables    : {code: bytes}, the int64 pointer table [T_code][K] of the keys
 //               of that dtype in key order, clients in list order
+PyObject* walk_impl(PyObject* dicts, PyObject* keys);
+
 PyObject* walk(PyObject*, PyObject* args) {
   PyObject* dicts;
   PyObject* keys;
   if (!PyArg_ParseTuple(args, "O!O!", &PyList_Type, &dicts, &PyList_Type, &keys)) return nullptr;
+  try {
+    return walk_impl(dicts, keys);
+  } catch (const std::exception&) {  // a tensor torch itself would refuse here: let the Python walk report it
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+}
+
+PyObject* walk_impl(PyObject* dicts, PyObject* keys) {
   const Py_ssize_t K = PyList_GET_SIZE(dicts), T = PyList_GET_SIZE(keys);
   if (K < 1) Py_RETURN_NONE;
   for (Py_ssize_t i = 0; i < K; ++i)
@@ -72,7 +84,7 @@ PyObject* walk(PyObject*, PyObject* args) {
       }
       if (!THPVariable_Check(v)) Py_RETURN_NONE;
       const at::Tensor& x = THPVariable_Unpack(v);
-      if (!x.defined() || !x.is_cuda() || !x.is_contiguous()) Py_RETURN_NONE;
+      if (!x.defined() || x.layout() != c10::kStrided || !x.is_cuda() || !x.is_contiguous()) Py_RETURN_NONE;
       if (i == 0) {
         t0 = &x;
         const int code = multi_code(x.scalar_type());

@@ -192,5 +192,6 @@ def test_dict_walker_builds_and_declines_host_inputs():
             return super().__getitem__(k)
 
     assert w.walk([Custom(a=torch.ones(3))], ["a"]) is None
+    assert w.walk([OrderedDict(a=torch.ones(3).to_sparse())], ["a"]) is None  # non-strided: no C++ throw escapes
     with pytest.raises(TypeError):
         w.walk([OrderedDict()], [["unhashable"]])
