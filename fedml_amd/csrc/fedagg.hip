@@ -988,132 +988,167 @@ int launch_median(const float* const* src, int K, int64_t N, float* out, hipStre
   return check_launch("fedagg_median_f32");
 }
 
-// More than 128 clients: the column no longer fits in one lane's registers.
-// A workgroup stages a tile of kRadixCols consecutive columns x K clients in
-// LDS (coalesced row segments in, stored column-major as order-preserving
-// uint32 keys), then each wave selects one column's lower median with an
-// 8-bit radix select over those keys: 4 passes of a 256-bin LDS histogram
-// (ds_add), a wave prefix sum over the bins, and the digit that holds rank
-// (K-1)/2.  Exact for every input: the key order is the float order with
-// -0 < +0 (a ±0 tie at the median may return the other zero than torch's
-// nth_element, as for the register kernel), and a column holding a NaN
-// returns its first NaN in client order (the row index is found with an LDS
-// atomic min while the tile is loaded).
-constexpr int kRadixCols = 32;
-
-__device__ __forceinline__ uint32_t f32_order_key(uint32_t u) {
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+// More than 128 clients, in registers: P = 2, 4 or 8 adjacent lanes share one
+// column, each lane holding 128 of its KMAX = 128·P (±inf-padded) values,
+// slot s = sub·128 + j = client s.  Every lane sorts its 128 values with the
+// pairwise network (all outputs used, so nothing is pruned); the sorted runs
+// are then merged across lanes as in a bitonic merge sort:
+//   - "reverse pairing" of two sorted runs A, B of length L held by lane
+//     groups g and g ^ (G-1): element i of A meets element L-1-i of B, the
+//     lower group keeps the min (the L smallest, a bitonic sequence), the
+//     upper the max.  Partner lane = sub ^ (G-1), partner register = 127 - i;
+//   - a half-cleaner cascade sorts each bitonic half: a stage whose slot
+//     distance is 128 pairs lane sub with sub ^ 1 at the same register, the
+//     rest run inside the lane.
+// Cross-lane moves are single DPP movs (xor 1 / 3 quad permutes, xor 7 =
+// row_half_mirror), the min-or-max choice one v_med3 against ±inf.  The last
+// level needs no merge: after its reverse pairing the lower half holds exactly
+// the KMAX/2 smallest values, whose maximum sits at the padded median slot
+// KMAX/2 - 1, i.e. it is the column's lower median.  VALU per column ≈ 7k
+// (P = 2), 19k (P = 4), 49k (P = 8) lane-ops, against 2k for K <= 128.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
 }
-__device__ __forceinline__ uint32_t f32_from_order_key(uint32_t k) {
-  return (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+template <int M>
+constexpr int dpp_xor_ctrl() {
+  static_assert(M == 1 || M == 2 || M == 3 || M == 7, "lane xor pattern without a single DPP mov");
+  // quad_perm [1,0,3,2], [2,3,0,1], [3,2,1,0]; row_half_mirror
+  return M == 1 ? 0xB1 : M == 2 ? 0x4E : M == 3 ? 0x1B : 0x141;
 }
 
-// Column stride in LDS: >= KCAP and = 9 (mod 64), so the column-major writes
-// of 64 consecutive columns hit 64 different banks and the 8 columns a wave
-// instruction can touch start 9 banks apart.
-template <int KCAP>
-constexpr int radix_stride() {
-  return KCAP + ((9 - KCAP % 64) + 64) % 64;
-}
+constexpr int kLaneVals = 128;
 
-template <int KCAP>
-__global__ __launch_bounds__(256) void median_radix_kernel(const float* const* __restrict__ src, int K, int64_t N,
-                                                           float* __restrict__ out) {
-  constexpr int C = kRadixCols, S = radix_stride<KCAP>();
-  __shared__ uint32_t keys[C * S];
-  __shared__ uint32_t hist[4][256];
-  __shared__ int nan_row[C];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t col0 = int64_t(blockIdx.x) * C;
-  const int ncols = int(min<int64_t>(C, N - col0));
-  if (t < C) nan_row[t] = K;
-  __syncthreads();
-
-  // ---- tile load: thread t reads column t % C of rows t / C, t / C + 8, ...
-  {
-    const int cc = t % C;
-    constexpr int RSTEP = 256 / C;
-    if (cc < ncols) {
-      int first_nan = K;
-      int r = t / C;
-      for (; r + 3 * RSTEP < K; r += 4 * RSTEP) {  // 4 rows in flight per thread
-        float x[4];
+// min (lower lanes, sel = -inf) or max (upper lanes, sel = +inf) of own
+// register i and the partner lane's register 127 - i, for every i
+template <int M>
+__device__ __forceinline__ void lanes_reverse_pair(float (&v)[kLaneVals], float sel) {
+  constexpr int R = kLaneVals;
+  // opaque to the compiler: knowing sel is ±inf it splits every v_med3 into
+  // min, max and a select (three ops and twice the live registers)
+  asm volatile("" : "+v"(sel));
 #pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load(as_global(src[r + u * RSTEP]) + col0 + cc);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          keys[cc * S + r + u * RSTEP] = f32_order_key(__float_as_uint(x[u]));
-          if (__builtin_isnan(x[u]) && first_nan == K) first_nan = r + u * RSTEP;
-        }
-      }
-      for (; r < K; r += RSTEP) {
-        const float x = __builtin_nontemporal_load(as_global(src[r]) + col0 + cc);
-        keys[cc * S + r] = f32_order_key(__float_as_uint(x));
-        if (__builtin_isnan(x) && first_nan == K) first_nan = r;
-      }
-      if (first_nan < K) atomicMin(&nan_row[cc], first_nan);
-    }
-  }
-  __syncthreads();
-
-  // ---- per-column radix select, one wave per column
-  for (int c = w; c < ncols; c += 4) {
-    const uint32_t* col = keys + c * S;
-    uint32_t prefix = 0, pmask = 0;
-    int rank = (K - 1) / 2;
-#pragma unroll 1
-    for (int shift = 24; shift >= 0; shift -= 8) {
-#pragma unroll
-      for (int b = lane; b < 256; b += 64) hist[w][b] = 0;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (int i = lane; i < K; i += 64) {
-        const uint32_t k = col[i];
-        if ((k & pmask) == prefix) atomicAdd(&hist[w][(k >> shift) & 0xffu], 1u);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      // lane owns bins 4*lane .. 4*lane+3; inclusive prefix sum over the wave
-      uint32_t h[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) h[j] = hist[w][4 * lane + j];
-      const int own = int(h[0] + h[1] + h[2] + h[3]);
-      int incl = own;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-      }
-      const int excl = incl - own;
-      const uint64_t bal = __ballot(excl <= rank && rank < incl);
-      const int L = __builtin_ctzll(bal);  // exactly one lane's bins hold the rank
-      int digit = 4 * lane, below = excl;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (digit == 4 * lane + j && below + int(h[j]) <= rank) {
-          below += int(h[j]);
-          ++digit;
-        }
-      }
-      digit = __builtin_amdgcn_readlane(digit, L);
-      below = __builtin_amdgcn_readlane(below, L);
-      prefix |= uint32_t(digit) << shift;
-      pmask |= 0xffu << shift;
-      rank -= below;
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (lane == 0) {
-      const int nr = nan_row[c];
-      out[col0 + c] = __uint_as_float(f32_from_order_key(nr < K ? col[nr] : prefix));
-    }
+  for (int i = 0; i < R / 2; ++i) {
+    const float a = dpp_mov<dpp_xor_ctrl<M>()>(v[R - 1 - i]);
+    const float b = dpp_mov<dpp_xor_ctrl<M>()>(v[i]);
+    v[i] = __builtin_amdgcn_fmed3f(v[i], a, sel);
+    v[R - 1 - i] = __builtin_amdgcn_fmed3f(v[R - 1 - i], b, sel);
   }
 }
 
-template <int KCAP>
-int launch_median_radix(const float* const* src, int K, int64_t N, float* out, hipStream_t st) {
-  const int64_t grid = (N + kRadixCols - 1) / kRadixCols;
+// in-lane half-cleaner cascade: a bitonic register array -> ascending
+__device__ __forceinline__ void lane_bitonic_merge(float (&v)[kLaneVals]) {
+#pragma unroll
+  for (int d = kLaneVals / 2; d > 0; d /= 2) {
+#pragma unroll
+    for (int i = 0; i < kLaneVals; ++i)
+      if ((i & d) == 0) cmpx(v[i], v[i + d]);
+  }
+}
+
+// merge levels G = 2, 4 (< P): afterwards every group of G lanes holds its
+// G·128 values sorted ascending over slots (sub % G)·128 + j
+template <int G, int P>
+__device__ __forceinline__ void lanes_merge_levels(float (&v)[kLaneVals], int sub) {
+  if constexpr (G < P) {
+    static_assert(G <= 4, "a level of 8 lanes would need xor-2 and xor-4 stages");
+    constexpr float inf = __builtin_huge_valf();
+    lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) ? inf : -inf);
+    if constexpr (G == 4) {  // slot distance 128: lane sub ^ 1, same register
+      float sel = (sub & 1) ? inf : -inf;
+      asm volatile("" : "+v"(sel));
+#pragma unroll
+      for (int i = 0; i < kLaneVals; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], dpp_mov<dpp_xor_ctrl<1>()>(v[i]), sel);
+    }
+    lane_bitonic_merge(v);
+    lanes_merge_levels<G * 2, P>(v, sub);
+  }
+}
+
+__device__ float g_median_pad[2] = {-__builtin_huge_valf(), __builtin_huge_valf()};
+
+template <int P, bool FULL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
+    const float* const* __restrict__ src, int K, int64_t N, float* __restrict__ out) {
+  static_assert(P == 2 || P == 4 || P == 8, "2, 4 or 8 lanes per column");
+  constexpr int R = kLaneVals, KMAX = P * R, PAD = 2;
+  // Row pointer of every slot, skewed by PAD entries per lane group so the P
+  // lanes of a column read different LDS banks.  A padded slot (K < KMAX)
+  // points at a ±inf constant and its column offset is masked to 0, so the
+  // load itself yields the pad: no per-slot, per-lane select.
+  __shared__ const float* rows[KMAX + PAD * P];
+  __shared__ uint64_t offmask[FULL ? 1 : KMAX + PAD * P];
+  const int t = threadIdx.x, sub = t & (P - 1);
+  if constexpr (FULL) K = KMAX;
+  const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
+  for (int i = t; i < KMAX; i += 256) {
+    const int q = i + PAD * (i / R);
+    if (FULL || i < K) {
+      rows[q] = src[i];
+      if constexpr (!FULL) offmask[q] = ~uint64_t(0);
+    } else {
+      rows[q] = &g_median_pad[i - K < below ? 0 : 1];
+      offmask[q] = 0;
+    }
+  }
+  __syncthreads();
+  // every lane stays active through the DPP exchanges; a column past the end
+  // recomputes the last one and does not store
+  const int64_t e = (int64_t(blockIdx.x) * 256 + t) / P;
+  const uint64_t boff = uint64_t(e < N ? e : N - 1) * 4u;
+  float v[R];
+  bool has_nan = false;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (j % 16 == 0 && j) __builtin_amdgcn_sched_barrier(0);
+    const int q = sub * (R + PAD) + j;
+    const uint64_t off = FULL ? boff : (boff & offmask[q]);
+    const auto row = reinterpret_cast<const char*>(rows[q]);
+    v[j] = __builtin_nontemporal_load(as_global(reinterpret_cast<const float*>(row + off)));
+    has_nan |= __builtin_isnan(v[j]);
+  }
+  // first NaN of the column in client (= slot) order, only in waves holding
+  // one (pads are ±inf, never NaN)
+  int nan_slot = KMAX;
+  float nan_v = 0.f;
+  if (__ballot(has_nan)) {
+#pragma unroll
+    for (int j = R - 1; j >= 0; --j) {
+      const bool n = __builtin_isnan(v[j]);
+      nan_slot = n ? sub * R + j : nan_slot;
+      nan_v = n ? v[j] : nan_v;
+    }
+#pragma unroll
+    for (int m = 1; m < P; m <<= 1) {
+      const int os = __shfl_xor(nan_slot, m, 64);
+      const float ov = __shfl_xor(nan_v, m, 64);
+      if (os < nan_slot) {
+        nan_slot = os;
+        nan_v = ov;
+      }
+    }
+  }
+  pairwise_sort<R>(v);
+  lanes_merge_levels<2, P>(v, sub);
+  // last level: after the reverse pairing against sub ^ (P-1) the lower P/2
+  // lanes hold the KMAX/2 smallest values; their max is the median
+  lanes_reverse_pair<P - 1>(v, (sub & (P / 2)) ? __builtin_huge_valf() : -__builtin_huge_valf());
+  float m = v[0];
+#pragma unroll
+  for (int i = 1; i < R; ++i) m = fmaxf(m, v[i]);
+  if constexpr (P >= 4) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
+  if constexpr (P >= 8) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
+  if (sub == 0 && e < N) out[e] = nan_slot < KMAX ? nan_v : m;
+}
+
+template <int P>
+int launch_median_lanes(const float* const* src, int K, int64_t N, float* out, hipStream_t st) {
+  const int64_t grid = (N * P + 255) / 256;
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N too large");
-  hipLaunchKernelGGL((median_radix_kernel<KCAP>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+  if (K == P * kLaneVals)
+    hipLaunchKernelGGL((median_lanes_kernel<P, true>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+  else
+    hipLaunchKernelGGL((median_lanes_kernel<P, false>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
   return check_launch("fedagg_median_f32");
 }
 
@@ -1494,10 +1529,10 @@ int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_
   if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: null pointer");
   if (N == 0) return FEDAGG_OK;
   auto st = reinterpret_cast<hipStream_t>(stream);
-  if (K > 128) {  // LDS tile + radix select
-    if (K <= 256) return launch_median_radix<256>(d_src, K, N, d_out, st);
-    if (K <= 512) return launch_median_radix<512>(d_src, K, N, d_out, st);
-    if (K <= 1024) return launch_median_radix<1024>(d_src, K, N, d_out, st);
+  if (K > 128) {  // 2, 4 or 8 lanes per column, register sort + cross-lane merges
+    if (K <= 256) return launch_median_lanes<2>(d_src, K, N, d_out, st);
+    if (K <= 512) return launch_median_lanes<4>(d_src, K, N, d_out, st);
+    if (K <= 1024) return launch_median_lanes<8>(d_src, K, N, d_out, st);
     return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K > 1024 clients is not supported");
   }
   // the register kernels address rows with 32-bit byte offsets

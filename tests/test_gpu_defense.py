@@ -78,9 +78,10 @@ def test_median_headline_shape_sampled(cuda_device):
 
 
 @pytest.mark.parametrize("K", [129, 200, 255, 256, 257, 512, 700, 1024])
-def test_median_radix_kernel_vs_oracle(K, cuda_device):
-    """More than 128 clients (LDS tile + radix select): every KCAP bucket and a
-    ragged last tile, with duplicates, infinities, NaN columns and -0.0."""
+def test_median_lanes_kernel_vs_oracle(K, cuda_device):
+    """More than 128 clients (2, 4 or 8 lanes per column, register sort plus
+    cross-lane merges): full and padded kernels of every lane count, a ragged
+    last workgroup, with duplicates, infinities, NaN columns and -0.0."""
     N = 3_001
     g = torch.Generator(device=cuda_device).manual_seed(K)
     rows = torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125
@@ -97,7 +98,7 @@ def test_median_radix_kernel_vs_oracle(K, cuda_device):
     gu.assert_same(out.cpu(), torch.from_numpy(exp), f"median K={K}")
 
 
-def test_median_radix_large_sampled(cuda_device):
+def test_median_lanes_large_sampled(cuda_device):
     """512 clients x 4M fp32 (the config-4 client count): 100,000 random
     columns plus the ragged tail against the oracle."""
     K, N = 512, 4_000_037

@@ -42,6 +42,17 @@ def main():
                                         ctypes.c_void_p]
     lib.median_probe_name.restype = ctypes.c_char_p
     dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    summary = {}
+    if "--big-only" not in sys.argv:
+        summary.update(probe_k128(lib, kn, dev, st))
+    probe_big(lib, kn, dev, st, summary)
+    print(json.dumps(summary, indent=1))
+    os.makedirs("gpurun_out", exist_ok=True)
+    json.dump(summary, open("gpurun_out/median_probe.json", "w"), indent=1)
+
+
+def probe_k128(lib, kn, dev, st):
     K, N = 128, 25_610_152
     L = (N + 63) // 64 * 64
     rows = torch.empty((K, L), device=dev)
@@ -75,32 +86,41 @@ def main():
         ms = statistics.median(res[name])
         summary[name] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
                          "compute_only_ms": round(statistics.median(res_c[name]), 4)}
-    # more than 128 clients: the product entry point (LDS tile + radix select)
     del rows, tab, same, out
     torch.cuda.empty_cache()
-    from fedml_amd import defense as dfn
+    return summary
 
+
+def probe_big(lib, kn, dev, st, summary):
+    """More than 128 clients: LDS-tile radix select (v0) vs lane-group register
+    sort (v1, shipped), interleaved; their outputs must agree bit for bit."""
+    lib.median_big_probe.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                     ctypes.c_void_p]
     N2 = 4_000_000
-    for K2 in (256, 512, 1024):
+    for K2 in (129, 256, 257, 512, 513, 1024):
         rows = torch.randn((K2, N2), device=dev) * 0.05
         tab = kn.upload_i64([rows[i].data_ptr() for i in range(K2)], dev)
-        out = torch.empty(N2, device=dev)
-        dfn.median_f32(tab, K2, N2, out)
-        ts = []
+        outs = [torch.empty(N2, device=dev) for _ in range(2)]
+        ts = [[], []]
+        for v in (0, 1):
+            assert lib.median_big_probe(v, tab.data_ptr(), K2, N2, outs[v].data_ptr(), st) == 0
+        torch.cuda.synchronize()
+        same_bits = bool(torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)))
         for _ in range(5):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            dfn.median_f32(tab, K2, N2, out)
-            e1.record()
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        ms = statistics.median(ts)
-        summary[f"radix_K{K2}_N{N2}"] = {"ms": round(ms, 4), "GBps": round((K2 + 1) * N2 * 4 / ms / 1e6, 1)}
-        del rows, tab, out
+            for v in (0, 1):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                lib.median_big_probe(v, tab.data_ptr(), K2, N2, outs[v].data_ptr(), st)
+                e1.record()
+                torch.cuda.synchronize()
+                ts[v].append(e0.elapsed_time(e1))
+        for v, name in ((0, "radix"), (1, "lanes")):
+            ms = statistics.median(ts[v])
+            summary[f"{name}_K{K2}_N{N2}"] = {"ms": round(ms, 4), "GBps": round((K2 + 1) * N2 * 4 / ms / 1e6, 1)}
+        summary[f"K{K2}_radix_equals_lanes"] = same_bits
+        print(K2, summary[f"radix_K{K2}_N{N2}"], summary[f"lanes_K{K2}_N{N2}"], same_bits, flush=True)
+        del rows, tab, outs
         torch.cuda.empty_cache()
-    print(json.dumps(summary, indent=1))
-    os.makedirs("gpurun_out", exist_ok=True)
-    json.dump(summary, open("gpurun_out/median_probe.json", "w"), indent=1)
 
 
 if __name__ == "__main__":
