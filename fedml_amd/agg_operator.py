@@ -158,29 +158,68 @@ _CODE_DT = {nat.DT_F32: torch.float32, nat.DT_BF16: torch.bfloat16, nat.DT_F16: 
             nat.DT_I64: torch.int64}
 
 
-def _reduce_device_walked(walked, dicts, keys, weights, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
+_PLANS: "OrderedDict[tuple, kn.MultiPlan]" = OrderedDict()
+
+
+def _multi_plan(numels: Sequence[int], code: int, acc_mode: int) -> kn.MultiPlan:
+    """Segment tables of the multi-tensor launch, cached per key-size list: a
+    server aggregates the same model every round."""
+    key = (tuple(numels), code, acc_mode)
+    plan = _PLANS.pop(key, None)
+    if plan is None:
+        plan = kn.MultiPlan(numels, _CODE_DT[code], acc_mode)
+        while len(_PLANS) >= 32:
+            _PLANS.popitem(last=False)
+    _PLANS[key] = plan
+    return plan
+
+
+# Pipelined device path: keys are walked largest first in chunks, and each
+# chunk is launched as soon as it is walked, so the GPU reduces the bulk of the
+# bytes while the host is still walking the many small keys.
+_CHUNK_KEYS = (16, 32, 64)  # first chunks small: the GPU starts early; then the rest in 96s
+
+
+def _chunks(order: Sequence[int]):
+    lo = 0
+    for n in _CHUNK_KEYS:
+        if lo >= len(order):
+            return
+        yield order[lo:lo + n]
+        lo += n
+    while lo < len(order):
+        yield order[lo:lo + 96]
+        lo += 96
+
+
+def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
     """Every key a contiguous, 16-byte aligned device tensor of one device
-    (what the native walker verified): one multi-tensor launch per dtype with
-    the walker's pointer tables, no per-tensor Python work."""
-    dev_idx, codes, numels, tables = walked
-    device = torch.device("cuda", dev_idx)
+    (what the native walker verifies): one multi-tensor launch per dtype and
+    chunk with the walker's pointer tables and natively allocated outputs, no
+    per-tensor Python work.  None if the walker declines any chunk (the caller
+    then runs the general path, which raises the reference's errors; launches
+    already made for earlier chunks only wrote outputs nobody sees)."""
+    order = w.order_by_size(dicts[0], keys)
+    if order is None:
+        return None
     K = len(dicts)
-    d0 = dicts[0]
     results: Dict[str, torch.Tensor] = {}
-    by_code: Dict[int, Tuple[List[int], List[int]]] = OrderedDict()
-    with torch.cuda.device(device):
-        for k, code in zip(keys, codes):
-            out = torch.empty(d0[k].shape, dtype=torch.float32 if code == nat.DT_I64 else _CODE_DT[code],
-                              device=device)
-            results[k] = out
-            ns, ops = by_code.setdefault(code, ([], []))
-            ns.append(out.numel())
-            ops.append(out.data_ptr())
-        if any(p & 15 for _, ops in by_code.values() for p in ops):
-            return None  # the caching allocator never does this; take the general path if it ever does
-        w32 = kn.upload_f32(weights, device)
-        for code, (ns, ops) in by_code.items():
-            kn.MultiPlan(ns, _CODE_DT[code], acc_mode).launch(tables[code], ops, w32, K, device)
+    keep = []  # device tables of the launches, alive until enqueued
+    w32 = None
+    for idx in _chunks(order):
+        ck = [keys[i] for i in idx]
+        walked = w.walk(dicts, ck, True)
+        if walked is None:
+            return None
+        dev_idx, codes, numels, tables, outs, out_tables = walked
+        device = torch.device("cuda", dev_idx)
+        with torch.cuda.device(device):
+            if w32 is None:
+                w32 = kn.upload_f32(weights, device)
+            for code, tab in tables.items():
+                ns = [n for n, c in zip(numels, codes) if c == code]
+                keep.append(_multi_plan(ns, code, acc_mode).launch(tab, out_tables[code], w32, K, device))
+        results.update(zip(ck, outs))
     return OrderedDict((k, results[k]) for k in keys)
 
 
@@ -192,11 +231,9 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
     acc_mode = _acc_mode(args)
     w = _walker()
     if w is not None and keys:
-        walked = w.walk(list(dicts), list(keys))
-        if walked is not None:
-            res = _reduce_device_walked(walked, dicts, keys, weights, acc_mode)
-            if res is not None:
-                return res
+        res = _reduce_device_walked(w, list(dicts), list(keys), weights, acc_mode)
+        if res is not None:
+            return res
     per_key = _gather(dicts, keys)
     K = len(dicts)
     results: Dict[str, torch.Tensor] = {}

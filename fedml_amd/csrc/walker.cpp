@@ -6,7 +6,9 @@
 // shape, device, contiguity and data pointer through Python costs ~0.4 us per
 // attribute per tensor (~20 ms per round, ten times the reduction itself).
 // This module walks the dicts in C++ and returns, per dtype, the flat [T][K]
-// table of client pointers that fedagg_wsum_multi consumes.
+// table of client pointers that fedagg_wsum_multi consumes, and optionally
+// allocates the T output tensors (at::empty, the caching allocator) so the
+// caller launches without touching any tensor from Python.
 //
 // It only ever takes the fast path: any irregularity (a missing key, a host or
 // non-contiguous tensor, mismatched shapes/dtypes/devices, a dtype the
@@ -18,8 +20,10 @@
 
 #include <Python.h>
 
+#include <ATen/ATen.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <exception>
 #include <vector>
@@ -44,26 +48,74 @@ bool plain_lookup(PyObject* d) {
   return Py_TYPE(d)->tp_as_mapping && Py_TYPE(d)->tp_as_mapping->mp_subscript == PyDict_Type.tp_as_mapping->mp_subscript;
 }
 
-// walk(dicts: list, keys: list) -> None | (device_index, codes, numels, tables)
-//   codes[t]  : FEDAGG_DT_* of key t
-//   numels[t] : elements of key t
-//   tables    : {code: bytes}, the int64 pointer table [T_code][K] of the keys
-//               of that dtype in key order, clients in list order
-PyObject* walk_impl(PyObject* dicts, PyObject* keys);
+// walk(dicts: list, keys: list, alloc: bool = False)
+//     -> None | (device_index, codes, numels, tables[, outs, out_tables])
+//   codes[t]   : FEDAGG_DT_* of key t
+//   numels[t]  : elements of key t
+//   tables     : {code: bytes}, the int64 pointer table [T_code][K] of the keys
+//                of that dtype in key order, clients in list order
+//   outs[t]    : (alloc) a new contiguous tensor shaped like client 0's key t,
+//                float32 for int64 keys (the reference's int64 * float
+//                promotion), the dtype otherwise, on the inputs' device
+//   out_tables : (alloc) {code: bytes}, the output pointers [T_code]
+PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc);
 
 PyObject* walk(PyObject*, PyObject* args) {
   PyObject* dicts;
   PyObject* keys;
-  if (!PyArg_ParseTuple(args, "O!O!", &PyList_Type, &dicts, &PyList_Type, &keys)) return nullptr;
+  int alloc = 0;
+  if (!PyArg_ParseTuple(args, "O!O!|p", &PyList_Type, &dicts, &PyList_Type, &keys, &alloc)) return nullptr;
   try {
-    return walk_impl(dicts, keys);
+    return walk_impl(dicts, keys, alloc != 0);
   } catch (const std::exception&) {  // a tensor torch itself would refuse here: let the Python walk report it
     PyErr_Clear();
     Py_RETURN_NONE;
   }
 }
 
-PyObject* walk_impl(PyObject* dicts, PyObject* keys) {
+// order_by_size(d: dict, keys: list) -> None | list of key indices, largest
+// tensor first (stable).  The pipelined reduction walks and launches the big
+// keys first, so the GPU starts on most of the bytes while the host is still
+// walking the many small ones.
+PyObject* order_by_size(PyObject*, PyObject* args) {
+  PyObject* d;
+  PyObject* keys;
+  if (!PyArg_ParseTuple(args, "OO!", &d, &PyList_Type, &keys)) return nullptr;
+  if (!plain_lookup(d)) Py_RETURN_NONE;
+  const Py_ssize_t T = PyList_GET_SIZE(keys);
+  std::vector<std::pair<int64_t, Py_ssize_t>> sz(T);
+  for (Py_ssize_t t = 0; t < T; ++t) {
+    PyObject* v = PyDict_GetItemWithError(d, PyList_GET_ITEM(keys, t));
+    if (!v) {
+      if (PyErr_Occurred()) return nullptr;
+      Py_RETURN_NONE;
+    }
+    if (!THPVariable_Check(v)) Py_RETURN_NONE;
+    sz[t] = {-THPVariable_Unpack(v).numel(), t};
+  }
+  std::stable_sort(sz.begin(), sz.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PyObject* out = PyList_New(T);
+  if (!out) return nullptr;
+  for (Py_ssize_t t = 0; t < T; ++t) PyList_SET_ITEM(out, t, PyLong_FromSsize_t(sz[t].second));
+  return out;
+}
+
+// {code: bytes of the int64 table} for every non-empty code; -1 on error
+int add_tables(PyObject* dict, const std::vector<int64_t> (&tab)[5]) {
+  for (int c = 0; c < 5; ++c) {
+    if (tab[c].empty()) continue;
+    PyObject* k = PyLong_FromLong(c);
+    PyObject* b = PyBytes_FromStringAndSize(reinterpret_cast<const char*>(tab[c].data()),
+                                            Py_ssize_t(tab[c].size() * sizeof(int64_t)));
+    const int rc = (k && b) ? PyDict_SetItem(dict, k, b) : -1;
+    Py_XDECREF(k);
+    Py_XDECREF(b);
+    if (rc) return -1;
+  }
+  return 0;
+}
+
+PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc) {
   const Py_ssize_t K = PyList_GET_SIZE(dicts), T = PyList_GET_SIZE(keys);
   if (K < 1) Py_RETURN_NONE;
   for (Py_ssize_t i = 0; i < K; ++i)
@@ -103,34 +155,55 @@ PyObject* walk_impl(PyObject* dicts, PyObject* keys) {
     }
   }
 
+  // outputs only once every key has passed, so a declined walk allocates nothing
+  std::vector<at::Tensor> outs;
+  std::vector<int64_t> otab[5];
+  if (alloc) {
+    outs.reserve(T);
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      const at::Tensor& x0 = THPVariable_Unpack(PyDict_GetItem(PyList_GET_ITEM(dicts, 0), PyList_GET_ITEM(keys, t)));
+      outs.push_back(at::empty(x0.sizes(), x0.options().dtype(codes[t] == 4 ? at::kFloat : x0.scalar_type())));
+      const auto p = reinterpret_cast<intptr_t>(outs.back().data_ptr());
+      if (p & 15) Py_RETURN_NONE;  // the caching allocator never does this
+      otab[codes[t]].push_back(static_cast<int64_t>(p));
+    }
+  }
+
   PyObject* py_codes = PyList_New(T);
   PyObject* py_numels = PyList_New(T);
   PyObject* tables = PyDict_New();
+  PyObject* py_outs = nullptr;
+  PyObject* out_tables = nullptr;
   if (!py_codes || !py_numels || !tables) goto fail;
   for (Py_ssize_t t = 0; t < T; ++t) {
     PyList_SET_ITEM(py_codes, t, PyLong_FromLong(codes[t]));
     PyList_SET_ITEM(py_numels, t, PyLong_FromLongLong(numels[t]));
   }
-  for (int c = 0; c < 5; ++c) {
-    if (tab[c].empty()) continue;
-    PyObject* k = PyLong_FromLong(c);
-    PyObject* b = PyBytes_FromStringAndSize(reinterpret_cast<const char*>(tab[c].data()),
-                                            Py_ssize_t(tab[c].size() * sizeof(int64_t)));
-    const int rc = (k && b) ? PyDict_SetItem(tables, k, b) : -1;
-    Py_XDECREF(k);
-    Py_XDECREF(b);
-    if (rc) goto fail;
+  if (add_tables(tables, tab)) goto fail;
+  if (alloc) {
+    py_outs = PyList_New(T);
+    out_tables = PyDict_New();
+    if (!py_outs || !out_tables || add_tables(out_tables, otab)) goto fail;
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      PyObject* o = THPVariable_Wrap(std::move(outs[t]));
+      if (!o) goto fail;
+      PyList_SET_ITEM(py_outs, t, o);
+    }
+    return Py_BuildValue("(iNNNNN)", device, py_codes, py_numels, tables, py_outs, out_tables);
   }
   return Py_BuildValue("(iNNN)", device, py_codes, py_numels, tables);
 fail:
   Py_XDECREF(py_codes);
   Py_XDECREF(py_numels);
   Py_XDECREF(tables);
+  Py_XDECREF(py_outs);
+  Py_XDECREF(out_tables);
   return nullptr;
 }
 
 PyMethodDef kMethods[] = {
     {"walk", walk, METH_VARARGS, "Pointer tables of K device state dicts for fedagg_wsum_multi, or None."},
+    {"order_by_size", order_by_size, METH_VARARGS, "Key indices of a state dict, largest tensor first, or None."},
     {nullptr, nullptr, 0, nullptr},
 };
 

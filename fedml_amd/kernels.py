@@ -162,6 +162,7 @@ class MultiPlan:
             begin.append(begin[-1] + nb)
         self.block_begin = begin
         self.total_blocks = begin[-1]
+        self._meta = {}
 
     def launch(self, src_ptrs, out_ptrs: List[int], d_w: torch.Tensor, K: int,
                device: torch.device) -> List[torch.Tensor]:
@@ -172,18 +173,24 @@ class MultiPlan:
         T = len(self.numels)
         if isinstance(src_ptrs, (bytes, bytearray)):
             src_ptrs = np.frombuffer(src_ptrs, dtype=np.int64)
+        if isinstance(out_ptrs, (bytes, bytearray)):
+            out_ptrs = np.frombuffer(out_ptrs, dtype=np.int64)
         if len(src_ptrs) != T * K or len(out_ptrs) != T:
             raise ValueError("MultiPlan.launch: table sizes do not match the plan")
-        # numels and block starts travel in one upload, pointers in another
-        d_meta = upload_i64(self.numels + self.block_begin, device)
-        if isinstance(src_ptrs, np.ndarray):
-            tab = np.concatenate([src_ptrs.astype(np.int64, copy=False), np.asarray(out_ptrs, dtype=np.int64)])
+        # numels and block starts: uploaded once per device and stream (the
+        # upload is ordered on that stream before every later launch on it)
+        st = nat.stream_handle()
+        d_meta = self._meta.get((device, st))
+        if d_meta is None:
+            d_meta = self._meta[(device, st)] = upload_i64(self.numels + self.block_begin, device)
+        if isinstance(src_ptrs, np.ndarray) or isinstance(out_ptrs, np.ndarray):
+            tab = np.concatenate([np.asarray(src_ptrs, dtype=np.int64), np.asarray(out_ptrs, dtype=np.int64)])
         else:
             tab = list(src_ptrs) + list(out_ptrs)
         d_tab = upload_i64(tab, device)
         nat.check(nat.lib().fedagg_wsum_multi(self.dt, self.acc_mode, d_tab.data_ptr(), d_tab.data_ptr() + 8 * T * K,
                                               d_meta.data_ptr(), d_meta.data_ptr() + 8 * T, T, d_w.data_ptr(), K,
-                                              self.total_blocks, nat.stream_handle()), "wsum_multi")
+                                              self.total_blocks, st), "wsum_multi")
         return [d_meta, d_tab]
 
 

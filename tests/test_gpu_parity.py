@@ -158,6 +158,49 @@ def test_native_walker_takes_device_dicts(cuda_device):
         gu.assert_same(res[key].cpu(), exp[key], key)
 
 
+def test_native_walker_allocates_outputs(cuda_device):
+    """walk(..., alloc=True): one output per key, client 0's shape, float32 for
+    int64 keys, on the inputs' device, and the output pointer tables match."""
+    import numpy as np
+
+    from fedml_amd import _native as nat
+
+    w = ao._walker()
+    entries = shapes.resnet50()[:12]
+    raw = _to_device(host_clients(entries, 2, seed=4, round_idx=1), cuda_device)
+    keys = list(raw[0][1].keys())
+    dev, codes, numels, tables, outs, out_tables = w.walk([d for _, d in raw], keys, True)
+    assert len(outs) == len(keys)
+    for k, c, o in zip(keys, codes, outs):
+        t0 = raw[0][1][k]
+        assert o.shape == t0.shape and o.is_cuda and o.device == t0.device and o.is_contiguous()
+        assert o.dtype == (torch.float32 if c == nat.DT_I64 else t0.dtype)
+    for c, tab in out_tables.items():
+        ptrs = np.frombuffer(tab, dtype=np.int64).tolist()
+        assert ptrs == [o.data_ptr() for o, cc in zip(outs, codes) if cc == c]
+
+
+def test_pipelined_walk_declines_in_a_later_chunk(cuda_device):
+    """A small key (walked in the last chunk, after larger keys were already
+    launched) that the walker declines: the general path recomputes every key
+    and the result is still the reference's."""
+    w = ao._walker()
+    entries = shapes.resnet50()
+    raw = _to_device(host_clients(entries, 3, seed=6, round_idx=2), cuda_device)
+    keys = list(raw[0][1].keys())
+    order = w.order_by_size(raw[0][1], keys)
+    small = keys[order[-1]]
+    assert order.index(keys.index(small)) >= 112  # not in the first chunks
+    args = type("A", (), {"federated_optimizer": "FedAvg"})()
+    exp = orc.agg(args, [(n, OrderedDict((k, t.cpu()) for k, t in d.items())) for n, d in raw])
+    t = raw[2][1][small]
+    raw[2][1][small] = torch.empty(t.numel() * 2 + 2, dtype=t.dtype, device=t.device)[1::2][:t.numel()].view(t.shape)
+    raw[2][1][small].copy_(t)
+    res = ao.FedMLAggOperator.agg(args, raw)
+    for key in exp:
+        gu.assert_same(res[key].cpu(), exp[key], key)
+
+
 def test_unaligned_views_take_scalar_path(cuda_device):
     """Tensors that are views at odd element offsets (not 16-byte aligned)."""
     K, N = 5, 4099

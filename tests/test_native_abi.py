@@ -195,3 +195,26 @@ def test_dict_walker_builds_and_declines_host_inputs():
     assert w.walk([OrderedDict(a=torch.ones(3).to_sparse())], ["a"]) is None  # non-strided: no C++ throw escapes
     with pytest.raises(TypeError):
         w.walk([OrderedDict()], [["unhashable"]])
+
+
+def test_dict_walker_order_by_size():
+    """order_by_size: key indices largest tensor first, ties in key order;
+    None where the walk would decline (missing key, non-tensor, custom dict)."""
+    from fedml_amd import agg_operator as ao
+
+    w = ao._walker()
+    d = OrderedDict(a=torch.ones(3), b=torch.ones(10), c=torch.ones(3), d=torch.ones(()), e=torch.ones(2, 5))
+    assert w.order_by_size(d, list(d)) == [1, 4, 0, 2, 3]
+    assert w.order_by_size(d, ["a", "zz"]) is None
+    assert w.order_by_size(OrderedDict(a=1), ["a"]) is None
+
+    class Custom(dict):
+        def __getitem__(self, k):
+            return super().__getitem__(k)
+
+    assert w.order_by_size(Custom(a=torch.ones(3)), ["a"]) is None
+    assert w.walk([d], list(d), True) is None  # host tensors: declined before allocating
+    assert [list(c) for c in ao._chunks(list(range(300)))] == [list(range(0, 16)), list(range(16, 48)),
+                                                              list(range(48, 112)), list(range(112, 208)),
+                                                              list(range(208, 300))]
+
