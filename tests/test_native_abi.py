@@ -218,3 +218,20 @@ def test_dict_walker_order_by_size():
                                                               list(range(48, 112)), list(range(112, 208)),
                                                               list(range(208, 300))]
 
+
+def test_dict_walker_pool_under_repeated_walks():
+    """Walks of >= 4096 tensors validate on the walker's thread pool: repeated
+    back-to-back walks finish (no lost wake-up or stale worker) and decline
+    host tensors every time; subclass values (nn.Parameter) are declined
+    before any validation thread sees them."""
+    from fedml_amd import agg_operator as ao
+
+    w = ao._walker()
+    keys = [f"k{t}" for t in range(64)]
+    dicts = [OrderedDict((k, torch.zeros(2)) for k in keys) for _ in range(128)]
+    for _ in range(300):
+        assert w.walk(dicts, keys) is None
+        assert w.walk(dicts, keys[:8], True) is None  # below the pool threshold
+    dicts[5][keys[3]] = torch.nn.Parameter(torch.zeros(2))
+    assert w.walk(dicts, keys) is None
+
