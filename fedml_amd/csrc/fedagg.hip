@@ -988,42 +988,41 @@ int launch_median(const float* const* src, int K, int64_t N, float* out, hipStre
   return check_launch("fedagg_median_f32");
 }
 
-// More than 128 clients, in registers: P = 2, 4 or 8 adjacent lanes share one
-// column, each lane holding 128 of its KMAX = 128·P (±inf-padded) values,
-// slot s = sub·128 + j = client s.  Every lane sorts its 128 values with the
-// pairwise network (all outputs used, so nothing is pruned); the sorted runs
-// are then merged across lanes as in a bitonic merge sort:
+// More than 128 clients, in registers: P adjacent lanes share one column,
+// each holding R of its KMAX = P·R (±inf-padded) values, slot s = sub·R + j =
+// client s (shipped: P = 4, R = 64 up to 256 clients, then R = 128 with P = 4
+// or 8).  Every lane sorts its R values with the pairwise network (all outputs
+// used, so nothing is pruned); the sorted runs are then merged across lanes as
+// in a bitonic merge sort:
 //   - "reverse pairing" of two sorted runs A, B of length L held by lane
 //     groups g and g ^ (G-1): element i of A meets element L-1-i of B, the
 //     lower group keeps the min (the L smallest, a bitonic sequence), the
-//     upper the max.  Partner lane = sub ^ (G-1), partner register = 127 - i;
-//   - a half-cleaner cascade sorts each bitonic half: a stage whose slot
-//     distance is 128 pairs lane sub with sub ^ 1 at the same register, the
-//     rest run inside the lane.
-// Cross-lane moves are single DPP movs (xor 1 / 3 quad permutes, xor 7 =
-// row_half_mirror), the min-or-max choice one v_med3 against ±inf.  The last
-// level needs no merge: after its reverse pairing the lower half holds exactly
-// the KMAX/2 smallest values, whose maximum sits at the padded median slot
-// KMAX/2 - 1, i.e. it is the column's lower median.  VALU per column ≈ 7k
-// (P = 2), 19k (P = 4), 49k (P = 8) lane-ops, against 2k for K <= 128.
+//     upper the max.  Partner lane = sub ^ (G-1), partner register = R-1-i;
+//   - a half-cleaner cascade sorts each bitonic half: stages whose slot
+//     distance is a multiple of R pair lane sub with sub ^ m at the same
+//     register, the rest run inside the lane.
+// Cross-lane moves are single DPP movs (xor 1 / 2 / 3 quad permutes, xor 7 =
+// row_half_mirror, xor 15 = row_mirror), the min-or-max choice one v_med3
+// against ±inf.  The last level needs no merge: after its reverse pairing the
+// lower half holds exactly the KMAX/2 smallest values, whose maximum sits at
+// the padded median slot KMAX/2 - 1, i.e. it is the column's lower median.
+// VALU per column ≈ 8k (P·R = 4·64), 20k (4·128), 49k (8·128) lane-ops,
+// against 2k for K <= 128.
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float x) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
 }
 template <int M>
 constexpr int dpp_xor_ctrl() {
-  static_assert(M == 1 || M == 2 || M == 3 || M == 7, "lane xor pattern without a single DPP mov");
-  // quad_perm [1,0,3,2], [2,3,0,1], [3,2,1,0]; row_half_mirror
-  return M == 1 ? 0xB1 : M == 2 ? 0x4E : M == 3 ? 0x1B : 0x141;
+  static_assert(M == 1 || M == 2 || M == 3 || M == 7 || M == 15, "lane xor pattern without a single DPP mov");
+  // quad_perm [1,0,3,2], [2,3,0,1], [3,2,1,0]; row_half_mirror; row_mirror
+  return M == 1 ? 0xB1 : M == 2 ? 0x4E : M == 3 ? 0x1B : M == 7 ? 0x141 : 0x140;
 }
 
-constexpr int kLaneVals = 128;
-
 // min (lower lanes, sel = -inf) or max (upper lanes, sel = +inf) of own
-// register i and the partner lane's register 127 - i, for every i
-template <int M>
-__device__ __forceinline__ void lanes_reverse_pair(float (&v)[kLaneVals], float sel) {
-  constexpr int R = kLaneVals;
+// register i and the partner lane's register R-1-i, for every i
+template <int M, int R>
+__device__ __forceinline__ void lanes_reverse_pair(float (&v)[R], float sel) {
   // opaque to the compiler: knowing sel is ±inf it splits every v_med3 into
   // min, max and a select (three ops and twice the live registers)
   asm volatile("" : "+v"(sel));
@@ -1036,42 +1035,48 @@ __device__ __forceinline__ void lanes_reverse_pair(float (&v)[kLaneVals], float 
   }
 }
 
+// half-cleaner stage between lanes sub and sub ^ M, same register
+template <int M, int R>
+__device__ __forceinline__ void lanes_cross_stage(float (&v)[R], int sub) {
+  float sel = (sub & M) ? __builtin_huge_valf() : -__builtin_huge_valf();
+  asm volatile("" : "+v"(sel));
+#pragma unroll
+  for (int i = 0; i < R; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], dpp_mov<dpp_xor_ctrl<M>()>(v[i]), sel);
+}
+
 // in-lane half-cleaner cascade: a bitonic register array -> ascending
-__device__ __forceinline__ void lane_bitonic_merge(float (&v)[kLaneVals]) {
+template <int R>
+__device__ __forceinline__ void lane_bitonic_merge(float (&v)[R]) {
 #pragma unroll
-  for (int d = kLaneVals / 2; d > 0; d /= 2) {
+  for (int d = R / 2; d > 0; d /= 2) {
 #pragma unroll
-    for (int i = 0; i < kLaneVals; ++i)
+    for (int i = 0; i < R; ++i)
       if ((i & d) == 0) cmpx(v[i], v[i + d]);
   }
 }
 
-// merge levels G = 2, 4 (< P): afterwards every group of G lanes holds its
-// G·128 values sorted ascending over slots (sub % G)·128 + j
-template <int G, int P>
-__device__ __forceinline__ void lanes_merge_levels(float (&v)[kLaneVals], int sub) {
+// merge levels G = 2, 4, 8 (< P): afterwards every group of G lanes holds its
+// G·R values sorted ascending over slots (sub % G)·R + j
+template <int G, int P, int R>
+__device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
   if constexpr (G < P) {
-    static_assert(G <= 4, "a level of 8 lanes would need xor-2 and xor-4 stages");
-    constexpr float inf = __builtin_huge_valf();
-    lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) ? inf : -inf);
-    if constexpr (G == 4) {  // slot distance 128: lane sub ^ 1, same register
-      float sel = (sub & 1) ? inf : -inf;
-      asm volatile("" : "+v"(sel));
-#pragma unroll
-      for (int i = 0; i < kLaneVals; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], dpp_mov<dpp_xor_ctrl<1>()>(v[i]), sel);
-    }
+    static_assert(G <= 8, "a level of 16 lanes would need an xor-4 stage");
+    lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) ? __builtin_huge_valf() : -__builtin_huge_valf());
+    if constexpr (G == 8) lanes_cross_stage<2>(v, sub);  // slot distance 2R
+    if constexpr (G >= 4) lanes_cross_stage<1>(v, sub);  // slot distance R
     lane_bitonic_merge(v);
-    lanes_merge_levels<G * 2, P>(v, sub);
+    lanes_merge_levels<G * 2, P, R>(v, sub);
   }
 }
 
 __device__ float g_median_pad[2] = {-__builtin_huge_valf(), __builtin_huge_valf()};
 
-template <int P, bool FULL>
+template <int P, int R, bool FULL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
     const float* const* __restrict__ src, int K, int64_t N, float* __restrict__ out) {
-  static_assert(P == 2 || P == 4 || P == 8, "2, 4 or 8 lanes per column");
-  constexpr int R = kLaneVals, KMAX = P * R, PAD = 2;
+  static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2, 4, 8 or 16 lanes per column");
+  static_assert(R == 64 || R == 128, "64 or 128 values per lane");
+  constexpr int KMAX = P * R, PAD = 2;
   // Row pointer of every slot, skewed by PAD entries per lane group so the P
   // lanes of a column read different LDS banks.  A padded slot (K < KMAX)
   // points at a ±inf constant and its column offset is masked to 0, so the
@@ -1129,7 +1134,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
     }
   }
   pairwise_sort<R>(v);
-  lanes_merge_levels<2, P>(v, sub);
+  lanes_merge_levels<2, P, R>(v, sub);
   // last level: after the reverse pairing against sub ^ (P-1) the lower P/2
   // lanes hold the KMAX/2 smallest values; their max is the median
   lanes_reverse_pair<P - 1>(v, (sub & (P / 2)) ? __builtin_huge_valf() : -__builtin_huge_valf());
@@ -1138,17 +1143,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
   for (int i = 1; i < R; ++i) m = fmaxf(m, v[i]);
   if constexpr (P >= 4) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
   if constexpr (P >= 8) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
+  if constexpr (P >= 16) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima across the two quads
   if (sub == 0 && e < N) out[e] = nan_slot < KMAX ? nan_v : m;
 }
 
-template <int P>
+template <int P, int R>
 int launch_median_lanes(const float* const* src, int K, int64_t N, float* out, hipStream_t st) {
   const int64_t grid = (N * P + 255) / 256;
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N too large");
-  if (K == P * kLaneVals)
-    hipLaunchKernelGGL((median_lanes_kernel<P, true>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+  if (K == P * R)
+    hipLaunchKernelGGL((median_lanes_kernel<P, R, true>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
   else
-    hipLaunchKernelGGL((median_lanes_kernel<P, false>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+    hipLaunchKernelGGL((median_lanes_kernel<P, R, false>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
   return check_launch("fedagg_median_f32");
 }
 
@@ -1530,9 +1536,9 @@ int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_
   if (N == 0) return FEDAGG_OK;
   auto st = reinterpret_cast<hipStream_t>(stream);
   if (K > 128) {  // 2, 4 or 8 lanes per column, register sort + cross-lane merges
-    if (K <= 256) return launch_median_lanes<2>(d_src, K, N, d_out, st);
-    if (K <= 512) return launch_median_lanes<4>(d_src, K, N, d_out, st);
-    if (K <= 1024) return launch_median_lanes<8>(d_src, K, N, d_out, st);
+    if (K <= 256) return launch_median_lanes<4, 64>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
+    if (K <= 512) return launch_median_lanes<4, 128>(d_src, K, N, d_out, st);
+    if (K <= 1024) return launch_median_lanes<8, 128>(d_src, K, N, d_out, st);
     return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K > 1024 clients is not supported");
   }
   // the register kernels address rows with 32-bit byte offsets

@@ -149,20 +149,30 @@ extern "C" const char* median_probe_name(int v) {
 }
 
 // More than 128 clients: v = 0 the LDS-tile radix select, v = 1 the
-// lane-group register sort (the shipped path)
+// lane-group register sort with 128 values per lane (shipped), v = 2 the same
+// with 64 values per lane and twice the lanes; for K <= 128: v = 4 the
+// shipped one-lane pruned network, v = 3 two lanes of 64
 extern "C" int median_big_probe(int v, const void* src, int K, int64_t N, void* out, void* stream) {
   auto s = reinterpret_cast<const float* const*>(src);
   auto o = reinterpret_cast<float*>(out);
   auto st = reinterpret_cast<hipStream_t>(stream);
-  if (K <= 128 || K > 1024 || N <= 0) return -1;
+  if (K > 1024 || N <= 0) return -1;
+  if (v == 3) return K <= 128 ? launch_median_lanes<2, 64>(s, K, N, o, st) : -1;  // K <= 128, two lanes
+  if (v == 4) return K <= 128 ? launch_median<128>(s, K, N, o, st) : -1;         // K <= 128, shipped
+  if (K <= 128) return -1;
   if (v == 0) {
     if (K <= 256) return launch_median_radix<256>(s, K, N, o, st);
     if (K <= 512) return launch_median_radix<512>(s, K, N, o, st);
     return launch_median_radix<1024>(s, K, N, o, st);
   }
-  if (K <= 256) return launch_median_lanes<2>(s, K, N, o, st);
-  if (K <= 512) return launch_median_lanes<4>(s, K, N, o, st);
-  return launch_median_lanes<8>(s, K, N, o, st);
+  if (v == 1) {
+    if (K <= 256) return launch_median_lanes<2, 128>(s, K, N, o, st);
+    if (K <= 512) return launch_median_lanes<4, 128>(s, K, N, o, st);
+    return launch_median_lanes<8, 128>(s, K, N, o, st);
+  }
+  if (K <= 256) return launch_median_lanes<4, 64>(s, K, N, o, st);
+  if (K <= 512) return launch_median_lanes<8, 64>(s, K, N, o, st);
+  return launch_median_lanes<16, 64>(s, K, N, o, st);
 }
 
 // K is fixed at 128 (the full kernel); src is a device table of 128 row pointers

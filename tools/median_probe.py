@@ -92,33 +92,38 @@ def probe_k128(lib, kn, dev, st):
 
 
 def probe_big(lib, kn, dev, st, summary):
-    """More than 128 clients: LDS-tile radix select (v0) vs lane-group register
-    sort (v1, shipped), interleaved; their outputs must agree bit for bit."""
+    """More than 128 clients: LDS-tile radix select (v0), lane-group register
+    sort with 128 values per lane (v1) and with 64 per lane (v2), interleaved;
+    at K = 128 the shipped pruned network (v4) against two lanes of 64 (v3).
+    All outputs must agree bit for bit."""
     lib.median_big_probe.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
                                      ctypes.c_void_p]
+    names = {0: "radix", 1: "lanes128", 2: "lanes64", 3: "lanes64x2", 4: "net128"}
     N2 = 4_000_000
-    for K2 in (129, 256, 257, 512, 513, 1024):
+    for K2 in (128, 129, 256, 257, 512, 513, 1024):
+        vs = (4, 3) if K2 <= 128 else (0, 1, 2)
         rows = torch.randn((K2, N2), device=dev) * 0.05
         tab = kn.upload_i64([rows[i].data_ptr() for i in range(K2)], dev)
-        outs = [torch.empty(N2, device=dev) for _ in range(2)]
-        ts = [[], []]
-        for v in (0, 1):
+        outs = {v: torch.empty(N2, device=dev) for v in vs}
+        ts = {v: [] for v in vs}
+        for v in vs:
             assert lib.median_big_probe(v, tab.data_ptr(), K2, N2, outs[v].data_ptr(), st) == 0
         torch.cuda.synchronize()
-        same_bits = bool(torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)))
+        ref = outs[vs[0]].view(torch.int32)
+        same_bits = all(bool(torch.equal(ref, outs[v].view(torch.int32))) for v in vs[1:])
         for _ in range(5):
-            for v in (0, 1):
+            for v in vs:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 lib.median_big_probe(v, tab.data_ptr(), K2, N2, outs[v].data_ptr(), st)
                 e1.record()
                 torch.cuda.synchronize()
                 ts[v].append(e0.elapsed_time(e1))
-        for v, name in ((0, "radix"), (1, "lanes")):
+        for v in vs:
             ms = statistics.median(ts[v])
-            summary[f"{name}_K{K2}_N{N2}"] = {"ms": round(ms, 4), "GBps": round((K2 + 1) * N2 * 4 / ms / 1e6, 1)}
-        summary[f"K{K2}_radix_equals_lanes"] = same_bits
-        print(K2, summary[f"radix_K{K2}_N{N2}"], summary[f"lanes_K{K2}_N{N2}"], same_bits, flush=True)
+            summary[f"{names[v]}_K{K2}_N{N2}"] = {"ms": round(ms, 4), "GBps": round((K2 + 1) * N2 * 4 / ms / 1e6, 1)}
+        summary[f"K{K2}_variants_agree"] = same_bits
+        print(K2, {names[v]: summary[f"{names[v]}_K{K2}_N{N2}"]["ms"] for v in vs}, same_bits, flush=True)
         del rows, tab, outs
         torch.cuda.empty_cache()
 
