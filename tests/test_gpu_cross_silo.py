@@ -1,0 +1,163 @@
+"""The cross-silo FedMLAggregator mirror (fedml_amd.cross_silo): updates
+ingested into HBM on arrival, then the reference's aggregate() flow, checked
+bit for bit against the oracle restatement of the reference's FedAvg."""
+from __future__ import annotations
+
+import copy
+from collections import OrderedDict
+
+import pytest
+import torch
+
+import golden_util as gu
+from fedml_amd import shapes
+from fedml_amd.cross_silo import FedMLAggregator
+from fedml_amd.server_aggregator import MI355XServerAggregator
+from fedml_amd.synth import host_clients
+from oracle import fedavg_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+class _Args:
+    federated_optimizer = "FedAvg"
+
+
+def _model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(37, 19), torch.nn.BatchNorm1d(19), torch.nn.Linear(19, 3))
+
+
+def _server(model, K, device):
+    args = _Args()
+    return FedMLAggregator(None, None, 0, {}, {}, {}, K, device, args, MI355XServerAggregator(model, args))
+
+
+def _round(model, K, seed, round_idx):
+    entries = [(k, tuple(t.shape), t.dtype) for k, t in model.state_dict().items()]
+    return host_clients(entries, K, seed=seed, round_idx=round_idx)
+
+
+def _keyless_server(K, device):
+    """A server whose model does not carry the test's keys (set_model_params is a no-op)."""
+    args = _Args()
+    agg = MI355XServerAggregator(torch.nn.Linear(1, 1), args)
+    agg.set_model_params = lambda p: None
+    return FedMLAggregator(None, None, 0, {}, {}, {}, K, device, args, agg)
+
+
+@pytest.mark.parametrize("K", [1, 3, 8])
+def test_rounds_match_reference(K, cuda_device):
+    """Two rounds on the same slots: each aggregate equals the reference's
+    FedAvg of that round's host updates; the dicts handed over now hold device
+    views with the updates' values and dtypes (what model_params_to_device
+    leaves behind), and the server model holds the average."""
+    model = _model().to(cuda_device)
+    server = _server(model, K, cuda_device)
+    for r in range(2):
+        raw = _round(model, K, seed=10 + r, round_idx=r)
+        exp = orc.agg(_Args(), copy.deepcopy(raw))
+        for i, (n, d) in enumerate(raw):
+            host_vals = OrderedDict((k, t.clone()) for k, t in d.items())
+            server.add_local_trained_result(i, d, n)
+            for k, t in d.items():
+                assert t.is_cuda and t.dtype == host_vals[k].dtype
+                gu.assert_same(t.cpu(), host_vals[k], f"view {k}")
+        assert server.check_whether_all_receive()
+        averaged, model_list, idxes = server.aggregate()
+        assert idxes == list(range(K))
+        assert averaged is model_list[0][1]  # the reference returns client 0's dict, keys rebound
+        for k in exp:
+            gu.assert_same(averaged[k].cpu(), exp[k], f"round {r} {k}")
+        sd = model.state_dict()
+        for k in exp:
+            if exp[k].dtype == sd[k].dtype:
+                gu.assert_same(sd[k].cpu(), exp[k], f"model {k}")
+        assert not server.check_whether_all_receive()
+
+
+def test_resnet50_round(cuda_device):
+    """Config 3's state dict (fp32 + int64 counters) through arrival and
+    aggregate: all 320 keys bit-exact."""
+    K = 4
+    raw = host_clients(shapes.resnet50(), K, seed=3, round_idx=5)
+    exp = orc.agg(_Args(), copy.deepcopy(raw))
+    server = _keyless_server(K, cuda_device)
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    assert server.bucket is not None and set(server.bucket.groups) == {torch.float32, torch.int64}
+    averaged, _, _ = server.aggregate()
+    for k in exp:
+        assert averaged[k].dtype == exp[k].dtype, k
+        gu.assert_same(averaged[k].cpu(), exp[k], k)
+
+
+def test_plain_dicts_stay_on_the_host(cuda_device):
+    """Plain dicts are left where the user put them (:61-62).  FedAvg then
+    returns client 0's plain dict, which :90-97 read as a per-client dict
+    {client_index: params}: the reference raises KeyError there, and so does
+    the mirror, after the reduction itself ran correctly on the host inputs."""
+    model = _model().to(cuda_device)
+    K = 3
+    server = _server(model, K, cuda_device)
+    raw = [(n, dict(d)) for n, d in _round(model, K, seed=22, round_idx=0)]
+    exp = orc.agg(_Args(), copy.deepcopy(raw))
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    assert server.bucket is None and all(not t.is_cuda for _, d in raw for t in d.values())
+    with pytest.raises(KeyError):
+        server.aggregate()
+    averaged = raw[0][1]  # keys rebound to the average before the KeyError
+    for k in exp:
+        assert not averaged[k].is_cuda
+        gu.assert_same(averaged[k], exp[k], k)
+
+
+def test_mixed_residency_raises_like_the_reference(cuda_device):
+    """One plain (host) dict among moved ones: the reference's `avg += p * w`
+    fails on mixed devices with a RuntimeError, and so does this."""
+    model = _model().to(cuda_device)
+    K = 3
+    server = _server(model, K, cuda_device)
+    raw = _round(model, K, seed=23, round_idx=0)
+    raw[1] = (raw[1][0], dict(raw[1][1]))
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    with pytest.raises(RuntimeError):
+        server.aggregate()
+
+
+def test_other_layout_moves_key_by_key(cuda_device):
+    """An update whose layout differs from the first client's is moved key by
+    key as in the reference; the result is unchanged."""
+    model = _model().to(cuda_device)
+    K = 3
+    server = _server(model, K, cuda_device)
+    raw = _round(model, K, seed=21, round_idx=0)
+    extra = OrderedDict(raw[2][1])
+    extra["unused.extra"] = torch.ones(3)  # not among client 0's keys: FedAvg ignores it
+    raw[2] = (raw[2][0], extra)
+    exp = orc.agg(_Args(), copy.deepcopy([(n, OrderedDict((k, v) for k, v in d.items() if k != "unused.extra"))
+                                          for n, d in raw]))
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    assert all(t.is_cuda for t in raw[2][1].values())
+    averaged, _, _ = server.aggregate()
+    for k in exp:
+        gu.assert_same(averaged[k].cpu(), exp[k], k)
+
+
+def test_int32_key_moves_key_by_key(cuda_device):
+    """A dtype the bucket would widen (int32) keeps the reference's per-key move."""
+    K = 2
+    d0 = OrderedDict(w=torch.randn(5), c=torch.arange(4, dtype=torch.int32))
+    d1 = OrderedDict(w=torch.randn(5), c=torch.arange(4, dtype=torch.int32) * 3)
+    raw = [(3, d0), (5, d1)]
+    exp = orc.agg(_Args(), copy.deepcopy(raw))
+    server = _keyless_server(K, cuda_device)
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    assert server.bucket is None and d0["c"].is_cuda and d0["c"].dtype == torch.int32
+    averaged, _, _ = server.aggregate()
+    for k in exp:
+        gu.assert_same(averaged[k].cpu(), exp[k], k)
