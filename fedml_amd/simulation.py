@@ -1,0 +1,45 @@
+"""The single-process simulators' copy of the FedAvg reduction, on MI355X.
+
+FedAvgAPI._aggregate (python/fedml/simulation/sp/fedavg/fedavg_api.py:144-159)
+and FedOptAPI._aggregate (sp/fedopt/fedopt_api.py:143-158) restate the plugin
+operator's FedAvg loop without ``args``: Σn with a Python loop, then
+avg[k] = p_0[k]·w_0, avg[k] += p_i[k]·w_i, w_i = n_i / Σn, rebinding the keys of
+client 0's dict.  ``fedavg_aggregate`` keeps that contract (same unpacking and
+so the same ValueError, ZeroDivisionError at Σn = 0, the same returned object)
+and runs the reduction in libfedagg.so through fedml_amd.agg_operator.
+
+A simulator swaps the method in one line:
+
+    FedAvgAPI._aggregate = lambda self, w_locals: fedavg_aggregate(w_locals)
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+from .agg_operator import weighted_reduce
+
+
+class _Defaults:
+    """The reduction options fedml_amd reads from FedML's args, at their defaults."""
+
+    fedagg_low_precision_acc = "reference"
+    fedagg_device = None
+
+
+def fedavg_aggregate(w_locals: List[Tuple[float, "OrderedDict"]], args=None) -> "OrderedDict":
+    """fedavg_api.py:144-159.  ``args`` (optional) may carry the fedml_amd
+    options ``fedagg_device`` / ``fedagg_low_precision_acc``."""
+    training_num = 0
+    for idx in range(len(w_locals)):
+        (sample_num, averaged_params) = w_locals[idx]
+        training_num += sample_num
+    (sample_num, averaged_params) = w_locals[0]
+    keys = list(averaged_params.keys())
+    if not keys:
+        return averaged_params
+    weights = [w_locals[i][0] / training_num for i in range(len(w_locals))]
+    res = weighted_reduce([w_locals[i][1] for i in range(len(w_locals))], keys, weights,
+                          args if args is not None else _Defaults())
+    for k in keys:
+        averaged_params[k] = res[k]
+    return averaged_params
