@@ -223,6 +223,35 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
     return OrderedDict((k, results[k]) for k in keys)
 
 
+_BATCH_MAX_BYTES = 256 << 20  # host rounds up to this size stage every client in one pack + one H2D
+_ROW_ESZ = {nat.DT_F32: 4, nat.DT_BF16: 2, nat.DT_F16: 2, nat.DT_F64: 8, nat.DT_I64: 8}
+
+
+def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
+    """Small host rounds (every key a contiguous CPU tensor of a row dtype,
+    the whole round <= 256 MB): the walker's host pointer tables drive ONE
+    native pack of all clients per dtype into pinned staging, ONE H2D, one
+    launch per dtype and one D2H, instead of a Python pass per client.  None
+    when the walk declines or the round is large (the per-client staging ring
+    then overlaps packing with the DMA)."""
+    walked = w.walk_host(dicts, keys)
+    if walked is None:
+        return None
+    codes, numels, tables = walked
+    K = len(dicts)
+    if K * sum(n * _ROW_ESZ[c] for n, c in zip(numels, codes)) > _BATCH_MAX_BYTES:
+        return None
+    d0 = dicts[0]
+    device = _host_device(args)
+    with torch.cuda.device(device):
+        bucket = _cached_bucket([(k, tuple(d0[k].shape), d0[k].dtype) for k in keys], K, device,
+                                _ACC_NAME[acc_mode])
+        bucket.put_batch(tables, dicts, [1] * K)
+        outs = bucket.new_outputs()
+        bucket.reduce_into(outs, weights)
+        return bucket.to_host(outs)
+
+
 def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights: Sequence[float], args
                     ) -> "OrderedDict[str, torch.Tensor]":
     """avg[k] = Σ_i fl(p_i[k] · w_i) in client order for every key (the FedAvg
@@ -232,6 +261,9 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
     w = _walker()
     if w is not None and keys:
         res = _reduce_device_walked(w, list(dicts), list(keys), weights, acc_mode)
+        if res is not None:
+            return res
+        res = _reduce_host_batched(w, list(dicts), list(keys), weights, args, acc_mode)
         if res is not None:
             return res
     per_key = _gather(dicts, keys)

@@ -132,6 +132,19 @@ class Pool {
   uint64_t gen_ = 0;
 };
 
+// FEDAGG_DT_* codes of the row dtypes a ClientBucket stores without
+// conversion (the host walk feeds a byte-for-byte pack)
+int row_code(c10::ScalarType s) {
+  switch (s) {
+    case c10::ScalarType::Float: return 0;
+    case c10::ScalarType::BFloat16: return 1;
+    case c10::ScalarType::Half: return 2;
+    case c10::ScalarType::Double: return 3;
+    case c10::ScalarType::Long: return 4;
+    default: return -1;
+  }
+}
+
 // dict and OrderedDict share dict's lookup; anything overriding __getitem__
 // goes through the Python walk so that its own semantics apply.
 bool plain_lookup(PyObject* d) {
@@ -149,7 +162,7 @@ bool plain_lookup(PyObject* d) {
 //                float32 for int64 keys (the reference's int64 * float
 //                promotion), the dtype otherwise, on the inputs' device
 //   out_tables : (alloc) {code: bytes}, the output pointers [T_code]
-PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc);
+PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc, bool host);
 
 PyObject* walk(PyObject*, PyObject* args) {
   PyObject* dicts;
@@ -157,8 +170,24 @@ PyObject* walk(PyObject*, PyObject* args) {
   int alloc = 0;
   if (!PyArg_ParseTuple(args, "O!O!|p", &PyList_Type, &dicts, &PyList_Type, &keys, &alloc)) return nullptr;
   try {
-    return walk_impl(dicts, keys, alloc != 0);
+    return walk_impl(dicts, keys, alloc != 0, false);
   } catch (const std::exception&) {  // a tensor torch itself would refuse here: let the Python walk report it
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+}
+
+// walk_host(dicts: list, keys: list) -> None | (codes, numels, tables)
+//   as walk() for host (CPU) tensors of the bucket's row dtypes (fp32, bf16,
+//   f16, f64, int64): the pointer tables feed one fedagg_host_pack per dtype
+//   that stages every client of a small round at once.  No alignment needed.
+PyObject* walk_host(PyObject*, PyObject* args) {
+  PyObject* dicts;
+  PyObject* keys;
+  if (!PyArg_ParseTuple(args, "O!O!", &PyList_Type, &dicts, &PyList_Type, &keys)) return nullptr;
+  try {
+    return walk_impl(dicts, keys, false, true);
+  } catch (const std::exception&) {
     PyErr_Clear();
     Py_RETURN_NONE;
   }
@@ -206,7 +235,7 @@ int add_tables(PyObject* dict, const std::vector<int64_t> (&tab)[5]) {
   return 0;
 }
 
-PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc) {
+PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc, bool host) {
   const Py_ssize_t K = PyList_GET_SIZE(dicts), T = PyList_GET_SIZE(keys);
   if (K < 1) Py_RETURN_NONE;
   for (Py_ssize_t i = 0; i < K; ++i)
@@ -238,18 +267,19 @@ PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc) {
     for (int64_t t = lo; t < hi; ++t) {
       const at::Tensor* const* row = ts.data() + size_t(t) * K;
       const at::Tensor& x0 = *row[0];
-      if (!x0.defined() || x0.layout() != c10::kStrided || !x0.is_cuda()) continue;
-      const int code = multi_code(x0.scalar_type());
+      const c10::DeviceType want = host ? c10::DeviceType::CPU : c10::DeviceType::CUDA;
+      if (!x0.defined() || x0.layout() != c10::kStrided || x0.device().type() != want) continue;
+      const int code = host ? row_code(x0.scalar_type()) : multi_code(x0.scalar_type());
       if (code < 0) continue;
-      const int dev = x0.get_device();
+      const int dev = host ? -1 : x0.get_device();
       bool good = true;
       for (Py_ssize_t i = 0; i < K && good; ++i) {
         const at::Tensor& x = *row[i];
-        good = x.defined() && x.layout() == c10::kStrided && x.is_cuda() && x.is_contiguous() &&
-               x.scalar_type() == x0.scalar_type() && x.get_device() == dev && x.sizes() == x0.sizes();
+        good = x.defined() && x.layout() == c10::kStrided && x.device().type() == want && x.is_contiguous() &&
+               x.scalar_type() == x0.scalar_type() && (host || x.get_device() == dev) && x.sizes() == x0.sizes();
         if (good) {
           const auto p = reinterpret_cast<intptr_t>(x.data_ptr());
-          good = (p & 15) == 0;
+          good = host || (p & 15) == 0;
           ptrs[size_t(t) * K + i] = static_cast<int64_t>(p);
         }
       }
@@ -265,7 +295,7 @@ PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc) {
     check(0, T);
 
   std::vector<int64_t> tab[5];
-  const int device = T ? devs[0] : -1;
+  const int device = T ? devs[0] : -1;  // -1 for a host walk
   for (Py_ssize_t t = 0; t < T; ++t) {
     if (!ok[t] || devs[t] != device) Py_RETURN_NONE;
     tab[codes[t]].insert(tab[codes[t]].end(), ptrs.begin() + size_t(t) * K, ptrs.begin() + size_t(t + 1) * K);
@@ -307,6 +337,7 @@ PyObject* walk_impl(PyObject* dicts, PyObject* keys, bool alloc) {
     }
     return Py_BuildValue("(iNNNNN)", device, py_codes, py_numels, tables, py_outs, out_tables);
   }
+  if (host) return Py_BuildValue("(NNN)", py_codes, py_numels, tables);
   return Py_BuildValue("(iNNN)", device, py_codes, py_numels, tables);
 fail:
   Py_XDECREF(py_codes);
@@ -320,6 +351,7 @@ fail:
 PyMethodDef kMethods[] = {
     {"walk", walk, METH_VARARGS, "Pointer tables of K device state dicts for fedagg_wsum_multi, or None."},
     {"order_by_size", order_by_size, METH_VARARGS, "Key indices of a state dict, largest tensor first, or None."},
+    {"walk_host", walk_host, METH_VARARGS, "Host pointer tables of K CPU state dicts for one batched pack, or None."},
     {nullptr, nullptr, 0, nullptr},
 };
 

@@ -390,3 +390,28 @@ def test_round_f32_matches_torch_rounding(dtype, cuda_device):
         exp = x.cpu().to(torch.float16)
     gu.assert_same(got, exp, str(dtype))
 
+
+
+def test_small_host_rounds_take_the_batched_pack(cuda_device, monkeypatch):
+    """Host dicts of a small round go through one pack + one H2D per dtype
+    (bucket.put_batch), also with int64 counters promoted into the fp32 rows
+    and across rounds that reuse the cached bucket's pinned staging; results
+    stay bit-exact."""
+    calls = []
+    orig = ClientBucket.put_batch
+
+    def spy(self, *a, **kw):
+        calls.append(self.capacity)
+        return orig(self, *a, **kw)
+
+    monkeypatch.setattr(ClientBucket, "put_batch", spy)
+    args = type("A", (), {"federated_optimizer": "FedAvg"})()
+    entries = shapes.resnet50()[:24] + [("extra.f64", (5,), torch.float64), ("extra.bf16", (7, 3), torch.bfloat16)]
+    for r in range(3):
+        raw = host_clients(entries, 6, seed=40 + r, round_idx=r)
+        exp = orc.agg(args, copy.deepcopy(raw))
+        res = ao.FedMLAggOperator.agg(args, raw)
+        for k in exp:
+            assert not res[k].is_cuda and res[k].dtype == exp[k].dtype, k
+            gu.assert_same(res[k], exp[k], f"round {r} {k}")
+    assert calls == [6, 6, 6]
