@@ -187,17 +187,17 @@ def main():
         from fedml_amd import defense as dfn
 
         gd = bucket.groups[dom_dt]
-        med_out = torch.empty(gd.padded, dtype=torch.float32, device=dev)
+        med_out = torch.empty(gd.padded, dtype=gd.rows.dtype, device=dev)  # the median is one of the inputs
 
         def step(ev=None):
             if ev is not None:
                 ev[0].record()
-            dfn.median_f32(gd.d_ptrs, K, gd.length, med_out)
+            dfn.median_rows(gd.d_ptrs, K, gd.length, med_out)
             if ev is not None:
                 ev[1].record()
 
         n_launch = 1
-        dom_bytes = K * gd.length * 4 + gd.length * 4
+        dom_bytes = (K + 1) * gd.length * gd.rows.element_size()
     elif mode == "single":
         outs = bucket.new_outputs()
         w = bucket.weights(ns_local)
@@ -304,7 +304,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": ("median_kernel<128>" if a.op == "median" else
+            "kernel": (f"median_kernel<128, {dom_dt}>" if a.op == "median" else
                        ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adagrad": "reduce_kernel<OpF32,AdagradEpi>"}
                         .get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>"))
                        + " (FedAvg+server step fused)"

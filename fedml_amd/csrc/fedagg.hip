@@ -923,9 +923,40 @@ __device__ __forceinline__ void pairwise_sort(float (&v)[N]) {
   net_apply<N>(v, std::make_integer_sequence<int, PairwiseNet<N>::M>{});
 }
 
-template <int KMAX, bool FULL, int BS, bool PRIO = false>
-__global__ __launch_bounds__(BS) void median_kernel(const float* const* __restrict__ src, int K, int64_t N,
-                                                    float* __restrict__ out) {
+// Element types of the median kernels.  bf16 / f16 columns are widened to
+// fp32 exactly, selected there, and the selected value narrowed back exactly
+// (it is one of the inputs), so the network is the same for all three.
+struct MedF32 {
+  using S = float;
+  static __device__ __forceinline__ float widen(S x) { return x; }
+  static __device__ __forceinline__ S narrow(float v) { return v; }
+  static constexpr uint32_t kNegInf = 0xff800000u, kPosInf = 0x7f800000u;
+};
+struct MedBF16 {
+  using S = uint16_t;
+  static __device__ __forceinline__ float widen(S x) { return __uint_as_float(uint32_t(x) << 16); }
+  static __device__ __forceinline__ S narrow(float v) { return S(__float_as_uint(v) >> 16); }
+  static constexpr uint32_t kNegInf = 0xff80u, kPosInf = 0x7f80u;
+};
+struct MedF16 {
+  using S = uint16_t;
+  static __device__ __forceinline__ float widen(S x) {
+    _Float16 h;
+    __builtin_memcpy(&h, &x, 2);
+    return float(h);
+  }
+  static __device__ __forceinline__ S narrow(float v) {
+    const _Float16 h = _Float16(v);
+    S x;
+    __builtin_memcpy(&x, &h, 2);
+    return x;
+  }
+  static constexpr uint32_t kNegInf = 0xfc00u, kPosInf = 0x7c00u;
+};
+
+template <int KMAX, bool FULL, int BS, bool PRIO = false, class E = MedF32>
+__global__ __launch_bounds__(BS) void median_kernel(const typename E::S* const* __restrict__ src, int K, int64_t N,
+                                                    typename E::S* __restrict__ out) {
   const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;
   if (e >= N) return;
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // issue this wave's loads ahead of others' sorting
@@ -933,7 +964,7 @@ __global__ __launch_bounds__(BS) void median_kernel(const float* const* __restri
   // The host guarantees N * 4 < 2^32: a 32-bit byte offset on each
   // wave-uniform row base lets every load use the SGPR-base + VGPR-offset
   // form, with no per-client 64-bit address arithmetic on the VALU.
-  const uint32_t boff = uint32_t(e) * 4u;
+  const uint32_t boff = uint32_t(e) * uint32_t(sizeof(typename E::S));
   const int below = (KMAX - 1) / 2 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
   float v[KMAX];
   bool has_nan = false;
@@ -947,8 +978,8 @@ __global__ __launch_bounds__(BS) void median_kernel(const float* const* __restri
     // pointer loads batch and nothing spills.
     const int ci = (FULL || c < K) ? c : K - 1;
     const auto row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
-    const float x =
-        __builtin_nontemporal_load(reinterpret_cast<const float __attribute__((address_space(1)))*>(row + boff));
+    const float x = E::widen(__builtin_nontemporal_load(
+        reinterpret_cast<const typename E::S __attribute__((address_space(1)))*>(row + boff)));
     // torch returns the first NaN of the column (client order) if there is
     // one.  The common case pays one compare per client (on x itself, which
     // also keeps CodeGenPrepare from turning the select below into a branch
@@ -973,19 +1004,20 @@ __global__ __launch_bounds__(BS) void median_kernel(const float* const* __restri
     }
   }
   pairwise_sort<KMAX>(v);
-  out[e] = has_nan ? nan_v : v[(KMAX - 1) / 2];
+  out[e] = E::narrow(has_nan ? nan_v : v[(KMAX - 1) / 2]);
 }
 
-template <int KMAX>
-int launch_median(const float* const* src, int K, int64_t N, float* out, hipStream_t st) {
+template <int KMAX, class E = MedF32>
+int launch_median(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
   constexpr int BS = 256;
   const int64_t grid = (N + BS - 1) / BS;
-  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N too large");
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
   if (K == KMAX)
-    hipLaunchKernelGGL((median_kernel<KMAX, true, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
+    hipLaunchKernelGGL((median_kernel<KMAX, true, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
   else
-    hipLaunchKernelGGL((median_kernel<KMAX, false, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
-  return check_launch("fedagg_median_f32");
+    hipLaunchKernelGGL((median_kernel<KMAX, false, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
+                       out);
+  return check_launch("fedagg_median");
 }
 
 // More than 128 clients, in registers: P adjacent lanes share one column,
@@ -1069,11 +1101,17 @@ __device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
   }
 }
 
-__device__ float g_median_pad[2] = {-__builtin_huge_valf(), __builtin_huge_valf()};
+// -inf / +inf in each element type: what a padded slot's load returns
+template <class E>
+__device__ typename E::S g_median_pad[2] = {__builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
+                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kNegInf)),
+                                            __builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
+                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kPosInf))};
 
-template <int P, int R, bool FULL>
+template <int P, int R, bool FULL, class E = MedF32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
-    const float* const* __restrict__ src, int K, int64_t N, float* __restrict__ out) {
+    const typename E::S* const* __restrict__ src, int K, int64_t N, typename E::S* __restrict__ out) {
+  using S = typename E::S;
   static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2, 4, 8 or 16 lanes per column");
   static_assert(R == 64 || R == 128, "64 or 128 values per lane");
   constexpr int KMAX = P * R, PAD = 2;
@@ -1081,7 +1119,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
   // lanes of a column read different LDS banks.  A padded slot (K < KMAX)
   // points at a ±inf constant and its column offset is masked to 0, so the
   // load itself yields the pad: no per-slot, per-lane select.
-  __shared__ const float* rows[KMAX + PAD * P];
+  __shared__ const S* rows[KMAX + PAD * P];
   __shared__ uint64_t offmask[FULL ? 1 : KMAX + PAD * P];
   const int t = threadIdx.x, sub = t & (P - 1);
   if constexpr (FULL) K = KMAX;
@@ -1092,7 +1130,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
       rows[q] = src[i];
       if constexpr (!FULL) offmask[q] = ~uint64_t(0);
     } else {
-      rows[q] = &g_median_pad[i - K < below ? 0 : 1];
+      rows[q] = &g_median_pad<E>[i - K < below ? 0 : 1];
       offmask[q] = 0;
     }
   }
@@ -1100,7 +1138,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
   // every lane stays active through the DPP exchanges; a column past the end
   // recomputes the last one and does not store
   const int64_t e = (int64_t(blockIdx.x) * 256 + t) / P;
-  const uint64_t boff = uint64_t(e < N ? e : N - 1) * 4u;
+  const uint64_t boff = uint64_t(e < N ? e : N - 1) * sizeof(S);
   float v[R];
   bool has_nan = false;
 #pragma unroll
@@ -1109,7 +1147,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
     const int q = sub * (R + PAD) + j;
     const uint64_t off = FULL ? boff : (boff & offmask[q]);
     const auto row = reinterpret_cast<const char*>(rows[q]);
-    v[j] = __builtin_nontemporal_load(as_global(reinterpret_cast<const float*>(row + off)));
+    v[j] = E::widen(__builtin_nontemporal_load(as_global(reinterpret_cast<const S*>(row + off))));
     has_nan |= __builtin_isnan(v[j]);
   }
   // first NaN of the column in client (= slot) order, only in waves holding
@@ -1144,18 +1182,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
   if constexpr (P >= 4) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
   if constexpr (P >= 8) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
   if constexpr (P >= 16) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima across the two quads
-  if (sub == 0 && e < N) out[e] = nan_slot < KMAX ? nan_v : m;
+  if (sub == 0 && e < N) out[e] = E::narrow(nan_slot < KMAX ? nan_v : m);
 }
 
-template <int P, int R>
-int launch_median_lanes(const float* const* src, int K, int64_t N, float* out, hipStream_t st) {
+template <int P, int R, class E = MedF32>
+int launch_median_lanes(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
   const int64_t grid = (N * P + 255) / 256;
-  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N too large");
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
   if (K == P * R)
-    hipLaunchKernelGGL((median_lanes_kernel<P, R, true>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+    hipLaunchKernelGGL((median_lanes_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
   else
-    hipLaunchKernelGGL((median_lanes_kernel<P, R, false>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
-  return check_launch("fedagg_median_f32");
+    hipLaunchKernelGGL((median_lanes_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+  return check_launch("fedagg_median");
 }
 
 // ---------------------------------------------------------------------------
@@ -1278,6 +1316,31 @@ int launch_multi(const void* const* d_src, void* const* d_out, const int64_t* d_
                      reinterpret_cast<typename OP::out_t* const*>(d_out), d_numel, d_block_begin, T, d_w, K);
   return check_launch("fedagg_wsum_multi");
 }
+}  // namespace
+
+namespace {
+
+template <class E>
+int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typename E::S* d_out,
+                    hipStream_t st) {
+  if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
+    if (K <= 256) return launch_median_lanes<4, 64, E>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
+    if (K <= 512) return launch_median_lanes<4, 128, E>(d_src, K, N, d_out, st);
+    if (K <= 1024) return launch_median_lanes<8, 128, E>(d_src, K, N, d_out, st);
+    return set_error(FEDAGG_EINVAL, "fedagg_median: K > 1024 clients is not supported");
+  }
+  // the register kernels address rows with 32-bit byte offsets
+  if (N > (int64_t(1) << 30)) return set_error(FEDAGG_EINVAL, "fedagg_median: N > 2^30 elements per row");
+  if (K <= 8) return launch_median<8, E>(d_src, K, N, d_out, st);
+  if (K <= 16) return launch_median<16, E>(d_src, K, N, d_out, st);
+  if (K <= 24) return launch_median<24, E>(d_src, K, N, d_out, st);
+  if (K <= 32) return launch_median<32, E>(d_src, K, N, d_out, st);
+  if (K <= 48) return launch_median<48, E>(d_src, K, N, d_out, st);
+  if (K <= 64) return launch_median<64, E>(d_src, K, N, d_out, st);
+  if (K <= 96) return launch_median<96, E>(d_src, K, N, d_out, st);
+  return launch_median<128, E>(d_src, K, N, d_out, st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1528,29 +1591,31 @@ int fedagg_lsa_reconstruct_f32(const int64_t* const* d_src, int32_t K, int64_t N
                                   reinterpret_cast<hipStream_t>(stream), "fedagg_lsa_reconstruct_f32");
 }
 
-int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_out, uint32_t flags,
-                      fedagg_stream_t stream) {
+int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K, int64_t N, void* d_out, uint32_t flags,
+                  fedagg_stream_t stream) {
   (void)flags;
-  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K must be >= 1 and N >= 0");
-  if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: null pointer");
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_median: K must be >= 1 and N >= 0");
+  if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_median: null pointer");
   if (N == 0) return FEDAGG_OK;
   auto st = reinterpret_cast<hipStream_t>(stream);
-  if (K > 128) {  // 2, 4 or 8 lanes per column, register sort + cross-lane merges
-    if (K <= 256) return launch_median_lanes<4, 64>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
-    if (K <= 512) return launch_median_lanes<4, 128>(d_src, K, N, d_out, st);
-    if (K <= 1024) return launch_median_lanes<8, 128>(d_src, K, N, d_out, st);
-    return set_error(FEDAGG_EINVAL, "fedagg_median_f32: K > 1024 clients is not supported");
+  switch (dtype) {
+    case FEDAGG_DT_F32:
+      return median_dispatch<MedF32>(reinterpret_cast<const float* const*>(d_src), K, N,
+                                     static_cast<float*>(d_out), st);
+    case FEDAGG_DT_BF16:
+      return median_dispatch<MedBF16>(reinterpret_cast<const uint16_t* const*>(d_src), K, N,
+                                      static_cast<uint16_t*>(d_out), st);
+    case FEDAGG_DT_F16:
+      return median_dispatch<MedF16>(reinterpret_cast<const uint16_t* const*>(d_src), K, N,
+                                     static_cast<uint16_t*>(d_out), st);
+    default:
+      return set_error(FEDAGG_EINVAL, "fedagg_median: dtype must be FEDAGG_DT_F32, _BF16 or _F16");
   }
-  // the register kernels address rows with 32-bit byte offsets
-  if (N > (int64_t(1) << 30)) return set_error(FEDAGG_EINVAL, "fedagg_median_f32: N > 2^30 elements per row");
-  if (K <= 8) return launch_median<8>(d_src, K, N, d_out, st);
-  if (K <= 16) return launch_median<16>(d_src, K, N, d_out, st);
-  if (K <= 24) return launch_median<24>(d_src, K, N, d_out, st);
-  if (K <= 32) return launch_median<32>(d_src, K, N, d_out, st);
-  if (K <= 48) return launch_median<48>(d_src, K, N, d_out, st);
-  if (K <= 64) return launch_median<64>(d_src, K, N, d_out, st);
-  if (K <= 96) return launch_median<96>(d_src, K, N, d_out, st);
-  return launch_median<128>(d_src, K, N, d_out, st);
+}
+
+int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_out, uint32_t flags,
+                      fedagg_stream_t stream) {
+  return fedagg_median(FEDAGG_DT_F32, reinterpret_cast<const void* const*>(d_src), K, N, d_out, flags, stream);
 }
 
 int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs, const int64_t* nbytes, int32_t n,

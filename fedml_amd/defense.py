@@ -12,8 +12,9 @@ that are pure reductions over the client axis.
                 The walk is reproduced as is: for models with BN buffers the
                 slices no longer line up with the weight keys and the last
                 .view() raises RuntimeError — exactly what FedML does.
-                The median itself is fedagg_median_f32 (one launch over the
-                whole weight row).
+                The median itself is fedagg_median (one launch over the
+                whole weight row; fp32 rows, or bf16 / f16 rows for 16-bit
+                models, whose torch.cat stays 16-bit).
 
 "trimmed_mean"  CoordinateWiseTrimmedMeanDefense.defend_before_aggregation
                 (coordinate_wise_trimmed_mean_defense.py:19-26 ->
@@ -49,6 +50,19 @@ def median_f32(d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor) -> None:
               "median_f32")
 
 
+_MEDIAN_DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16, torch.float16: nat.DT_F16}
+
+
+def median_rows(d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor) -> None:
+    """Coordinate-wise lower median of K device rows of out's dtype (fp32, bf16
+    or f16; fedagg_median)."""
+    kn._require_cuda(out, "median")
+    if out.dtype not in _MEDIAN_DT:
+        raise TypeError(f"median: fp32, bf16 or f16 rows (got {out.dtype})")
+    nat.check(nat.lib().fedagg_median(_MEDIAN_DT[out.dtype], d_ptrs.data_ptr(), K, N, out.data_ptr(), 0,
+                                      nat.stream_handle()), "median")
+
+
 def coordinate_wise_median(raw_client_grad_list: List[Tuple[float, "OrderedDict"]], device=None
                            ) -> "OrderedDict":
     """CoordinateWiseMedianDefense.defend_on_aggregation on the GPU."""
@@ -64,17 +78,24 @@ def coordinate_wise_median(raw_client_grad_list: List[Tuple[float, "OrderedDict"
     dev = t0.device if t0.is_cuda else (torch.device(device) if device is not None else
                                         torch.device("cuda", torch.cuda.current_device()))
     dts = {dicts[0][k].dtype for k in wkeys}
-    if not dts <= {torch.float32, torch.int64, torch.int32, torch.bool}:
-        raise NotImplementedError(f"wise_median on the GPU supports fp32 weights (got {sorted(map(str, dts))})")
+    # vectorize_weight's torch.cat promotes to one dtype: fp32 (with integer
+    # weights riding as fl32(v)), or a 16-bit model's own bf16 / f16
+    if dts <= {torch.float32, torch.int64, torch.int32, torch.bool} and torch.float32 in dts:
+        row_dt = torch.float32
+    elif dts in ({torch.bfloat16}, {torch.float16}):
+        row_dt = next(iter(dts))
+    else:
+        raise NotImplementedError("wise_median on the GPU takes fp32 weights (integer keys allowed), or all-bf16 "
+                                  f"/ all-f16 weights (got {sorted(map(str, dts))})")
     with torch.cuda.device(dev):
         layout = [(k, tuple(dicts[0][k].shape), dicts[0][k].dtype) for k in wkeys]
-        bucket = ClientBucket(layout, K, dev)  # integer weights ride as fl32(v), as torch.cat would promote
+        bucket = ClientBucket(layout, K, dev)
         for i in range(K):
             bucket.put(i, {k: dicts[i][k] for k in wkeys}, 1)
         bucket.sync_ingest()
-        g = bucket.groups[torch.float32]
-        row_med = torch.empty(g.padded, dtype=torch.float32, device=dev)
-        median_f32(g.d_ptrs, K, g.length, row_med)
+        g = bucket.groups[row_dt]
+        row_med = torch.empty(g.padded, dtype=row_dt, device=dev)
+        median_rows(g.d_ptrs, K, g.length, row_med)
         # the reference's vector: weight keys back to back, no alignment gaps
         vec = torch.cat([row_med[o:o + n] for o, n in zip(g.offsets, g.numels)]) if g.keys else row_med[:0]
         if not t0.is_cuda:

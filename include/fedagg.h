@@ -214,6 +214,15 @@ int fedagg_wsum_fedopt_adagrad_f32(const float* const* d_src, const float* d_w,
 int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N,
                       float* d_out, uint32_t flags, fedagg_stream_t stream);
 
+/* The same median for dtype FEDAGG_DT_F32, _BF16 or _F16 rows (d_src and
+ * d_out of that dtype): a bf16 / f16 model's stack, torch.median over it
+ * (torch.cat keeps the 16-bit dtype).  Values are widened to fp32 exactly,
+ * selected, and the selected input narrowed back exactly; a NaN column
+ * returns a NaN. */
+int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K,
+                  int64_t N, void* d_out, uint32_t flags,
+                  fedagg_stream_t stream);
+
 /* Secure aggregation in a finite field (LightSecAgg), numpy int64 semantics:
  * wrapping adds, floor modulo.  p > 0.
  *

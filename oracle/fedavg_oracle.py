@@ -432,17 +432,28 @@ def lower_median_cols(stack: np.ndarray) -> np.ndarray:
     return med
 
 
+def _exact_f32(t: torch.Tensor) -> np.ndarray:
+    """Values as float32, exactly (bf16 bits widened, f16 / ints converted)."""
+    a = to_np(t).ravel()
+    if t.dtype == torch.bfloat16:
+        return (a.astype(np.uint32) << 16).view(np.float32)
+    return a.astype(np.float32)
+
+
 def coordinate_wise_median(raw_grad_list):
     """CoordinateWiseMedianDefense.defend_on_aggregation
     (coordinate_wise_median_defense.py:18-44), including its walk over ALL of
     client 0's keys (misaligned for models with BN buffers -> RuntimeError)."""
     vecs = []
     for n, params in raw_grad_list:
-        parts = [to_np(v).ravel() for k, v in params.items() if _is_weight_param(k)]
+        parts = [_exact_f32(v) for k, v in params.items() if _is_weight_param(k)]
         if not parts:
             raise RuntimeError("torch.cat(): expected a non-empty list of Tensors")
-        vecs.append(np.concatenate([p.astype(np.float32) for p in parts]))
-    med = torch.from_numpy(lower_median_cols(np.stack(vecs)))
+        vecs.append(np.concatenate(parts))
+    # torch.cat's promoted dtype (bf16 / f16 models stay 16-bit); the median
+    # is one of the inputs, so selecting in fp32 and casting back is exact
+    cat_dtype = torch.cat([v.reshape(-1)[:0] for k, v in raw_grad_list[0][1].items() if _is_weight_param(k)]).dtype
+    med = torch.from_numpy(lower_median_cols(np.stack(vecs))).to(cat_dtype)
     index = 0
     (num0, averaged_params) = raw_grad_list[0]
     for k, params in list(averaged_params.items()):

@@ -230,6 +230,12 @@ for _k in (17, 64, 100, 128):
 _def("median_specials_k5", "wise_median", 5, [["x", [64], F32]], seed=130, specials=True)
 _def("median_specials_k8", "wise_median", 8, [["x", [64], F32]], seed=131, specials=True)
 _def("median_resnet_mini_k3", "wise_median", 3, RESNET_MINI, seed=132, expect_error=True)  # misaligned walk
+# 16-bit models (config 4 is bf16): torch.median over bf16 / f16 stacks
+for _k in (3, 17, 128, 200):
+    _def(f"median_bf16_ragged_k{_k}", "wise_median", _k, RAGGED_BF16, seed=150 + _k)
+for _k in (5, 130):
+    _def(f"median_f16_ragged_k{_k}", "wise_median", _k, [[n, s, F16] for n, s, _ in RAGGED_BF16], seed=160 + _k)
+_def("median_bf16_specials_k9", "wise_median", 9, [["x", [64], BF16]], seed=170, specials=True)
 _def("trimmed_k10_b01", "trimmed_mean", 10, RESNET_MINI, seed=140, beta=0.1,
      sample_nums=[50, 10, 10, 70, 30, 90, 20, 60, 40, 80])
 _def("trimmed_k10_b02_ties", "trimmed_mean", 10, RAGGED_F32[:4], seed=141, beta=0.2,

@@ -79,7 +79,7 @@ def test_median_headline_shape_sampled(cuda_device):
 
 @pytest.mark.parametrize("K", [129, 200, 255, 256, 257, 512, 700, 1024])
 def test_median_lanes_kernel_vs_oracle(K, cuda_device):
-    """More than 128 clients (2, 4 or 8 lanes per column, register sort plus
+    """More than 128 clients (4 or 8 lanes per column, register sorts plus
     cross-lane merges): full and padded kernels of every lane count, a ragged
     last workgroup, with duplicates, infinities, NaN columns and -0.0."""
     N = 3_001
@@ -120,3 +120,24 @@ def test_median_rejects_too_many_clients(cuda_device):
     d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(1025)], cuda_device)
     with pytest.raises(nat.FedAggNativeError):
         dfn.median_f32(d_ptrs, 1025, 64, torch.empty(64, device=cuda_device))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K", [1, 9, 64, 127, 128, 129, 256, 257, 700, 1024])
+def test_median_16bit_rows_vs_oracle(dtype, K, cuda_device):
+    """bf16 / f16 rows (a 16-bit model's stack): every kernel family, with
+    duplicates, infinities, NaN columns and -0.0; the result is the selected
+    input, bit for bit."""
+    N = 2_051
+    g = torch.Generator(device=cuda_device).manual_seed(K + 7)
+    rows = (torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125).to(dtype)
+    rows[:, 17:29] = torch.randn(K, 12, generator=g, device=cuda_device).to(dtype)
+    rows[:, :7] = float("inf")
+    rows[:, 7:9] = -float("inf")
+    rows[K // 2, 100:110] = float("nan")
+    rows[:, 200:203] = -0.0
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, dtype=dtype, device=cuda_device)
+    dfn.median_rows(d_ptrs, K, N, out)
+    exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
+    gu.assert_same(out.cpu(), exp, f"median {dtype} K={K}")
