@@ -26,6 +26,7 @@ from __future__ import annotations
 from collections import OrderedDict
 from typing import Dict, List, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from . import _native as nat
@@ -228,25 +229,29 @@ _ROW_ESZ = {nat.DT_F32: 4, nat.DT_BF16: 2, nat.DT_F16: 2, nat.DT_F64: 8, nat.DT_
 
 
 def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
-    """Small host rounds (every key a contiguous CPU tensor of a row dtype,
-    the whole round <= 256 MB): the walker's host pointer tables drive ONE
-    native pack of all clients per dtype into pinned staging, ONE H2D, one
-    launch per dtype and one D2H, instead of a Python pass per client.  None
-    when the walk declines or the round is large (the per-client staging ring
-    then overlaps packing with the DMA)."""
+    """Host rounds whose every key is a contiguous CPU tensor of a row dtype:
+    the walker's host pointer tables drive the staging, with no per-key
+    Python work.  Up to 256 MB per round: ONE native pack of all clients per
+    dtype into pinned staging and ONE H2D; larger rounds one pack + one H2D
+    per client through the staging ring, so packing client i+1 overlaps
+    client i's DMA.  Then one launch per dtype and one D2H.  None when the
+    walk declines (the general path then raises the reference's errors)."""
     walked = w.walk_host(dicts, keys)
     if walked is None:
         return None
     codes, numels, tables = walked
     K = len(dicts)
-    if K * sum(n * _ROW_ESZ[c] for n, c in zip(numels, codes)) > _BATCH_MAX_BYTES:
-        return None
     d0 = dicts[0]
     device = _host_device(args)
     with torch.cuda.device(device):
         bucket = _cached_bucket([(k, tuple(d0[k].shape), d0[k].dtype) for k in keys], K, device,
                                 _ACC_NAME[acc_mode])
-        bucket.put_batch(tables, dicts, [1] * K)
+        if K * sum(n * _ROW_ESZ[c] for n, c in zip(numels, codes)) <= _BATCH_MAX_BYTES:
+            bucket.put_batch(tables, dicts, [1] * K)
+        else:  # large round: per client, packing the next while the last one's DMA runs
+            t2d = {c: np.frombuffer(t, dtype=np.int64).reshape(-1, K) for c, t in tables.items()}
+            for i in range(K):
+                bucket.put_from_table(i, t2d, dicts[i], 1)
         outs = bucket.new_outputs()
         bucket.reduce_into(outs, weights)
         return bucket.to_host(outs)

@@ -213,6 +213,72 @@ class ClientBucket:
         for i, n in enumerate(sample_nums):
             self.sample_nums[i] = n
 
+    def put_from_table(self, slot: int, tables: Dict[int, "np.ndarray"], state_dict, sample_num: float) -> None:
+        """put() for one client of a walked host round: the walker's pointer
+        tables (``{code: int64 [T_code, capacity]}``) give every key's host
+        pointer, so each dtype group is ONE native pack into a pinned staging
+        row of the ring plus ONE async H2D, with no per-key Python work apart
+        from integer keys promoted into the fp32 rows (converted from
+        state_dict)."""
+        code_dt = {nat.DT_F32: torch.float32, nat.DT_BF16: torch.bfloat16, nat.DT_F16: torch.float16,
+                   nat.DT_F64: torch.float64, nat.DT_I64: torch.int64}
+        if self._copy is None:
+            self._copy = torch.cuda.Stream(self.device)
+            self._copy.wait_stream(torch.cuda.current_stream(self.device))
+        plans = self._table_plans()
+        by_dt = {code_dt[c]: t for c, t in tables.items()}
+        for dt, g in self.groups.items():
+            if g.length == 0:
+                continue
+            native, offs, nb, ints = plans[dt]
+            st = self._staging.get(dt)
+            if st is None:
+                st = self._staging[dt] = {"bufs": [[torch.empty(g.length, dtype=dt).pin_memory(), None]
+                                                   for _ in range(_STAGES)], "next": 0}
+            b = st["bufs"][st["next"]]
+            st["next"] = (st["next"] + 1) % _STAGES
+            if b[1] is not None:
+                b[1].synchronize()
+            stage = b[0]
+            if native.size:
+                srcs = np.ascontiguousarray(by_dt[dt][native, slot])
+                nat.check(nat.lib().fedagg_host_pack(stage.data_ptr(), srcs.ctypes.data, offs.ctypes.data,
+                                                     nb.ctypes.data, int(srcs.size), _PACK_THREADS), "host_pack")
+            for key, lo, n in ints:
+                stage[lo:lo + n].copy_(state_dict[key].reshape(-1))
+            with torch.cuda.stream(self._copy):
+                g.rows[slot, :g.length].copy_(stage[:g.length], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._copy)
+            b[1] = ev
+            self._pending = True
+        self.sample_nums[slot] = sample_num
+
+    def _table_plans(self):
+        """Per dtype group: the rows of the walker's table that feed it (keys of
+        that dtype with data), their byte offsets and sizes in the row, and the
+        promoted integer keys (key, element offset, count)."""
+        if getattr(self, "_tplans", None) is None:
+            plans = {}
+            for dt, g in self.groups.items():
+                esz = torch.empty((), dtype=dt).element_size()
+                native, offs, nb, ints = [], [], [], []
+                r = 0
+                for key, off, n in zip(g.keys, g.offsets, g.numels):
+                    if key in self.int_keys:
+                        if n:
+                            ints.append((key, off, n))
+                        continue
+                    if n:
+                        native.append(r)
+                        offs.append(off * esz)
+                        nb.append(n * esz)
+                    r += 1
+                plans[dt] = (np.asarray(native, dtype=np.int64), np.asarray(offs, dtype=np.int64),
+                             np.asarray(nb, dtype=np.int64), ints)
+            self._tplans = plans
+        return self._tplans
+
     def _stage(self, dt: torch.dtype, slot: int, parts) -> None:
         g = self.groups[dt]
         if self._copy is None:

@@ -415,3 +415,28 @@ def test_small_host_rounds_take_the_batched_pack(cuda_device, monkeypatch):
             assert not res[k].is_cuda and res[k].dtype == exp[k].dtype, k
             gu.assert_same(res[k], exp[k], f"round {r} {k}")
     assert calls == [6, 6, 6]
+
+
+def test_large_host_rounds_stage_per_client_from_tables(cuda_device, monkeypatch):
+    """Above the one-image limit, host rounds stage client by client from the
+    walker's pointer tables (bucket.put_from_table), int64 counters included;
+    bit-exact, and the cached bucket's ring is reused across rounds."""
+    calls = []
+    orig = ClientBucket.put_from_table
+
+    def spy(self, slot, *a, **kw):
+        calls.append(slot)
+        return orig(self, slot, *a, **kw)
+
+    monkeypatch.setattr(ClientBucket, "put_from_table", spy)
+    monkeypatch.setattr(ao, "_BATCH_MAX_BYTES", 0)
+    args = type("A", (), {"federated_optimizer": "FedAvg"})()
+    entries = shapes.resnet50()[:40] + [("extra.f16", (9,), torch.float16)]
+    for r in range(2):
+        raw = host_clients(entries, 5, seed=60 + r, round_idx=r)
+        exp = orc.agg(args, copy.deepcopy(raw))
+        res = ao.FedMLAggOperator.agg(args, raw)
+        for k in exp:
+            assert not res[k].is_cuda and res[k].dtype == exp[k].dtype, k
+            gu.assert_same(res[k], exp[k], f"round {r} {k}")
+    assert calls == list(range(5)) * 2
