@@ -192,7 +192,7 @@ def main():
         def step(ev=None):
             if ev is not None:
                 ev[0].record()
-            dfn.median_rows(gd.d_ptrs, K, gd.length, med_out)
+            dfn.median_rows(gd.d_ptrs, K, gd.length, med_out, aligned=True)
             if ev is not None:
                 ev[1].record()
 

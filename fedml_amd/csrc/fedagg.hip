@@ -909,18 +909,27 @@ struct PairwiseNet {
   static constexpr Table table = make();
 };
 
-template <int N, int I>
-__device__ __forceinline__ void net_cmp(float (&v)[N]) {
+// two 16-bit order keys per register: one v_pk_min_i16 + one v_pk_max_i16
+typedef short short2_t __attribute__((ext_vector_type(2)));
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void cmpx(short2_t& a, short2_t& b) {
+  const short2_t lo = __builtin_elementwise_min(a, b), hi = __builtin_elementwise_max(a, b);
+  a = lo;
+  b = hi;
+}
+
+template <int N, int I, class T>
+__device__ __forceinline__ void net_cmp(T (&v)[N]) {
   constexpr int A = PairwiseNet<N>::table.p[I].a, B = PairwiseNet<N>::table.p[I].b;
   cmpx(v[A], v[B]);
 }
-template <int N, int... I>
-__device__ __forceinline__ void net_apply(float (&v)[N], std::integer_sequence<int, I...>) {
+template <int N, class T, int... I>
+__device__ __forceinline__ void net_apply(T (&v)[N], std::integer_sequence<int, I...>) {
   (net_cmp<N, I>(v), ...);
 }
-template <int N>
-__device__ __forceinline__ void pairwise_sort(float (&v)[N]) {
-  net_apply<N>(v, std::make_integer_sequence<int, PairwiseNet<N>::M>{});
+template <int N, class T>
+__device__ __forceinline__ void pairwise_sort(T (&v)[N]) {
+  net_apply<N, T>(v, std::make_integer_sequence<int, PairwiseNet<N>::M>{});
 }
 
 // Element types of the median kernels.  bf16 / f16 columns are widened to
@@ -1016,6 +1025,106 @@ int launch_median(const typename E::S* const* src, int K, int64_t N, typename E:
     hipLaunchKernelGGL((median_kernel<KMAX, true, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
   else
     hipLaunchKernelGGL((median_kernel<KMAX, false, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
+                       out);
+  return check_launch("fedagg_median");
+}
+
+// 16-bit rows, K <= 128, two columns per lane: a 32-bit load brings columns
+// 2e and 2e+1 of a client as one register, each half is turned into an
+// order-preserving int16 key (x ^ 0x7fff for negative values, so signed
+// compares follow the float order, -0 just below +0), and the same pruned
+// network runs on v_pk_min_i16 / v_pk_max_i16: half the VALU per column of the
+// widening kernel, which is VALU-bound on 16-bit rows.  Keys map back to the
+// input bits by the same transform.  Pads are the int16 extremes, below / above
+// every non-NaN key; a NaN column returns its first NaN, as everywhere.  Needs
+// 4-byte aligned rows and output (the FEDAGG_ALIGNED16 flag); an odd last
+// column is loaded and stored as 16 bits by its lane.
+__device__ __forceinline__ short2_t pk16_key(uint32_t x) {
+  const short2_t v = __builtin_bit_cast(short2_t, x);
+  return v ^ ((v >> short(15)) & short(0x7fff));
+}
+__device__ __forceinline__ uint32_t pk16_bits(short2_t k) {
+  return __builtin_bit_cast(uint32_t, k ^ ((k >> short(15)) & short(0x7fff)));
+}
+
+template <int KMAX, bool FULL, class E, bool TAIL>
+__device__ __forceinline__ void median_pk16_pair(const uint16_t* const* __restrict__ src, int K, int64_t e,
+                                                 uint16_t* __restrict__ out) {
+  if constexpr (FULL) K = KMAX;
+  const uint32_t boff = uint32_t(e) * 4u;
+  const int below = (KMAX - 1) / 2 - (K - 1) / 2;
+  uint32_t raw[KMAX];
+  uint32_t nanacc = 0;  // per half, max of |x| bits
+#pragma unroll
+  for (int c = 0; c < KMAX; ++c) {
+    if (c % 16 == 0 && c) __builtin_amdgcn_sched_barrier(0);
+    const int ci = (FULL || c < K) ? c : K - 1;
+    const auto row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
+    uint32_t x;
+    if constexpr (!TAIL)
+      x = __builtin_nontemporal_load(reinterpret_cast<const uint32_t __attribute__((address_space(1)))*>(row + boff));
+    else  // the odd last column alone, duplicated into both halves
+      x = *reinterpret_cast<const uint16_t __attribute__((address_space(1)))*>(row + boff) * 0x10001u;
+    raw[c] = x;
+    const uint32_t mag = x & 0x7fff7fffu;
+    nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
+                                                                     __builtin_bit_cast(ushort2_t, mag)));
+  }
+  const bool nan_lo = (nanacc & 0xffffu) > E::kPosInf, nan_hi = (nanacc >> 16) > E::kPosInf;
+  uint32_t nan_bits = 0;
+  if (nan_lo || nan_hi) {  // first NaN per half, in client order (only columns holding one)
+    bool f_lo = false, f_hi = false;
+#pragma unroll
+    for (int c = 0; c < KMAX; ++c) {
+      if (!FULL && c >= K) break;
+      const uint32_t x = raw[c];
+      const bool n_lo = !f_lo && (x & 0x7fffu) > E::kPosInf, n_hi = !f_hi && ((x >> 16) & 0x7fffu) > E::kPosInf;
+      if (n_lo) nan_bits = (nan_bits & 0xffff0000u) | (x & 0xffffu);
+      if (n_hi) nan_bits = (nan_bits & 0xffffu) | (x & 0xffff0000u);
+      f_lo = f_lo || n_lo;
+      f_hi = f_hi || n_hi;
+    }
+  }
+  short2_t v[KMAX];
+#pragma unroll
+  for (int c = 0; c < KMAX; ++c) {
+    if constexpr (FULL)
+      v[c] = pk16_key(raw[c]);
+    else
+      v[c] = (c < K) ? pk16_key(raw[c]) : ((c - K < below) ? short2_t(short(-32768)) : short2_t(short(32767)));
+  }
+  pairwise_sort<KMAX>(v);
+  uint32_t m = pk16_bits(v[(KMAX - 1) / 2]);
+  if (nan_lo) m = (m & 0xffff0000u) | (nan_bits & 0xffffu);
+  if (nan_hi) m = (m & 0xffffu) | (nan_bits & 0xffff0000u);
+  if constexpr (!TAIL)
+    *reinterpret_cast<uint32_t*>(out + 2 * e) = m;
+  else
+    out[2 * e] = uint16_t(m);
+}
+
+template <int KMAX, bool FULL, class E, int BS = 256>
+__global__ __launch_bounds__(BS) void median_pk16_kernel(const uint16_t* const* __restrict__ src, int K, int64_t N,
+                                                         uint16_t* __restrict__ out) {
+  static_assert(sizeof(typename E::S) == 2, "16-bit rows");
+  const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;  // column pair
+  const int64_t pairs = (N + 1) / 2;
+  if (e >= pairs) return;
+  if ((N & 1) && e == pairs - 1)
+    median_pk16_pair<KMAX, FULL, E, true>(src, K, e, out);
+  else
+    median_pk16_pair<KMAX, FULL, E, false>(src, K, e, out);
+}
+
+template <int KMAX, class E>
+int launch_median_pk16(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  constexpr int BS = 256;
+  const int64_t grid = ((N + 1) / 2 + BS - 1) / BS;
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
+  if (K == KMAX)
+    hipLaunchKernelGGL((median_pk16_kernel<KMAX, true, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
+  else
+    hipLaunchKernelGGL((median_pk16_kernel<KMAX, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
                        out);
   return check_launch("fedagg_median");
 }
@@ -1321,7 +1430,7 @@ int launch_multi(const void* const* d_src, void* const* d_out, const int64_t* d_
 namespace {
 
 template <class E>
-int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typename E::S* d_out,
+int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typename E::S* d_out, bool aligned,
                     hipStream_t st) {
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
     if (K <= 256) return launch_median_lanes<4, 64, E>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
@@ -1331,6 +1440,14 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
   }
   // the register kernels address rows with 32-bit byte offsets
   if (N > (int64_t(1) << 30)) return set_error(FEDAGG_EINVAL, "fedagg_median: N > 2^30 elements per row");
+  if constexpr (sizeof(typename E::S) == 2) {
+    if (aligned) {  // two columns per lane on packed int16 keys
+      if (K <= 32) return launch_median_pk16<32, E>(d_src, K, N, d_out, st);
+      if (K <= 64) return launch_median_pk16<64, E>(d_src, K, N, d_out, st);
+      if (K <= 96) return launch_median_pk16<96, E>(d_src, K, N, d_out, st);
+      return launch_median_pk16<128, E>(d_src, K, N, d_out, st);
+    }
+  }
   if (K <= 8) return launch_median<8, E>(d_src, K, N, d_out, st);
   if (K <= 16) return launch_median<16, E>(d_src, K, N, d_out, st);
   if (K <= 24) return launch_median<24, E>(d_src, K, N, d_out, st);
@@ -1593,7 +1710,7 @@ int fedagg_lsa_reconstruct_f32(const int64_t* const* d_src, int32_t K, int64_t N
 
 int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K, int64_t N, void* d_out, uint32_t flags,
                   fedagg_stream_t stream) {
-  (void)flags;
+  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
   if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_median: K must be >= 1 and N >= 0");
   if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_median: null pointer");
   if (N == 0) return FEDAGG_OK;
@@ -1601,13 +1718,13 @@ int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K, int64_t N,
   switch (dtype) {
     case FEDAGG_DT_F32:
       return median_dispatch<MedF32>(reinterpret_cast<const float* const*>(d_src), K, N,
-                                     static_cast<float*>(d_out), st);
+                                     static_cast<float*>(d_out), aligned, st);
     case FEDAGG_DT_BF16:
       return median_dispatch<MedBF16>(reinterpret_cast<const uint16_t* const*>(d_src), K, N,
-                                      static_cast<uint16_t*>(d_out), st);
+                                      static_cast<uint16_t*>(d_out), aligned, st);
     case FEDAGG_DT_F16:
       return median_dispatch<MedF16>(reinterpret_cast<const uint16_t* const*>(d_src), K, N,
-                                     static_cast<uint16_t*>(d_out), st);
+                                     static_cast<uint16_t*>(d_out), aligned, st);
     default:
       return set_error(FEDAGG_EINVAL, "fedagg_median: dtype must be FEDAGG_DT_F32, _BF16 or _F16");
   }

@@ -53,13 +53,15 @@ def median_f32(d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor) -> None:
 _MEDIAN_DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16, torch.float16: nat.DT_F16}
 
 
-def median_rows(d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor) -> None:
+def median_rows(d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor, aligned: bool = False) -> None:
     """Coordinate-wise lower median of K device rows of out's dtype (fp32, bf16
-    or f16; fedagg_median)."""
+    or f16; fedagg_median).  aligned: every row pointer and out are 16-byte
+    aligned (bucket rows are), which lets 16-bit rows use the packed kernel."""
     kn._require_cuda(out, "median")
     if out.dtype not in _MEDIAN_DT:
         raise TypeError(f"median: fp32, bf16 or f16 rows (got {out.dtype})")
-    nat.check(nat.lib().fedagg_median(_MEDIAN_DT[out.dtype], d_ptrs.data_ptr(), K, N, out.data_ptr(), 0,
+    flags = nat.FEDAGG_ALIGNED16 if aligned and out.data_ptr() % 16 == 0 else 0
+    nat.check(nat.lib().fedagg_median(_MEDIAN_DT[out.dtype], d_ptrs.data_ptr(), K, N, out.data_ptr(), flags,
                                       nat.stream_handle()), "median")
 
 
@@ -95,7 +97,7 @@ def coordinate_wise_median(raw_client_grad_list: List[Tuple[float, "OrderedDict"
         bucket.sync_ingest()
         g = bucket.groups[row_dt]
         row_med = torch.empty(g.padded, dtype=row_dt, device=dev)
-        median_rows(g.d_ptrs, K, g.length, row_med)
+        median_rows(g.d_ptrs, K, g.length, row_med, aligned=True)  # bucket rows are 256-B aligned
         # the reference's vector: weight keys back to back, no alignment gaps
         vec = torch.cat([row_med[o:o + n] for o, n in zip(g.offsets, g.numels)]) if g.keys else row_med[:0]
         if not t0.is_cuda:

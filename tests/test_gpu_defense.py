@@ -122,22 +122,32 @@ def test_median_rejects_too_many_clients(cuda_device):
         dfn.median_f32(d_ptrs, 1025, 64, torch.empty(64, device=cuda_device))
 
 
+@pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K", [1, 9, 64, 127, 128, 129, 256, 257, 700, 1024])
-def test_median_16bit_rows_vs_oracle(dtype, K, cuda_device):
-    """bf16 / f16 rows (a 16-bit model's stack): every kernel family, with
-    duplicates, infinities, NaN columns and -0.0; the result is the selected
-    input, bit for bit."""
+@pytest.mark.parametrize("K", [1, 9, 33, 64, 127, 128, 129, 256, 257, 700, 1024])
+def test_median_16bit_rows_vs_oracle(aligned, dtype, K, cuda_device):
+    """bf16 / f16 rows (a 16-bit model's stack): every kernel family (aligned
+    rows with K <= 128 take the packed two-columns-per-lane kernel, with an odd
+    last column), with duplicates, infinities, NaN columns (a NaN in only one
+    column of a packed pair too) and -0.0; the result is the selected input,
+    bit for bit."""
     N = 2_051
     g = torch.Generator(device=cuda_device).manual_seed(K + 7)
-    rows = (torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125).to(dtype)
+    vals = (torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125).to(dtype)
+    if aligned:  # 256-B row stride, as bucket rows have
+        rows = torch.empty((K, 2_112), dtype=dtype, device=cuda_device)[:, :N]
+        rows.copy_(vals)
+    else:
+        rows = vals
     rows[:, 17:29] = torch.randn(K, 12, generator=g, device=cuda_device).to(dtype)
     rows[:, :7] = float("inf")
     rows[:, 7:9] = -float("inf")
     rows[K // 2, 100:110] = float("nan")
     rows[:, 200:203] = -0.0
+    rows[K - 1, 301] = float("nan")  # odd column of a pair: its neighbour stays a plain median
+    rows[0, N - 1] = float("nan")    # the unpaired last column
     d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
     out = torch.empty(N, dtype=dtype, device=cuda_device)
-    dfn.median_rows(d_ptrs, K, N, out)
+    dfn.median_rows(d_ptrs, K, N, out, aligned=aligned)
     exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
     gu.assert_same(out.cpu(), exp, f"median {dtype} K={K}")
