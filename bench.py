@@ -38,6 +38,7 @@ from fedml_amd.sharded import ClientAxisAggregator, ParamAxisAggregator  # noqa:
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+LSA_PRIME, LSA_QBITS = 2 ** 15 - 19, 10  # the reference's example LightSecAgg config (fedml_config.yaml:58-59)
 
 CONFIGS = {
     "cfg1": dict(model="lr_mnist", K=4, desc="FedAvg 4 clients x LogisticRegression MNIST (7,850 params) fp32"),
@@ -63,8 +64,9 @@ def parse():
     ap.add_argument("--fedopt", nargs="?", const="sgd", default=None, choices=["sgd", "adam", "adagrad"],
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
                          "or Adam / Adagrad lr=1.0 with torch defaults)")
-    ap.add_argument("--op", default="fedavg", choices=["fedavg", "median"],
-                    help="1 GPU: the reduction measured (median = the wise_median defense kernel)")
+    ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa"],
+                    help="1 GPU: the reduction measured (median = the wise_median defense kernel; secagg = "
+                         "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -159,10 +161,20 @@ def main():
         params = [k for k, _, d in entries if d == torch.float32]
         server = FedOptServer(init, params, K, a.fedopt, 1.0, 0.9, dev)
         bucket = server.bucket
+    elif a.op in ("secagg", "lsa"):
+        if world > 1:
+            raise SystemExit("--op secagg / lsa is a 1-GPU measurement")
+        # the model's elements as finite-field int64 rows (LightSecAgg's
+        # transform_tensor_to_finite output), one group
+        bucket = ClientBucket([(k, s, torch.int64) for k, s, _ in entries], K, dev, promote_ints=False)
     else:
         bucket = ClientBucket(entries, K, dev, low_precision_acc=a.acc)
     for gi, (dt, g) in enumerate(bucket.groups.items()):
-        fill_rows(g.rows, g.length, seed=1000 * rank + gi, round_idx=3)
+        if a.op in ("secagg", "lsa"):
+            gen = torch.Generator(device=dev).manual_seed(1000 * rank + gi)
+            g.rows.random_(0, LSA_PRIME, generator=gen)
+        else:
+            fill_rows(g.rows, g.length, seed=1000 * rank + gi, round_idx=3)
     from fedml_amd.synth import sample_nums
     ns_all = sample_nums(K * world, seed=1)
     ns_local = ns_all[rank * K:(rank + 1) * K]
@@ -198,6 +210,31 @@ def main():
 
         n_launch = 1
         dom_bytes = (K + 1) * gd.length * gd.rows.element_size()
+    elif a.op in ("secagg", "lsa"):
+        from fedml_amd import _native as nat
+
+        gd = bucket.groups[torch.int64]
+        if a.op == "secagg":
+            sec_out = torch.empty(gd.padded, dtype=torch.int64, device=dev)
+            call = lambda: nat.lib().fedagg_sum_mod_i64(gd.d_ptrs.data_ptr(), K, gd.length, LSA_PRIME,  # noqa: E731
+                                                        sec_out.data_ptr(), nat.FEDAGG_ALIGNED16, nat.stream_handle())
+            dom_bytes = (K + 1) * gd.length * 8
+        else:
+            mask = torch.empty(gd.padded, dtype=torch.int64, device=dev).random_(0, LSA_PRIME)
+            sec_out = torch.empty(gd.padded, dtype=torch.float32, device=dev)
+            call = lambda: nat.lib().fedagg_lsa_reconstruct_f32(  # noqa: E731
+                gd.d_ptrs.data_ptr(), K, gd.length, mask.data_ptr(), LSA_PRIME, LSA_QBITS, 1.0 / K,
+                sec_out.data_ptr(), nat.FEDAGG_ALIGNED16, nat.stream_handle())
+            dom_bytes = (K + 1) * gd.length * 8 + gd.length * 4
+
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record()
+            nat.check(call(), a.op)
+            if ev is not None:
+                ev[1].record()
+
+        n_launch = 1
     elif mode == "single":
         outs = bucket.new_outputs()
         w = bucket.weights(ns_local)
@@ -282,7 +319,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if dom_dt == torch.bfloat16 else "f32",
+        "dtype": "int64" if a.op in ("secagg", "lsa") else "bf16" if dom_dt == torch.bfloat16 else "f32",
         "data": "synthetic (base~N(0,0.05^2), client=base+0.01*eps, generated in HBM)",
         "config": {
             "workload": cfg["desc"],
@@ -304,7 +341,9 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": (f"median_kernel<128, {dom_dt}>" if a.op == "median" else
+            "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>"}[a.op]
+                       if a.op in ("secagg", "lsa") else
+                       f"median_kernel<128, {dom_dt}>" if a.op == "median" else
                        ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adagrad": "reduce_kernel<OpF32,AdagradEpi>"}
                         .get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>"))
                        + " (FedAvg+server step fused)"
@@ -315,7 +354,7 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
         line["cpu_baseline"] = cpu_baseline(entries, K, a.cpu_sample_elems)
     if rank == 0:
         print(json.dumps(line), flush=True)
