@@ -150,9 +150,14 @@ def main():
     mode = a.mode if world > 1 else "single"
 
     server = None
-    if a.fedopt:
-        if world > 1:
-            raise SystemExit("--fedopt is a 1-GPU measurement")
+    sharded_opt = None
+    if a.fedopt and world > 1:
+        if mode != "client":
+            raise SystemExit("--fedopt over several GPUs shards the client axis (--mode client)")
+        bucket = ClientBucket(entries, K, dev)
+        if set(bucket.groups) != {torch.float32}:
+            raise SystemExit("--fedopt over several GPUs takes an fp32 adapter set (config 5)")
+    elif a.fedopt:
         from collections import OrderedDict
 
         from fedml_amd.fedopt import FedOptServer
@@ -185,7 +190,22 @@ def main():
     n_elems = bucket.num_elements()
 
     # per-step work -------------------------------------------------------------
-    if server is not None:
+    if a.fedopt and world > 1:
+        from fedml_amd.sharded import ShardedFedOpt
+
+        gd = bucket.groups[torch.float32]
+        init = torch.zeros(gd.length, dtype=torch.float32, device=dev)
+        sharded_opt = ShardedFedOpt(gd.rows, gd.length, init, a.fedopt, 1.0, 0.9, chunks=a.chunks)
+        total = sum(ns_all)
+        w = [n / total for n in ns_all[rank * K:(rank + 1) * K]]
+
+        def step(ev=None):
+            sharded_opt.aggregate(w, events=ev)
+
+        n_launch = len(sharded_opt.agg.bounds)
+        sharded_opt.aggregate(w)  # first step (no state read) before timing
+        dom_bytes = K * gd.length * 4 + gd.length * 4  # rows in, fp32 partial out (the step is 1/G of a pass)
+    elif server is not None:
         for i, n in enumerate(ns_local):
             server.sample_num_dict[i] = n
 
@@ -328,8 +348,11 @@ def main():
             "elements_per_client": n_elems,
             "layout": "ClientBucket rows [K, L] per dtype, 256-B aligned rows",
             "low_precision_acc": a.acc,
-            "server_step": ({"sgd": "SGD lr=1.0 momentum=0.9 fused", "adam": "Adam lr=1.0 betas=(0.9,0.999) fused",
-                             "adagrad": "Adagrad lr=1.0 eps=1e-10 fused"}[a.fedopt] if server is not None else None),
+            "server_step": ({"sgd": "SGD lr=1.0 momentum=0.9", "adam": "Adam lr=1.0 betas=(0.9,0.999)",
+                             "adagrad": "Adagrad lr=1.0 eps=1e-10"}[a.fedopt]
+                            + (" fused" if server is not None else
+                               f", on each rank's 1/{world} shard after the reduce-scatter, sharded state")
+                            if a.fedopt else None),
             "parallelism": {"single": "1 GPU", "client": f"client-axis x{world}, RCCL reduce-scatter, "
                                                          f"{a.chunks}-chunk pipeline",
                             "param": f"parameter-axis x{world}, no collective"}[mode],
@@ -348,6 +371,7 @@ def main():
                         .get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>"))
                        + " (FedAvg+server step fused)"
                        if server is not None else
+                       f"reduce_kernel<OpF32> x{n_launch}/step + shard step" if sharded_opt is not None else
                        f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step"),
             "alg_bytes_per_step": dom_bytes,
             "kernel_ms_per_step": round(kern_ms, 4),

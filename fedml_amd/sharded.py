@@ -218,3 +218,94 @@ class ParamAxisAggregator:
         if events is not None:
             events[0][1].record(cur)
         return self.out[:self.length]
+
+
+class ShardedFedOpt:
+    """Config 5 on G GPUs: FedOpt with the client axis sharded.
+
+    The round's FedAvg is the client-axis mode above (local fp32 partial +
+    RCCL reduce-scatter), so rank g ends up owning the average of its
+    ``owned_ranges``.  The server optimizer then steps ONLY those elements,
+    with the global parameters and the optimizer state (momentum / Adam
+    moments / Adagrad sums) sharded the same way: a 1/G slice of the state
+    per GPU and no second exchange (gather the parameters with
+    ``gather_params`` when the full model is needed, e.g. to broadcast it).
+
+    The step is the fused FedAvg + optimizer kernel with ONE source, the
+    reduced shard, at weight 1.0 (fl(x * 1.0) == x), so it is the single-GPU
+    server step applied to the multi-GPU average.  Every element is treated as
+    a parameter: a LoRA adapter set (config 5) has no buffers.
+
+    stepper: test hook ``stepper(param, state: dict, avg)`` replacing the HIP
+    step (gloo tests on host rows, tests/test_sharded_gloo.py).
+    """
+
+    def __init__(self, rows: torch.Tensor, length: int, global_flat: torch.Tensor, optimizer: str = "sgd",
+                 lr: float = 1.0, momentum: float = 0.0, group=None, chunks: int = 8, reducer=None, stepper=None):
+        self.optimizer = optimizer.lower()
+        if self.optimizer not in ("sgd", "adam", "adagrad"):
+            raise NotImplementedError(f"server_optimizer {optimizer!r}: 'sgd', 'adam' and 'adagrad'")
+        self.lr, self.momentum = float(lr), float(momentum) if self.optimizer == "sgd" else 0.0
+        self.betas, self.eps = (0.9, 0.999), (1e-10 if self.optimizer == "adagrad" else 1e-8)
+        self.agg = ClientAxisAggregator(rows, length, group=group, chunks=chunks, reducer=reducer)
+        self.stepper = stepper
+        self.length = length
+        n = self.agg.shard.numel()
+        dev = self.agg.device
+        # this rank's slice of the global model, in shard order; padding past
+        # `length` stays 0 (its partial sums are 0 as well)
+        self.param = torch.zeros(n, dtype=torch.float32, device=dev)
+        for c, (a, b) in enumerate(self.agg.owned_ranges()):
+            a2, b2 = min(a, length), min(b, length)
+            if b2 > a2:
+                self.param[c * self.agg.piece: c * self.agg.piece + (b2 - a2)].copy_(global_flat[a2:b2])
+        z = lambda: torch.zeros(n, dtype=torch.float32, device=dev)  # noqa: E731
+        self.state = {"sgd": {"momentum_buffer": z()} if self.momentum else {},
+                      "adam": {"exp_avg": z(), "exp_avg_sq": z()} if self.optimizer == "adam" else {},
+                      "adagrad": {"sum": z()} if self.optimizer == "adagrad" else {}}[self.optimizer]
+        self.step_count = 0
+        if self.agg.on_gpu and stepper is None:
+            self._src = kn.upload_i64([self.agg.shard.data_ptr()], dev)  # one source: the reduced shard
+
+    def aggregate(self, weights: Sequence[float], events: Optional[List] = None) -> torch.Tensor:
+        """One round: weights are the GLOBAL w_i of this rank's clients.
+        Returns this rank's updated parameter shard."""
+        avg = self.agg.aggregate(weights, events=events)
+        first = self.step_count == 0
+        step = self.step_count + 1
+        if self.stepper is not None:
+            self.stepper(self.param, self.state, avg)
+        else:
+            n = avg.numel()
+            one = kn.HostWeights([1.0])
+            if self.optimizer == "sgd":
+                kn.wsum_fedopt_sgd(self._src, one, 1, n, self.param, self.state.get("momentum_buffer"), self.lr,
+                                   self.momentum, first, True)
+            elif self.optimizer == "adam":
+                sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step)
+                kn.wsum_fedopt_adam(self._src, one, 1, n, self.param, self.state["exp_avg"],
+                                    self.state["exp_avg_sq"], sc, first, True)
+            else:
+                kn.wsum_fedopt_adagrad(self._src, one, 1, n, self.param, self.state["sum"], self.lr, self.eps, True)
+        self.step_count = step
+        return self.param
+
+    def gather_params(self) -> torch.Tensor:
+        """The full [length] global model on every rank (all-gather of the
+        parameter shards, reassembled like ClientAxisAggregator.gather_full)."""
+        agg = self.agg
+        if agg.world == 1:
+            parts = [self.param]
+        elif agg.host_staged:
+            parts = [torch.empty_like(self.param, device="cpu") for _ in range(agg.world)]
+            dist.all_gather(parts, self.param.cpu(), group=agg.group)
+            parts = [p.to(self.param.device) for p in parts]
+        else:
+            parts = [torch.empty_like(self.param) for _ in range(agg.world)]
+            dist.all_gather(parts, self.param, group=agg.group)
+        full = torch.empty(len(agg.bounds) * agg.chunk_len, dtype=torch.float32, device=self.param.device)
+        for c in range(len(agg.bounds)):
+            for r in range(agg.world):
+                full[c * agg.chunk_len + r * agg.piece: c * agg.chunk_len + (r + 1) * agg.piece] = \
+                    parts[r][c * agg.piece:(c + 1) * agg.piece]
+        return full[:self.length]

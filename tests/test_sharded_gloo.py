@@ -125,3 +125,71 @@ def test_shard_range_tiles_axis():
                 assert b0 == a1
             for a, _ in spans:
                 assert a % 64 == 0 or a == n
+
+
+def _sgd_stepper(lr, momentum):
+    """torch.optim.SGD's update on flat host tensors (grad = p_old - avg)."""
+    def step(param, state, avg):
+        grad = param - avg
+        if momentum:
+            buf = state.get("momentum_buffer")
+            if buf is None or not state.get("_started"):
+                state["momentum_buffer"] = grad.clone()
+                state["_started"] = True
+            else:
+                buf.mul_(momentum).add_(grad)
+            grad = state["momentum_buffer"]
+        param.add_(grad, alpha=-lr)
+    return step
+
+
+def _fedopt_worker(rank, world, port, K_local, L, chunks, q):
+    try:
+        from fedml_amd.sharded import ShardedFedOpt
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        K = K_local * world
+        g0 = torch.from_numpy(np.random.default_rng(99).standard_normal(L, dtype=np.float32))
+        srv = ShardedFedOpt(torch.zeros(K_local, L), L, g0, "sgd", lr=0.7, momentum=0.9, chunks=chunks,
+                            reducer=_oracle_reducer, stepper=_sgd_stepper(0.7, 0.9))
+        out = []
+        for r in range(2):
+            allrows = _clients(K, L) + r  # a different round
+            srv.agg.rows = allrows[rank * K_local:(rank + 1) * K_local].clone()
+            ns = [int(v) for v in np.random.default_rng(7 + r).integers(100, 1001, K)]
+            ws = [n / sum(ns) for n in ns]
+            srv.aggregate(ws[rank * K_local:(rank + 1) * K_local])
+            out.append((srv.agg.gather_full().numpy().copy(), srv.gather_params().numpy().copy()))
+        q.put((rank, out, None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,K_local,L,chunks", [(2, 3, 5_003, 3), (3, 2, 700, 8)])
+def test_sharded_fedopt(world, K_local, L, chunks):
+    """Config 5's multi-GPU FedOpt: client-axis average, then the server SGD
+    (momentum 0.9) step on each rank's shard with sharded state.  The gathered
+    parameters equal the same step applied to the full gathered average, over
+    two rounds (state carried), on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fedopt_worker, args=(r, world, port, K_local, L, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, out, err in res:
+        assert err is None, err
+    g0 = torch.from_numpy(np.random.default_rng(99).standard_normal(L, dtype=np.float32))
+    p, state = g0.clone(), {}
+    step = _sgd_stepper(0.7, 0.9)
+    for r in range(2):
+        avg = torch.from_numpy(res[0][1][r][0])
+        step(p, state, avg)
+        for rank, out, _ in res:
+            np.testing.assert_array_equal(out[r][0], res[0][1][r][0])  # every rank gathers the same average
+            np.testing.assert_array_equal(out[r][1], p.numpy())
