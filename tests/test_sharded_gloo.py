@@ -72,7 +72,8 @@ def _worker(rank, world, port, K_local, L, chunks, q):
         q.put((rank, None, None, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,K_local,L,chunks", [(2, 4, 10_001, 3), (3, 3, 4_097, 8), (2, 1, 65, 8)])
+@pytest.mark.parametrize("world,K_local,L,chunks", [(2, 4, 10_001, 3), (3, 3, 4_097, 8), (2, 1, 65, 8),
+                                                      (4, 2, 3_001, 4), (8, 1, 2_049, 8)])
 def test_client_and_param_axis(world, K_local, L, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
