@@ -147,6 +147,7 @@ class ClientBucket:
         if self._copy is None:
             self._copy = torch.cuda.Stream(self.device)
             self._copy.wait_stream(torch.cuda.current_stream(self.device))
+        self._order_after_readers()
         with torch.cuda.stream(self._copy):
             for dt, host in regions:
                 if host is not None:
@@ -204,6 +205,7 @@ class ClientBucket:
                 lo, hi = g.offsets[j], g.offsets[j] + g.numels[j]
                 for i in range(K):
                     stage[i, lo:hi].copy_(state_dicts[i][g.keys[j]].reshape(-1))
+            self._order_after_readers()
             with torch.cuda.stream(self._copy):
                 g.rows.copy_(stage, non_blocking=True)
                 ev = torch.cuda.Event()
@@ -246,6 +248,7 @@ class ClientBucket:
                                                      nb.ctypes.data, int(srcs.size), _PACK_THREADS), "host_pack")
             for key, lo, n in ints:
                 stage[lo:lo + n].copy_(state_dict[key].reshape(-1))
+            self._order_after_readers()
             with torch.cuda.stream(self._copy):
                 g.rows[slot, :g.length].copy_(stage[:g.length], non_blocking=True)
                 ev = torch.cuda.Event()
@@ -311,12 +314,20 @@ class ClientBucket:
                                              (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*nbytes), n,
                                              _PACK_THREADS), "host_pack")
         del keep
+        self._order_after_readers()
         with torch.cuda.stream(self._copy):
             g.rows[slot, lo:hi].copy_(stage[lo:hi], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._copy)
         b[1] = ev
         self._pending = True
+
+    def _order_after_readers(self) -> None:
+        """An H2D into the rows must not overtake work already enqueued on the
+        caller's stream that reads them (the previous round's reduction when
+        the next update arrives before it finished): the copy stream waits for
+        the current stream first.  A GPU-side wait, no host synchronisation."""
+        self._copy.wait_stream(torch.cuda.current_stream(self.device))
 
     def sync_ingest(self) -> None:
         """Make the current stream wait for every H2D issued by put()."""

@@ -440,3 +440,29 @@ def test_large_host_rounds_stage_per_client_from_tables(cuda_device, monkeypatch
             assert not res[k].is_cuda and res[k].dtype == exp[k].dtype, k
             gu.assert_same(res[k], exp[k], f"round {r} {k}")
     assert calls == list(range(5)) * 2
+
+
+def test_next_update_does_not_overtake_a_pending_reduction(cuda_device):
+    """An update put() while the previous round's reduction is still queued on
+    the caller's stream must not overwrite the rows under it: the reduction
+    sees the old round, the next one the new data."""
+    K, N = 3, 1 << 20
+    bucket = ClientBucket([("x", (N,), torch.float32)], K, cuda_device)
+    old = [torch.full((N,), float(i + 1)) for i in range(K)]
+    new = torch.full((N,), 100.0)
+    for i in range(K):
+        bucket.put(i, {"x": old[i]}, 1)
+    outs = bucket.new_outputs()
+    w = bucket.weights([1, 1, 2])
+    bucket.sync_ingest()
+    torch.cuda._sleep(200_000_000)  # keep the stream busy so the reduction is still queued
+    bucket.reduce_into(outs, w)
+    bucket.put(0, {"x": new}, 1)  # host H2D on the copy stream
+    first = outs[torch.float32][:N].clone()
+    outs2 = bucket.new_outputs()
+    bucket.reduce_into(outs2, w)
+    torch.cuda.synchronize()
+    exp_old = orc.wsum(old, w)
+    exp_new = orc.wsum([new, old[1], old[2]], w)
+    gu.assert_same(first.cpu(), exp_old, "pending reduction")
+    gu.assert_same(outs2[torch.float32][:N].cpu(), exp_new, "next round")
