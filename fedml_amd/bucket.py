@@ -138,7 +138,10 @@ class ClientBucket:
         this bucket's row image, so each dtype group is ONE host->device copy
         straight from the message buffer (asynchronous when the transport
         received it into pinned memory; the runtime stages pageable memory
-        itself at ~PCIe rate).  No per-key host work at all."""
+        itself at ~PCIe rate).  No per-key host work at all.  A pinned message
+        buffer must not be rewritten (e.g. by the next receive) before
+        sync_ingest() or the reduction has been enqueued and the stream has
+        passed it; wait_ingest() blocks the host until then."""
         from . import wire
 
         if not 0 <= slot < self.capacity:
@@ -328,6 +331,12 @@ class ClientBucket:
         the next update arrives before it finished): the copy stream waits for
         the current stream first.  A GPU-side wait, no host synchronisation."""
         self._copy.wait_stream(torch.cuda.current_stream(self.device))
+
+    def wait_ingest(self) -> None:
+        """Block the host until every H2D issued by the put paths has landed
+        (the caller may then reuse its pinned receive buffers)."""
+        if self._copy is not None:
+            self._copy.synchronize()
 
     def sync_ingest(self) -> None:
         """Make the current stream wait for every H2D issued by put()."""
