@@ -178,7 +178,10 @@ def _multi_plan(numels: Sequence[int], code: int, acc_mode: int) -> kn.MultiPlan
 # Pipelined device path: keys are walked largest first in chunks, and each
 # chunk is launched as soon as it is walked, so the GPU reduces the bulk of the
 # bytes while the host is still walking the many small keys.
-_CHUNK_KEYS = (16, 32, 64)  # first chunks small: the GPU starts early; then the rest in 96s
+# first chunks small so the GPU starts early, then the rest in 96s.  Config 3
+# (tools/devdict_bench.py --chunks): 4,12,48 -> 2.52 ms per agg(), 8,24,64 ->
+# 2.55, 16,32,64 -> 2.61, 32,64 -> 2.61, 2,6,24,64 -> 2.57.
+_CHUNK_KEYS = (4, 12, 48)
 
 
 def _chunks(order: Sequence[int]):
