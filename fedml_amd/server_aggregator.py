@@ -123,3 +123,27 @@ class MI355XServerAggregator(ServerAggregator):
 
     def test(self, test_data, device, args):
         return None
+
+
+class _TaskEvalServerAggregator(MI355XServerAggregator):
+    """MyServerAggregatorNWP / MyServerAggregatorTAGPred
+    (my_server_aggregator_nwp.py:12-50, my_server_aggregator_prediction.py:12-67):
+    the same state-dict exchange and aggregation as the default aggregator;
+    they differ only in task-specific evaluation, which is outside the
+    aggregation path and raises here instead of reporting
+    nothing."""
+
+    def get_model_params(self):
+        return self.model.cpu().state_dict()  # :13-14 of both: always the host copy
+
+    def test(self, test_data, device, args):
+        raise NotImplementedError(f"server-side evaluation for dataset {getattr(args, 'dataset', None)!r} "
+                                  "is out of scope (fedml_amd rebuilds the aggregation path)")
+
+
+def create_server_aggregator(model, args) -> ServerAggregator:
+    """aggregator_creator.py:6-13: the dataset picks the class; every one of
+    them aggregates through FedMLAggOperator.agg on the GPU here."""
+    if getattr(args, "dataset", None) in ("stackoverflow_lr", "fed_shakespeare", "stackoverflow_nwp"):
+        return _TaskEvalServerAggregator(model, args)
+    return MI355XServerAggregator(model, args)

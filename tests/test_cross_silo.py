@@ -48,3 +48,22 @@ def test_client_draws_match_the_reference_numpy_calls():
     exp = np.random.choice([64, 65, 66, 67], 2, replace=False)
     assert list(s.client_selection(2, [64, 65, 66, 67], 2)) == list(exp)
     assert s.client_selection(2, [64, 65], 2) == [64, 65]
+
+
+def test_create_server_aggregator_picks_by_dataset():
+    """aggregator_creator.py:6-13: task-specific classes only change evaluation."""
+    from fedml_amd.server_aggregator import MI355XServerAggregator, create_server_aggregator
+
+    class A:
+        dataset = "mnist"
+
+    agg = create_server_aggregator(torch.nn.Linear(2, 2), A())
+    assert type(agg) is MI355XServerAggregator and agg.test(None, None, A()) is None
+    A.dataset = "stackoverflow_nwp"
+    agg = create_server_aggregator(torch.nn.Linear(2, 2), A())
+    assert isinstance(agg, MI355XServerAggregator)
+    try:
+        agg.test(None, None, A())
+        raise AssertionError("task evaluation should raise")
+    except NotImplementedError:
+        pass
