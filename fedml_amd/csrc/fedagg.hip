@@ -647,6 +647,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void re
   reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, int64_t(blockIdx.x) * BS * V);
 }
 
+// XCD-contiguous tile order (tuning variant): workgroups are dispatched to the
+// 8 XCDs round-robin, so block b runs on XCD b % 8; this remap gives each XCD
+// one contiguous range of tiles instead of every eighth tile (a bijection for
+// any grid size: XCD x takes q + (x < r) tiles, G = 8q + r).
+template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI, class WS>
+__global__ __launch_bounds__(BS) void reduce_xcd_kernel(Seg<OP> s, EPI epi, WS w, int K) {
+  const int64_t G = gridDim.x, b = blockIdx.x, q = G / 8, r = G % 8, x = b % 8;
+  const int64_t tile = x * q + (x < r ? x : r) + b / 8;
+  reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, tile * BS * V);
+}
+
 // Grid-stride form: a resident grid walks the tiles, so no partial last wave of
 // workgroups is left running alone at the end.
 template <class OP, int U, int V, bool NT, int BS>
@@ -807,6 +818,15 @@ int variant_fn(const float* const* src, const float* w, int32_t K, int64_t N, fl
   return launch_uvn<OpF32, U, V, NT, BS>(src, PtrW<float>{w}, K, N, out, true, st, "fedagg_wsum_f32_variant");
 }
 
+template <int U, int V, int BS>
+int xcd_fn(const float* const* src, const float* w, int32_t K, int64_t N, float* out, hipStream_t st) {
+  const int64_t grid = ((N + 3) / 4 + int64_t(BS) * V - 1) / (int64_t(BS) * V);
+  Seg<OpF32> s{src, N};
+  hipLaunchKernelGGL((reduce_xcd_kernel<OpF32, U, V, true, true, BS, StoreEpi<OpF32>, PtrW<float>>), dim3(unsigned(grid)),
+                     dim3(BS), 0, st, s, StoreEpi<OpF32>{out}, PtrW<float>{w}, K);
+  return check_launch("xcd");
+}
+
 template <int U, int V, int BS, int PER_CU>
 int persistent_fn(const float* const* src, const float* w, int32_t K, int64_t N, float* out, hipStream_t st) {
   constexpr int E = 4;
@@ -831,6 +851,7 @@ const Variant kVariants[] = {
     {"U4V4nt_p8", persistent_fn<4, 4, 256, 8>},   {"U4V2nt_p8", persistent_fn<4, 2, 256, 8>},
     {"U1V4nt", variant_fn<1, 4, true, 256>},      {"U1V2nt", variant_fn<1, 2, true, 256>},
     {"U2V2nt", variant_fn<2, 2, true, 256>},
+    {"U4V4nt_xcd", xcd_fn<4, 4, 256>},            {"U1V4nt_xcd", xcd_fn<1, 4, 256>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
