@@ -551,6 +551,61 @@ __device__ __forceinline__ void reduce_scalar(const Seg<OP>& s, const EPI& epi, 
   epi.one(e, acc);
 }
 
+// Bounds-checked elements e, e + BS, ... (< e1), M at most, all chains in
+// lockstep with SU clients' loads in flight; identical arithmetic to
+// reduce_scalar, element by element.
+template <class OP, int M, int BS, class EPI, class WS>
+__device__ __forceinline__ void reduce_edge(const Seg<OP>& s, const EPI& epi, const WS& w, int K, int64_t e, int64_t e1) {
+  constexpr int SU = (64 / M) < 1 ? 1 : ((64 / M) > 16 ? 16 : (64 / M));
+  using in_t = typename OP::in_t;
+  if (e >= e1) return;  // a lane past the end of a short last block owns nothing (and must load nothing)
+  bool ok[M];
+  typename OP::acc_t acc[M];
+  {
+    const auto p0 = as_global(s.src[0]);
+    const auto w0 = w[0];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      ok[j] = e + int64_t(j) * BS < e1;
+      acc[j] = OP::first(p0[ok[j] ? e + int64_t(j) * BS : e], w0);
+    }
+  }
+  // Out-of-range elements load a valid in-range address instead (e itself,
+  // in range after the check above), so the loads need no predicate and
+  // batch; their chains are discarded.
+  int64_t idx[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) idx[j] = ok[j] ? e + int64_t(j) * BS : e;
+  int c = 1;
+  for (; c + SU <= K; c += SU) {
+    in_t x[SU][M];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const auto p = as_global(s.src[c + u]);
+#pragma unroll
+      for (int j = 0; j < M; ++j) x[u][j] = p[idx[j]];
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const auto wu = w[c + u];
+#pragma unroll
+      for (int j = 0; j < M; ++j) acc[j] = OP::step(acc[j], x[u][j], wu);
+    }
+  }
+  for (; c < K; ++c) {  // fewer than SU clients left
+    const auto p = as_global(s.src[c]);
+    const auto wc = w[c];
+    in_t x[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) x[j] = p[idx[j]];
+#pragma unroll
+    for (int j = 0; j < M; ++j) acc[j] = OP::step(acc[j], x[j], wc);
+  }
+#pragma unroll
+  for (int j = 0; j < M; ++j)
+    if (ok[j]) epi.one(e + int64_t(j) * BS, acc[j]);
+}
+
 // Body of one workgroup of BS lanes: packs [pack0, pack0 + BS*V) of segment s.
 template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI, class WS>
 __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi, const WS& w, int K, int64_t pack0) {
@@ -624,9 +679,12 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi, c
     for (int v = 0; v < V; ++v) epi.pack(off[v], acc[v], pre[v]);
   } else {
     // ---- edge path: element-wise with bounds ---------------------------------
+    // The lane's V*E elements (e0 + t + j*BS) advance TOGETHER through the
+    // client chain, so a ragged last block costs one chain, not V*E chains
+    // one after another (that tail dominated small tensors with many clients).
     const int64_t e0 = pack0 * E;
     const int64_t e1 = min(s.numel, (pack0 + int64_t(BS) * V) * E);
-    for (int64_t e = e0 + t; e < e1; e += BS) reduce_scalar<OP>(s, epi, w, K, e);
+    reduce_edge<OP, V * E, BS>(s, epi, w, K, e0 + t, e1);
   }
 }
 
@@ -698,6 +756,13 @@ template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; st
 struct SmallCfg { static constexpr int U = 16, V = 1, BS = 64; static constexpr bool NT = true; };
 constexpr int64_t kSmallBelowBlocks = 1024;  // shipped-tile workgroups below which SmallCfg is used
 
+// Many clients over a tensor too small to give every CU a workgroup (e.g. 1,000
+// clients x a 7,850-element model): each lane's chain over the clients is a
+// sequence of memory round trips, so twice the clients in flight halves it.
+struct TinyCfg { static constexpr int U = 32, V = 1, BS = 64; static constexpr bool NT = true; };
+constexpr int64_t kTinyBelowElems = 65536;  // fewer than 256 small-tile workgroups
+constexpr int32_t kTinyFromClients = 48;
+
 // Mid-sized launches (1,024 to 4,096 tiles: every tile resident at once or
 // nearly so) stream one client at a time per lane (56 VGPRs instead of 94).
 // tools/tune_wsum.py and tools/adam_probe.py on MI355X: 64 x 4.19M (config 5)
@@ -739,6 +804,8 @@ template <class OP, class WS>
 int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t N, typename OP::out_t* o, bool al,
               hipStream_t st, const char* name) {
   const int64_t blocks = blocks_for<OP>(N);
+  if (N < kTinyBelowElems && K >= kTinyFromClients)
+    return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks <= kMidUpToBlocks)

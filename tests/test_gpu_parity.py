@@ -466,3 +466,21 @@ def test_next_update_does_not_overtake_a_pending_reduction(cuda_device):
     exp_new = orc.wsum([new, old[1], old[2]], w)
     gu.assert_same(first.cpu(), exp_old, "pending reduction")
     gu.assert_same(outs2[torch.float32][:N].cpu(), exp_new, "next round")
+
+
+@pytest.mark.parametrize("K", [2, 17, 48, 100])
+@pytest.mark.parametrize("N", [1, 3, 5, 63, 65, 255, 257, 1023, 4_097, 70_001])
+def test_tight_tensors_every_tile_config(K, N, cuda_device):
+    """Separately allocated client tensors of exactly N elements (no padding
+    to read into), aligned and at an odd element offset, across the tile
+    configs (tiny many-client, small, shipped) and their ragged edge paths."""
+    g = torch.Generator(device=cuda_device).manual_seed(K * 100_003 + N)
+    ts = [torch.randn(N, generator=g, device=cuda_device) * 0.05 for _ in range(K)]
+    views = [torch.randn(N + 1, generator=g, device=cuda_device)[1:] for _ in range(K)]  # 4-byte offset
+    ns = [3 + 7 * i for i in range(K)]
+    w = [n / sum(ns) for n in ns]
+    for group in (ts, views):
+        out = torch.empty(N, device=cuda_device)
+        kn.wsum_tensors(group, w, out)
+        exp = orc.wsum([t.cpu() for t in group], w)
+        gu.assert_same(out.cpu(), exp, f"K={K} N={N}")
