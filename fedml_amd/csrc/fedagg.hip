@@ -1305,8 +1305,8 @@ __device__ typename E::S g_median_pad[2] = {__builtin_bit_cast(typename E::S, st
                                             __builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
                                                 sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kPosInf))};
 
-template <int P, int R, bool FULL, class E = MedF32>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
+template <int P, int R, bool FULL, class E = MedF32, int BS = 256>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
     const typename E::S* const* __restrict__ src, int K, int64_t N, typename E::S* __restrict__ out) {
   using S = typename E::S;
   static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2, 4, 8 or 16 lanes per column");
@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
   const int t = threadIdx.x, sub = t & (P - 1);
   if constexpr (FULL) K = KMAX;
   const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
-  for (int i = t; i < KMAX; i += 256) {
+  for (int i = t; i < KMAX; i += BS) {
     const int q = i + PAD * (i / R);
     if (FULL || i < K) {
       rows[q] = src[i];
@@ -1334,7 +1334,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
   __syncthreads();
   // every lane stays active through the DPP exchanges; a column past the end
   // recomputes the last one and does not store
-  const int64_t e = (int64_t(blockIdx.x) * 256 + t) / P;
+  const int64_t e = (int64_t(blockIdx.x) * BS + t) / P;
   const uint64_t boff = uint64_t(e < N ? e : N - 1) * sizeof(S);
   float v[R];
   bool has_nan = false;
@@ -1382,14 +1382,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void m
   if (sub == 0 && e < N) out[e] = E::narrow(nan_slot < KMAX ? nan_v : m);
 }
 
-template <int P, int R, class E = MedF32>
+template <int P, int R, class E = MedF32, int BS = 256>
 int launch_median_lanes(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
-  const int64_t grid = (N * P + 255) / 256;
+  const int64_t grid = (N * P + BS - 1) / BS;
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
   if (K == P * R)
-    hipLaunchKernelGGL((median_lanes_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+    hipLaunchKernelGGL((median_lanes_kernel<P, R, true, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
+                       out);
   else
-    hipLaunchKernelGGL((median_lanes_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
+    hipLaunchKernelGGL((median_lanes_kernel<P, R, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
+                       out);
   return check_launch("fedagg_median");
 }
 

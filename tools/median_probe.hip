@@ -170,9 +170,20 @@ extern "C" int median_big_probe(int v, const void* src, int K, int64_t N, void* 
     if (K <= 512) return launch_median_lanes<4, 128>(s, K, N, o, st);
     return launch_median_lanes<8, 128>(s, K, N, o, st);
   }
-  if (K <= 256) return launch_median_lanes<4, 64>(s, K, N, o, st);
-  if (K <= 512) return launch_median_lanes<8, 64>(s, K, N, o, st);
-  return launch_median_lanes<16, 64>(s, K, N, o, st);
+  if (v == 2) {
+    if (K <= 256) return launch_median_lanes<4, 64>(s, K, N, o, st);
+    if (K <= 512) return launch_median_lanes<8, 64>(s, K, N, o, st);
+    return launch_median_lanes<16, 64>(s, K, N, o, st);
+  }
+  // v == 5 / 6: the shipped layouts with 128- / 64-lane blocks
+  if (v == 5) {
+    if (K <= 256) return launch_median_lanes<4, 64, MedF32, 128>(s, K, N, o, st);
+    if (K <= 512) return launch_median_lanes<4, 128, MedF32, 128>(s, K, N, o, st);
+    return launch_median_lanes<8, 128, MedF32, 128>(s, K, N, o, st);
+  }
+  if (K <= 256) return launch_median_lanes<4, 64, MedF32, 64>(s, K, N, o, st);
+  if (K <= 512) return launch_median_lanes<4, 128, MedF32, 64>(s, K, N, o, st);
+  return launch_median_lanes<8, 128, MedF32, 64>(s, K, N, o, st);
 }
 
 // K is fixed at 128 (the full kernel); src is a device table of 128 row pointers

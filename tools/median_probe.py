@@ -98,10 +98,10 @@ def probe_big(lib, kn, dev, st, summary):
     All outputs must agree bit for bit."""
     lib.median_big_probe.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
                                      ctypes.c_void_p]
-    names = {0: "radix", 1: "lanes128", 2: "lanes64", 3: "lanes64x2", 4: "net128"}
+    names = {0: "radix", 1: "lanes128", 2: "lanes64", 3: "lanes64x2", 4: "net128", 5: "shipped_bs128", 6: "shipped_bs64"}
     N2 = 4_000_000
     for K2 in (128, 129, 256, 257, 512, 513, 1024):
-        vs = (4, 3) if K2 <= 128 else (0, 1, 2)
+        vs = (4, 3) if K2 <= 128 else (1, 2, 5, 6)
         rows = torch.randn((K2, N2), device=dev) * 0.05
         tab = kn.upload_i64([rows[i].data_ptr() for i in range(K2)], dev)
         outs = {v: torch.empty(N2, device=dev) for v in vs}
