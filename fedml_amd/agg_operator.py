@@ -182,6 +182,19 @@ def _multi_plan(numels: Sequence[int], code: int, acc_mode: int) -> kn.MultiPlan
 # (tools/devdict_bench.py --chunks): 4,12,48 -> 2.52 ms per agg(), 8,24,64 ->
 # 2.55, 16,32,64 -> 2.61, 32,64 -> 2.61, 2,6,24,64 -> 2.57.
 _CHUNK_KEYS = (4, 12, 48)
+# Chunks from this index on hold only small keys (ResNet-50: 87K of 25.6M
+# elements over 256 keys).  Their launches are bound by the 128-deep client
+# chain per element, not by bytes (26-52 us each at config 3), so they go to a
+# side stream and run beside the big HBM-bound launches instead of after them.
+_SIDE_FROM_CHUNK = len(_CHUNK_KEYS)
+_SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(device: torch.device) -> "torch.cuda.Stream":
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device)
+    return s
 
 
 def _chunks(order: Sequence[int]):
@@ -210,20 +223,44 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
     results: Dict[str, torch.Tensor] = {}
     keep = []  # device tables of the launches, alive until enqueued
     w32 = None
-    for idx in _chunks(order):
-        ck = [keys[i] for i in idx]
-        walked = w.walk(dicts, ck, True)
-        if walked is None:
-            return None
-        dev_idx, codes, numels, tables, outs, out_tables = walked
-        device = torch.device("cuda", dev_idx)
-        with torch.cuda.device(device):
-            if w32 is None:
-                w32 = kn.upload_f32(weights, device)
-            for code, tab in tables.items():
-                ns = [n for n, c in zip(numels, codes) if c == code]
-                keep.append(_multi_plan(ns, code, acc_mode).launch(tab, out_tables[code], w32, K, device))
-        results.update(zip(ck, outs))
+    start = {}  # device -> event on the caller's stream before the first launch
+    joins = []  # (caller's stream, side stream) pairs to rejoin before returning
+    try:
+        for ci, idx in enumerate(_chunks(order)):
+            ck = [keys[i] for i in idx]
+            walked = w.walk(dicts, ck, True)
+            if walked is None:
+                return None
+            dev_idx, codes, numels, tables, outs, out_tables = walked
+            device = torch.device("cuda", dev_idx)
+            with torch.cuda.device(device):
+                if w32 is None:
+                    w32 = kn.upload_f32(weights, device)
+                cur = torch.cuda.current_stream(device)
+                if device not in start:
+                    # what the caller's stream queued before this call (the
+                    # inputs' producers, earlier users of the outputs' memory)
+                    # and the weights' upload
+                    start[device] = torch.cuda.Event()
+                    start[device].record(cur)
+                st = cur
+                if ci >= _SIDE_FROM_CHUNK and tables:
+                    st = _side_stream(device)
+                    # ... but not the big launches of this call: the side
+                    # launches run beside them
+                    st.wait_event(start[device])
+                    if (cur, st) not in joins:
+                        joins.append((cur, st))
+                with torch.cuda.stream(st):
+                    for code, tab in tables.items():
+                        ns = [n for n, c in zip(numels, codes) if c == code]
+                        keep.append(_multi_plan(ns, code, acc_mode).launch(tab, out_tables[code], w32, K, device))
+            results.update(zip(ck, outs))
+    finally:
+        # the caller's stream waits for the side launches, also when a later
+        # chunk is declined (their outputs are then freed into its pool)
+        for cur, st in joins:
+            cur.wait_stream(st)
     return OrderedDict((k, results[k]) for k in keys)
 
 

@@ -201,6 +201,34 @@ def test_pipelined_walk_declines_in_a_later_chunk(cuda_device):
         gu.assert_same(res[key].cpu(), exp[key], key)
 
 
+def test_tail_chunks_on_side_stream_are_stream_ordered(cuda_device):
+    """The small-key chunks launch on a side stream.  Called on a non-default
+    stream whose queue still holds the inputs' producer (a slow GEMM chain
+    feeding every client tensor), agg() must read the produced values, and the
+    caller's stream must see the side stream's outputs without a device sync."""
+    entries = shapes.resnet50()
+    K = 4
+    raw = host_clients(entries, K, seed=11, round_idx=3)
+    keys = list(raw[0][1].keys())
+    assert len(keys) > sum(ao._CHUNK_KEYS)  # some chunks go to the side stream
+    args = type("A", (), {"federated_optimizer": "FedAvg"})()
+    exp = orc.agg(args, copy.deepcopy(raw))
+    staged = _to_device(raw, cuda_device)
+    s = torch.cuda.Stream(cuda_device)
+    torch.cuda.synchronize(cuda_device)
+    with torch.cuda.stream(s):
+        m = torch.randn(4096, 4096, device=cuda_device)
+        for _ in range(8):  # tens of ms of queued work before the inputs exist
+            m = torch.tanh(m @ m)
+        one = (m[0, 0] * 0).abs() + 1  # 1, but only once the chain has run
+        # the producers: x * 1 == x exactly, ordered after the GEMM chain on s
+        dev = [(n, OrderedDict((k, x * one.to(x.dtype)) for k, x in d.items())) for n, d in staged]
+        res = ao.FedMLAggOperator.agg(args, dev)
+        got = OrderedDict((k, v.to("cpu", non_blocking=False)) for k, v in res.items())
+    for key in exp:
+        gu.assert_same(got[key], exp[key], key)
+
+
 def test_unaligned_views_take_scalar_path(cuda_device):
     """Tensors that are views at odd element offsets (not 16-byte aligned)."""
     K, N = 5, 4099
