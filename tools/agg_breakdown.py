@@ -18,7 +18,7 @@ def breakdown(lst, reps: int = 5) -> dict:
     keys = list(dicts[0].keys())
     K = len(dicts)
     w = ao._walker()
-    t = {"order": [], "walk_alloc": [], "plans": [], "launch": []}
+    t = {"order": [], "walk_alloc": [], "plans": [], "launch": [], "weights": [], "to_first_launch": []}
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -26,20 +26,25 @@ def breakdown(lst, reps: int = 5) -> dict:
         tw = tp = tl = 0.0
         t1 = time.perf_counter()
         w32 = None
+        tu = first = 0.0
         for idx in ao._chunks(order):
             a = time.perf_counter()
             dev_idx, codes, numels, tables, outs, out_tables = w.walk(dicts, [keys[i] for i in idx], True)
             b = time.perf_counter()
             dev = torch.device("cuda", dev_idx)
             if w32 is None:
+                u = time.perf_counter()
                 w32 = kn.upload_f32([1.0 / K] * K, dev)
+                tu = time.perf_counter() - u
             plans = {c: ao._multi_plan([n for n, cc in zip(numels, codes) if cc == c], c, 0) for c in tables}
             c_ = time.perf_counter()
             for c, plan in plans.items():
                 plan.launch(tables[c], out_tables[c], w32, K, dev)
             d = time.perf_counter()
+            if not first:
+                first = d - t0
             tw, tp, tl = tw + (b - a), tp + (c_ - b), tl + (d - c_)
-        for k, v in zip(t, (t1 - t0, tw, tp, tl)):
+        for k, v in zip(t, (t1 - t0, tw, tp - tu, tl, tu, first)):
             t[k].append(v * 1e3)
     torch.cuda.synchronize()
     return {k: round(statistics.median(v), 3) for k, v in t.items()}
