@@ -188,6 +188,8 @@ _CHUNK_KEYS = (4, 12, 48)
 # side stream and run beside the big HBM-bound launches instead of after them.
 _SIDE_FROM_CHUNK = len(_CHUNK_KEYS)
 _SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
+# The weights go up with the first chunk's pointer table (one H2D, not two).
+_WEIGHTS_IN_TABLE = True
 
 
 def _side_stream(device: torch.device) -> "torch.cuda.Stream":
@@ -234,27 +236,38 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
             dev_idx, codes, numels, tables, outs, out_tables = walked
             device = torch.device("cuda", dev_idx)
             with torch.cuda.device(device):
-                if w32 is None:
-                    w32 = kn.upload_f32(weights, device)
                 cur = torch.cuda.current_stream(device)
-                if device not in start:
+
+                def mark_start(device=device, cur=cur):
                     # what the caller's stream queued before this call (the
                     # inputs' producers, earlier users of the outputs' memory)
-                    # and the weights' upload
-                    start[device] = torch.cuda.Event()
-                    start[device].record(cur)
+                    # and the weights' upload, but none of this call's kernels
+                    if device not in start:
+                        start[device] = torch.cuda.Event()
+                        start[device].record(cur)
+
+                side = ci >= _SIDE_FROM_CHUNK and bool(tables)
+                if w32 is None and (side or not _WEIGHTS_IN_TABLE):
+                    w32 = kn.upload_f32(weights, device)
+                    mark_start()
                 st = cur
-                if ci >= _SIDE_FROM_CHUNK and tables:
+                if side:
                     st = _side_stream(device)
-                    # ... but not the big launches of this call: the side
-                    # launches run beside them
+                    # the side launches run beside this call's big launches
                     st.wait_event(start[device])
                     if (cur, st) not in joins:
                         joins.append((cur, st))
                 with torch.cuda.stream(st):
                     for code, tab in tables.items():
                         ns = [n for n, c in zip(numels, codes) if c == code]
-                        keep.append(_multi_plan(ns, code, acc_mode).launch(tab, out_tables[code], w32, K, device))
+                        plan = _multi_plan(ns, code, acc_mode)
+                        if w32 is None:  # the weights ride in the first table's H2D
+                            ret = plan.launch(tab, out_tables[code], None, K, device, weights=weights,
+                                              on_uploaded=mark_start)
+                            w32 = ret[-1]
+                        else:
+                            ret = plan.launch(tab, out_tables[code], w32, K, device)
+                        keep.append(ret)
             results.update(zip(ck, outs))
     finally:
         # the caller's stream waits for the side launches, also when a later

@@ -142,6 +142,17 @@ _MULTI_DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16, torch.float
 MULTI_DTYPES = tuple(_MULTI_DT)
 
 
+class DevPtr:
+    """A device address inside a tensor (kept alive here): data_ptr() only."""
+
+    def __init__(self, owner: torch.Tensor, ptr: int):
+        self.owner = owner
+        self.ptr = ptr
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+
 class MultiPlan:
     """Segment table for the one-launch multi-tensor kernel (fedagg_wsum_multi):
     T keys of one dtype, each with K client pointers.  int64 keys produce
@@ -164,12 +175,17 @@ class MultiPlan:
         self.total_blocks = begin[-1]
         self._meta = {}
 
-    def launch(self, src_ptrs, out_ptrs: List[int], d_w: torch.Tensor, K: int,
-               device: torch.device) -> List[torch.Tensor]:
+    def launch(self, src_ptrs, out_ptrs: List[int], d_w, K: int, device: torch.device,
+               weights: "Sequence[float] | None" = None, on_uploaded=None) -> list:
         """src_ptrs is the flattened [T][K] table (a list of ints, or an int64
         numpy array / bytes as the native dict walker produces it).  Returns
         the device tables, which must stay referenced until the launch has
-        been enqueued."""
+        been enqueued.
+
+        d_w None: the fp32 weights ride at the end of the pointer table's
+        upload (one H2D instead of two), and the returned list ends with a
+        DevPtr to them for later launches.  on_uploaded() is called after the
+        upload is enqueued and before the kernel is."""
         T = len(self.numels)
         if isinstance(src_ptrs, (bytes, bytearray)):
             src_ptrs = np.frombuffer(src_ptrs, dtype=np.int64)
@@ -183,15 +199,29 @@ class MultiPlan:
         d_meta = self._meta.get((device, st))
         if d_meta is None:
             d_meta = self._meta[(device, st)] = upload_i64(self.numels + self.block_begin, device)
-        if isinstance(src_ptrs, np.ndarray) or isinstance(out_ptrs, np.ndarray):
-            tab = np.concatenate([np.asarray(src_ptrs, dtype=np.int64), np.asarray(out_ptrs, dtype=np.int64)])
+        tail = []
+        if d_w is None:
+            if weights is None or len(weights) != K:
+                raise ValueError("MultiPlan.launch: K weights needed when d_w is None")
+            wf = np.asarray([float(v) for v in weights], dtype=np.float32)
+            if wf.size % 2:
+                wf = np.append(wf, np.float32(0.0))
+            tail = [wf.view(np.int64)]
+        if tail or isinstance(src_ptrs, np.ndarray) or isinstance(out_ptrs, np.ndarray):
+            tab = np.concatenate([np.asarray(src_ptrs, dtype=np.int64), np.asarray(out_ptrs, dtype=np.int64)] + tail)
         else:
             tab = list(src_ptrs) + list(out_ptrs)
         d_tab = upload_i64(tab, device)
+        ret = [d_meta, d_tab]
+        if d_w is None:
+            d_w = DevPtr(d_tab, d_tab.data_ptr() + 8 * (T * K + T))
+            ret.append(d_w)
+        if on_uploaded is not None:
+            on_uploaded()
         nat.check(nat.lib().fedagg_wsum_multi(self.dt, self.acc_mode, d_tab.data_ptr(), d_tab.data_ptr() + 8 * T * K,
                                               d_meta.data_ptr(), d_meta.data_ptr() + 8 * T, T, d_w.data_ptr(), K,
                                               self.total_blocks, st), "wsum_multi")
-        return [d_meta, d_tab]
+        return ret
 
 
 class MultiF32Plan(MultiPlan):

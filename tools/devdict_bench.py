@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--chunks", default="", help="comma list overriding agg_operator._CHUNK_KEYS (e.g. 4,12,48)")
+    ap.add_argument("--ab-weights", action="store_true",
+                    help="also time agg() with the weights in the first table's H2D vs a separate upload, "
+                         "interleaved (agg_operator._WEIGHTS_IN_TABLE)")
     a = ap.parse_args()
     if a.chunks:
         from fedml_amd import agg_operator as ao
@@ -73,6 +76,22 @@ def main():
            "host_enqueue_ms_median": sorted(t[0] for t in times)[len(times) // 2] * 1e3,
            "wall_to_done_ms_median": sorted(t[1] for t in times)[len(times) // 2] * 1e3,
            "gpu_window_ms_median": sorted(gpu)[len(gpu) // 2]}
+    if a.ab_weights:
+        from fedml_amd import agg_operator as ao
+
+        ab = {True: [], False: []}
+        for r in range(4 * a.reps):
+            flag = bool(r % 2)
+            ao._WEIGHTS_IN_TABLE = flag
+            lst = [(raw[0][0], OrderedDict(c0))] + raw[1:]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            FedMLAggOperator.agg(args, lst)
+            torch.cuda.synchronize()
+            ab[flag].append((time.perf_counter() - t0) * 1e3)
+        ao._WEIGHTS_IN_TABLE = True
+        res["ab_wall_to_done_ms"] = {"weights_in_table": sorted(ab[True])[len(ab[True]) // 2],
+                                     "separate_upload": sorted(ab[False])[len(ab[False]) // 2]}
     print(json.dumps(res, indent=1))
     os.makedirs("gpurun_out", exist_ok=True)
     json.dump(res, open("gpurun_out/devdict.json", "w"), indent=1)
