@@ -182,6 +182,7 @@ def _multi_plan(numels: Sequence[int], code: int, acc_mode: int) -> kn.MultiPlan
 # (tools/devdict_bench.py --chunks): 4,12,48 -> 2.52 ms per agg(), 8,24,64 ->
 # 2.55, 16,32,64 -> 2.61, 32,64 -> 2.61, 2,6,24,64 -> 2.57.
 _CHUNK_KEYS = (4, 12, 48)
+_TAIL_CHUNK = 96  # keys per chunk after _CHUNK_KEYS
 # Chunks from this index on hold only small keys (ResNet-50: 87K of 25.6M
 # elements over 256 keys).  Their launches are bound by the 128-deep client
 # chain per element, not by bytes (26-52 us each at config 3), so they go to a
@@ -207,8 +208,8 @@ def _chunks(order: Sequence[int]):
         yield order[lo:lo + n]
         lo += n
     while lo < len(order):
-        yield order[lo:lo + 96]
-        lo += 96
+        yield order[lo:lo + _TAIL_CHUNK]
+        lo += _TAIL_CHUNK
 
 
 def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--chunks", default="", help="comma list overriding agg_operator._CHUNK_KEYS (e.g. 4,12,48)")
+    ap.add_argument("--tail", type=int, default=0, help="override agg_operator._TAIL_CHUNK")
     ap.add_argument("--ab-weights", action="store_true",
                     help="also time agg() with the weights in the first table's H2D vs a separate upload, "
                          "interleaved (agg_operator._WEIGHTS_IN_TABLE)")
@@ -38,6 +39,10 @@ def main():
         from fedml_amd import agg_operator as ao
 
         ao._CHUNK_KEYS = tuple(int(x) for x in a.chunks.split(","))
+    if a.tail:
+        from fedml_amd import agg_operator as ao
+
+        ao._TAIL_CHUNK = a.tail
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     ents = shapes.resnet50()
@@ -72,7 +77,8 @@ def main():
     import agg_breakdown  # noqa: F401  (tools/agg_breakdown.py)
 
     bd = agg_breakdown.breakdown([(raw[0][0], OrderedDict(c0))] + raw[1:], a.reps)
-    res = {"K": a.K, "tensors": a.K * len(ents), "chunks": a.chunks or "default", "breakdown_ms": bd,
+    res = {"K": a.K, "tensors": a.K * len(ents), "chunks": a.chunks or "default", "tail": a.tail or "default",
+           "breakdown_ms": bd,
            "host_enqueue_ms_median": sorted(t[0] for t in times)[len(times) // 2] * 1e3,
            "wall_to_done_ms_median": sorted(t[1] for t in times)[len(times) // 2] * 1e3,
            "gpu_window_ms_median": sorted(gpu)[len(gpu) // 2]}
