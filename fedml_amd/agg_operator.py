@@ -225,8 +225,8 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
     K = len(dicts)
     results: Dict[str, torch.Tensor] = {}
     keep = []  # device tables of the launches, alive until enqueued
-    w32 = None
-    start = {}  # device -> event on the caller's stream before the first launch
+    w32 = {}  # device -> the weights there (the walker checks one device per chunk, not across chunks)
+    start = {}  # device -> event on the caller's stream before this call's first kernel there
     joins = []  # (caller's stream, side stream) pairs to rejoin before returning
     try:
         for ci, idx in enumerate(_chunks(order)):
@@ -248,8 +248,8 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
                         start[device].record(cur)
 
                 side = ci >= _SIDE_FROM_CHUNK and bool(tables)
-                if w32 is None and (side or not _WEIGHTS_IN_TABLE):
-                    w32 = kn.upload_f32(weights, device)
+                if device not in w32 and (side or not _WEIGHTS_IN_TABLE):
+                    w32[device] = kn.upload_f32(weights, device)
                     mark_start()
                 st = cur
                 if side:
@@ -262,12 +262,12 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
                     for code, tab in tables.items():
                         ns = [n for n, c in zip(numels, codes) if c == code]
                         plan = _multi_plan(ns, code, acc_mode)
-                        if w32 is None:  # the weights ride in the first table's H2D
+                        if device not in w32:  # the weights ride in the first table's H2D
                             ret = plan.launch(tab, out_tables[code], None, K, device, weights=weights,
                                               on_uploaded=mark_start)
-                            w32 = ret[-1]
+                            w32[device] = ret[-1]
                         else:
-                            ret = plan.launch(tab, out_tables[code], w32, K, device)
+                            ret = plan.launch(tab, out_tables[code], w32[device], K, device)
                         keep.append(ret)
             results.update(zip(ck, outs))
     finally:
