@@ -142,6 +142,16 @@ _MULTI_DT = {torch.float32: nat.DT_F32, torch.bfloat16: nat.DT_BF16, torch.float
 MULTI_DTYPES = tuple(_MULTI_DT)
 
 
+def weights_as_i64(weights: Sequence[float]) -> np.ndarray:
+    """fp32 weights (RNE from the Python floats, as torch.tensor rounds them)
+    packed two per int64 slot, zero-padded to an even count: the tail of a
+    pointer table upload, read by the kernel as K floats."""
+    wf = np.asarray([float(v) for v in weights], dtype=np.float32)
+    if wf.size % 2:
+        wf = np.append(wf, np.float32(0.0))
+    return wf.view(np.int64)
+
+
 class DevPtr:
     """A device address inside a tensor (kept alive here): data_ptr() only."""
 
@@ -203,10 +213,7 @@ class MultiPlan:
         if d_w is None:
             if weights is None or len(weights) != K:
                 raise ValueError("MultiPlan.launch: K weights needed when d_w is None")
-            wf = np.asarray([float(v) for v in weights], dtype=np.float32)
-            if wf.size % 2:
-                wf = np.append(wf, np.float32(0.0))
-            tail = [wf.view(np.int64)]
+            tail = [weights_as_i64(weights)]
         if tail or isinstance(src_ptrs, np.ndarray) or isinstance(out_ptrs, np.ndarray):
             tab = np.concatenate([np.asarray(src_ptrs, dtype=np.int64), np.asarray(out_ptrs, dtype=np.int64)] + tail)
         else:

@@ -235,3 +235,21 @@ def test_dict_walker_pool_under_repeated_walks():
     dicts[5][keys[3]] = torch.nn.Parameter(torch.zeros(2))
     assert w.walk(dicts, keys) is None
 
+
+
+@pytest.mark.parametrize("K", [1, 3, 4, 129])
+def test_weights_ride_in_pointer_table(K):
+    """The device-dict path appends the fp32 weights to the first pointer
+    table's upload: K floats, RNE from the Python floats as torch.tensor
+    rounds them, two per int64 slot, zero-padded to an even count."""
+    import numpy as np
+
+    from fedml_amd import kernels as kn
+
+    ns = [float(v) for v in np.random.default_rng(K).integers(1, 1000, K)]
+    ws = [n / sum(ns) for n in ns]
+    packed = kn.weights_as_i64(ws)
+    assert packed.dtype == np.int64 and packed.size == (K + 1) // 2
+    back = packed.view(np.float32)
+    assert torch.equal(torch.from_numpy(back[:K].copy()), torch.tensor(ws, dtype=torch.float32))
+    assert back.size == K or back[K] == 0.0
