@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-elems", type=int, default=2_600_000)
+    ap.add_argument("--cpu-reps", type=int, default=5, help="cpu_baseline: timed runs after one warm-up")
     return ap.parse_args()
 
 
@@ -92,28 +92,51 @@ def fill_rows(rows: torch.Tensor, length: int, seed: int, round_idx: int = 0) ->
     del base, eps
 
 
-def cpu_baseline(entries, K: int, sample_elems: int) -> dict:
-    """The reference's own CPU loop (torch eager, oracle/cpu_baseline.py) on the
-    first keys of the same state dict up to ~sample_elems elements per client,
-    all K clients; reported in client-params/s."""
-    from oracle import cpu_baseline as cb
-    from fedml_amd.synth import host_clients
+def host_round(bucket) -> list:
+    """The bench's round as the reference's CPU server holds it: K pageable
+    per-key host tensors per client (contiguous slices of one host copy of
+    each client's row; integer keys as int64 tensors), copied from HBM."""
+    from collections import OrderedDict
 
-    sub, tot = [], 0
-    for e in entries:
-        n = 1
-        for s in e[1]:
-            n *= s
-        if tot + n > sample_elems and sub:
-            break
-        sub.append(e)
-        tot += n
-    raw = host_clients(sub, K, seed=123)
-    r = cb.time_fedavg(raw, reps=3)
-    return {"value": K * tot / r["median_s"], "unit": "client-params/s", "cores": r["threads"], "kind": "port",
-            "sample": f"{K} clients x first {len(sub)} of {len(entries)} state-dict keys ({tot:,} elements/client), "
-                      f"torch-eager restatement of agg_operator.py:35-44, median of {r['reps']} after 1 warm-up, "
-                      f"{r['median_s'] * 1e3:.1f} ms/aggregation"}
+    raw = []
+    for i in range(bucket.capacity):
+        d = OrderedDict()
+        rows = {dt: g.rows[i, :g.length].cpu() for dt, g in bucket.groups.items()}
+        for key, shape, dt in bucket.entries:
+            g, j = bucket.where[key]
+            t = rows[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].view(shape)
+            d[key] = t.to(dt) if key in bucket.int_keys else t
+        raw.append((bucket.sample_nums[i] if bucket.sample_nums[i] is not None else 1, d))
+    return raw
+
+
+def cpu_baseline(bucket, ns, reps: int) -> dict:
+    """The reference's own CPU loop (agg_operator.py:35-44 in torch eager,
+    oracle/cpu_baseline.py) on the FULL workload: every key of the state dict,
+    all K clients, the same values as the HBM rows.  Median of `reps` runs
+    after one warm-up, at every CPU this job may use and at one thread."""
+    from oracle import cpu_baseline as cb
+
+    raw = host_round(bucket)
+    raw = [(n, d) for n, (_, d) in zip(ns, raw)]
+    cpus = cb.host_cpus()
+    full = cb.time_fedavg(raw, reps=reps, threads=cpus["usable"])
+    one = cb.time_fedavg(raw, reps=reps, threads=1)
+    K = len(raw)
+    n_elems = bucket.num_elements()
+    del raw
+    return {"value": K * n_elems / full["median_s"], "unit": "client-params/s", "cores": full["threads"],
+            "kind": "port",
+            "sample": f"full workload: all {len(bucket.entries)} state-dict keys x {K} clients "
+                      f"({n_elems:,} elements/client), torch-eager restatement of agg_operator.py:35-44, "
+                      f"median of {reps} after 1 warm-up: {full['median_s'] * 1e3:.1f} ms/aggregation at "
+                      f"{full['threads']} threads, {one['median_s'] * 1e3:.1f} ms at 1 thread",
+            "threads": full["threads"],
+            "ms_per_aggregation": round(full["median_s"] * 1e3, 2),
+            "single_thread": {"value": K * n_elems / one["median_s"], "threads": 1,
+                              "ms_per_aggregation": round(one["median_s"] * 1e3, 2)},
+            "host": {"cpu_model": cpus["model"], "nproc": cpus["nproc"], "affinity_cpus": cpus["affinity"],
+                     "cgroup_quota_cpus": cpus["cgroup_quota_cpus"]}}
 
 
 def load_traffic(config: str, mode: str, world: int, variant: str = ""):
@@ -154,16 +177,16 @@ def main():
     if a.fedopt and world > 1:
         if mode != "client":
             raise SystemExit("--fedopt over several GPUs shards the client axis (--mode client)")
-        bucket = ClientBucket(entries, K, dev)
+        bucket = ClientBucket(entries, K, dev)  # integer buffers promoted into the fp32 row
         if set(bucket.groups) != {torch.float32}:
-            raise SystemExit("--fedopt over several GPUs takes an fp32 adapter set (config 5)")
+            raise SystemExit("--fedopt over several GPUs takes an fp32 model (integer buffers promoted)")
     elif a.fedopt:
         from collections import OrderedDict
 
         from fedml_amd.fedopt import FedOptServer
 
         init = OrderedDict((k, torch.zeros(s, dtype=d)) for k, s, d in entries)
-        params = [k for k, _, d in entries if d == torch.float32]
+        params = shapes.param_names(entries)
         server = FedOptServer(init, params, K, a.fedopt, 1.0, 0.9, dev)
         bucket = server.bucket
     elif a.op in ("secagg", "lsa"):
@@ -191,11 +214,12 @@ def main():
 
     # per-step work -------------------------------------------------------------
     if a.fedopt and world > 1:
-        from fedml_amd.sharded import ShardedFedOpt
+        from fedml_amd.sharded import ShardedFedOpt, buffer_ranges
 
         gd = bucket.groups[torch.float32]
         init = torch.zeros(gd.length, dtype=torch.float32, device=dev)
-        sharded_opt = ShardedFedOpt(gd.rows, gd.length, init, a.fedopt, 1.0, 0.9, chunks=a.chunks)
+        sharded_opt = ShardedFedOpt(gd.rows, gd.length, init, a.fedopt, 1.0, 0.9, chunks=a.chunks,
+                                    buffers=buffer_ranges(bucket, shapes.param_names(entries)))
         total = sum(ns_all)
         w = [n / total for n in ns_all[rank * K:(rank + 1) * K]]
 
@@ -379,7 +403,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
-        line["cpu_baseline"] = cpu_baseline(entries, K, a.cpu_sample_elems)
+        line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -451,6 +451,11 @@ def torch_aggregator(args, raw_grad_list, training_num):
         _gather([raw_grad_list[i][2] for i in range(K)], keys)
         _, weights_delta, c_delta_para = raw_grad_list[K - 1]
         w_c = 1 / args.client_num_in_total
+        # :110,113: the running c_delta sum is client 0's own tensor (bound at
+        # i == 0), so `+=` leaves Σ_i c_i in it, in place: the one side
+        # effect of the branch that outlives it
+        if K > 1:
+            sequential_sum_inplace([raw_grad_list[i][2] for i in range(K)], keys, args)
         # :116-117 overwrite the weighted sums with the LAST client's delta and
         # its control variate times w_c; only that survives.
         scaled = weighted_reduce([c_delta_para], keys, [w_c], args)

@@ -114,7 +114,8 @@ class ClientBucket:
         (``sync_ingest``, called by reduce_into)."""
         if not 0 <= slot < self.capacity:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
-        host: Dict[torch.dtype, List[Tuple[int, int, torch.Tensor]]] = {}
+        host: Dict[torch.dtype, List[Tuple[int, int, int, torch.Tensor]]] = {}
+        dev_seen: Dict[torch.dtype, int] = {}  # device keys met so far per group: host runs break there
         for key, _, _ in self.entries:
             t = state_dict[key]
             g, j = self.where[key]
@@ -127,8 +128,9 @@ class ClientBucket:
                 if src.dtype != g.dtype:
                     src = src.to(g.dtype)
                 g.rows[slot, g.offsets[j]:g.offsets[j] + g.numels[j]].copy_(src, non_blocking=True)
+                dev_seen[g.dtype] = dev_seen.get(g.dtype, 0) + 1
             else:
-                host.setdefault(g.dtype, []).append((g.offsets[j], g.numels[j], t))
+                host.setdefault(g.dtype, []).append((dev_seen.get(g.dtype, 0), g.offsets[j], g.numels[j], t))
         for dt, parts in host.items():
             self._stage(dt, slot, parts)
         self.sample_nums[slot] = sample_num
@@ -299,12 +301,19 @@ class ClientBucket:
         if b[1] is not None:
             b[1].synchronize()  # this staging row's previous H2D has landed
         stage = b[0]
-        lo = min(p[0] for p in parts)
-        hi = max(p[0] + p[1] for p in parts)
+        # parts: (run, element offset, count, tensor) in layout order; a run
+        # is a stretch of host keys with no device key between them, and each
+        # run is ONE H2D of its span: never over a device key's range, which
+        # put() already copied D2D (the staging there holds stale bytes)
+        runs: Dict[int, List[int]] = {}
+        for run, off, n, _ in parts:
+            r = runs.setdefault(run, [off, off + n])
+            r[0], r[1] = min(r[0], off), max(r[1], off + n)
+        lo = min(r[0] for r in runs.values())
         esz = stage.element_size()
         keep = []
         srcs, offs, nbytes = [], [], []
-        for off, n, t in parts:
+        for _, off, n, t in parts:
             src = t.reshape(-1)
             if src.dtype != dt or not src.is_contiguous():
                 src = src.to(dt).contiguous()
@@ -319,7 +328,8 @@ class ClientBucket:
         del keep
         self._order_after_readers()
         with torch.cuda.stream(self._copy):
-            g.rows[slot, lo:hi].copy_(stage[lo:hi], non_blocking=True)
+            for a, e in runs.values():
+                g.rows[slot, a:e].copy_(stage[a:e], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._copy)
         b[1] = ev

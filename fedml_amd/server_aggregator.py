@@ -21,9 +21,14 @@ FedML's own ServerAggregator through this operator.
 """
 from __future__ import annotations
 
+import copy
+import logging
 from abc import ABC, abstractmethod
 from collections import OrderedDict
 from typing import List, Tuple
+
+import torch
+from torch import nn
 
 from . import defense as dfn
 from .agg_operator import FedMLAggOperator
@@ -105,9 +110,79 @@ class ServerAggregator(ABC):
         pass
 
 
+def _evaluate(model, test_data, device, task: str) -> dict:
+    """The `_test` loops of default_aggregator.py:25-75 ("classification", and
+    its stackoverflow_lr branch "tag_prediction"), my_server_aggregator_
+    prediction.py:19-60 ("tag_prediction") and my_server_aggregator_nwp.py:
+    19-43 ("nwp"): the same criteria, predictions and metric sums.  Server
+    evaluation is model inference, not aggregation; it runs with torch on
+    `device` exactly as in the reference."""
+    model.to(device)
+    model.eval()
+    metrics = {"test_correct": 0, "test_loss": 0, "test_total": 0}
+    if task == "tag_prediction":
+        metrics.update(test_precision=0, test_recall=0)
+        criterion = nn.BCELoss(reduction="sum").to(device)
+    elif task == "nwp":
+        criterion = nn.CrossEntropyLoss(ignore_index=0).to(device)
+    else:
+        metrics.update(test_precision=0, test_recall=0)
+        criterion = nn.CrossEntropyLoss().to(device)
+    with torch.no_grad():
+        for batch_idx, (x, target) in enumerate(test_data):
+            x = x.to(device)
+            target = target.to(device)
+            pred = model(x)
+            loss = criterion(pred, target)
+            if task == "tag_prediction":
+                predicted = (pred > 0.5).int()
+                correct = predicted.eq(target).sum(axis=-1).eq(target.size(1)).sum()
+                true_positive = ((target * predicted) > 0.1).int().sum(axis=-1)
+                metrics["test_precision"] += (true_positive / (predicted.sum(axis=-1) + 1e-13)).sum().item()
+                metrics["test_recall"] += (true_positive / (target.sum(axis=-1) + 1e-13)).sum().item()
+            elif task == "nwp":
+                _, predicted = torch.max(pred, 1)
+                target_pos = ~(target == 0)
+                correct = (predicted.eq(target) * target_pos).sum()
+            else:
+                _, predicted = torch.max(pred, 1)
+                correct = predicted.eq(target).sum()
+            metrics["test_correct"] += correct.item()
+            metrics["test_loss"] += loss.item() * target.size(0)
+            if task == "nwp":
+                metrics["test_total"] += target_pos.sum().item()
+            elif task == "tag_prediction" or len(target.size()) == 1:
+                metrics["test_total"] += target.size(0)
+            elif len(target.size()) == 2:  # next-word prediction targets through the default class
+                metrics["test_total"] += target.size(0) * target.size(1)
+    return metrics
+
+
+def _report(args, round_args, metrics) -> tuple:
+    """default_aggregator.py:77-106: accuracy and mean loss over the test
+    set, logged, returned as the four-metric tuple the server stores in its
+    Context (fedml_aggregator.py:193-202).  mlops is outside this build;
+    wandb is logged when enabled, as in the reference."""
+    test_tot_corrects = [copy.deepcopy(metrics["test_correct"])]
+    test_num_samples = [copy.deepcopy(metrics["test_total"])]
+    test_losses = [copy.deepcopy(metrics["test_loss"])]
+    test_acc = sum(test_tot_corrects) / sum(test_num_samples)
+    test_loss = sum(test_losses) / sum(test_num_samples)
+    if getattr(args, "enable_wandb", False):
+        import wandb  # the reference imports it unconditionally
+
+        wandb.log({"Test/Acc": test_acc, "round": round_args.round_idx})
+        wandb.log({"Test/Loss": test_loss, "round": round_args.round_idx})
+    logging.info({"test_acc": test_acc, "test_loss": test_loss})
+    return (test_acc, test_loss, None, None)
+
+
 class MI355XServerAggregator(ServerAggregator):
-    """DefaultServerAggregator (default_aggregator.py:12-23) on MI355X:
-    state_dict in, load_state_dict out, FedAvg on the GPU."""
+    """DefaultServerAggregator (default_aggregator.py:12-106) on MI355X:
+    state_dict in, load_state_dict out, FedAvg on the GPU, and the
+    reference's server-side evaluation in test()."""
+
+    _task = "classification"
 
     def __init__(self, model, args):
         super().__init__(model, args)
@@ -121,29 +196,42 @@ class MI355XServerAggregator(ServerAggregator):
     def set_model_params(self, model_parameters):
         self.model.load_state_dict(model_parameters)
 
+    def _test(self, test_data, device, args):
+        task = self._task
+        if task == "classification" and getattr(args, "dataset", None) == "stackoverflow_lr":
+            task = "tag_prediction"  # default_aggregator.py:45-63
+        return _evaluate(self.model, test_data, device, task)
+
     def test(self, test_data, device, args):
-        return None
+        """-> (test_acc, test_loss, None, None), default_aggregator.py:77-106."""
+        return _report(self.args, args, self._test(test_data, device, args))
 
 
-class _TaskEvalServerAggregator(MI355XServerAggregator):
-    """MyServerAggregatorNWP / MyServerAggregatorTAGPred
-    (my_server_aggregator_nwp.py:12-50, my_server_aggregator_prediction.py:12-67):
-    the same state-dict exchange and aggregation as the default aggregator;
-    they differ only in task-specific evaluation, which is outside the
-    aggregation path and raises here instead of reporting
-    nothing."""
+class MI355XServerAggregatorTAGPred(MI355XServerAggregator):
+    """MyServerAggregatorTAGPred (my_server_aggregator_prediction.py:12-90):
+    the host copy of the model, multi-label (BCE) evaluation."""
+
+    _task = "tag_prediction"
 
     def get_model_params(self):
-        return self.model.cpu().state_dict()  # :13-14 of both: always the host copy
+        return self.model.cpu().state_dict()  # :13-14
 
-    def test(self, test_data, device, args):
-        raise NotImplementedError(f"server-side evaluation for dataset {getattr(args, 'dataset', None)!r} "
-                                  "is out of scope (fedml_amd rebuilds the aggregation path)")
+
+class MI355XServerAggregatorNWP(MI355XServerAggregator):
+    """MyServerAggregatorNWP (my_server_aggregator_nwp.py:12-72): the host copy
+    of the model, next-word-prediction evaluation (padding id 0 ignored)."""
+
+    _task = "nwp"
+
+    def get_model_params(self):
+        return self.model.cpu().state_dict()  # :13-14
 
 
 def create_server_aggregator(model, args) -> ServerAggregator:
     """aggregator_creator.py:6-13: the dataset picks the class; every one of
     them aggregates through FedMLAggOperator.agg on the GPU here."""
-    if getattr(args, "dataset", None) in ("stackoverflow_lr", "fed_shakespeare", "stackoverflow_nwp"):
-        return _TaskEvalServerAggregator(model, args)
+    if args.dataset == "stackoverflow_lr":
+        return MI355XServerAggregatorTAGPred(model, args)
+    if args.dataset in ("fed_shakespeare", "stackoverflow_nwp"):
+        return MI355XServerAggregatorNWP(model, args)
     return MI355XServerAggregator(model, args)

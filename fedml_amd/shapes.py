@@ -112,6 +112,16 @@ MODELS = {
 }
 
 
+_BUFFER_SUFFIXES = (".running_mean", ".running_var", ".num_batches_tracked")
+
+
+def param_names(entries: List[Entry]) -> List[str]:
+    """The named parameters of these state-dict entries (model.named_parameters()
+    order): everything but BatchNorm's registered buffers.  What FedOpt steps
+    (FedOptAggregator.py:118-125); buffers take the average."""
+    return [k for k, _, _ in entries if not k.endswith(_BUFFER_SUFFIXES)]
+
+
 def numel(entries: List[Entry], dtype: torch.dtype | None = None) -> int:
     tot = 0
     for _, shape, dt in entries:

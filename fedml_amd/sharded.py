@@ -88,10 +88,14 @@ class ClientAxisAggregator:
                            for lo, _ in self.bounds]
         elif reducer is None:
             raise ValueError("host rows need a reducer (the HIP kernels read HBM only)")
+        # The exchange runs whenever there is more than one rank, or a process
+        # group was handed in explicitly (a one-rank RCCL group exercises the
+        # comm stream, the async handles and the stream joins on one GPU).
+        self.collective = dist.is_initialized() and (self.world > 1 or group is not None)
         # gloo has no device collectives: stage through the host (a rehearsal
         # mode for N ranks sharing one GPU; RCCL is the production backend)
-        self.host_staged = (self.world > 1 and self.on_gpu and dist.get_backend(group) == "gloo")
-        self.comm_stream = torch.cuda.Stream(dev) if self.world > 1 and self.on_gpu and not self.host_staged else None
+        self.host_staged = self.collective and self.on_gpu and dist.get_backend(group) == "gloo"
+        self.comm_stream = torch.cuda.Stream(dev) if self.collective and self.on_gpu and not self.host_staged else None
 
     def owned_ranges(self) -> List[Tuple[int, int]]:
         """Global element ranges this rank owns, in shard order (one per chunk)."""
@@ -106,13 +110,15 @@ class ClientAxisAggregator:
         if not self.on_gpu:
             return self._aggregate_host(weights)
         cur = torch.cuda.current_stream(self.device)
-        d_w = kn.weights_for(weights, torch.float32, self.device)
+        d_w = kn.weights_for(weights, torch.float32, self.device) if self.K else None
         works = []
         for c, (lo, hi) in enumerate(self.bounds):
             part = self.partial[c * self.chunk_len: c * self.chunk_len + (hi - lo)]
             if events is not None:
                 events[c][0].record(cur)
-            if self.reducer is not None:
+            if self.K == 0:  # a rank without clients this round contributes zeros
+                part.zero_()
+            elif self.reducer is not None:
                 self.reducer(self.rows[:, lo:hi], weights, part)
             else:
                 kn.wsum_ptrs(self.dtype, self.d_ptrs[c], d_w, self.K, hi - lo, part, True)
@@ -123,7 +129,7 @@ class ClientAxisAggregator:
                 dst = torch.empty(self.piece, dtype=src.dtype)
                 dist.reduce_scatter_tensor(dst, src, op=dist.ReduceOp.SUM, group=self.group)
                 self.shard[c * self.piece:(c + 1) * self.piece].copy_(dst)
-            elif self.world > 1:
+            elif self.collective:
                 # chunk c's exchange overlaps chunk c+1's reduction
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):
@@ -142,10 +148,14 @@ class ClientAxisAggregator:
 
     def _aggregate_host(self, weights: Sequence[float]) -> torch.Tensor:
         for c, (lo, hi) in enumerate(self.bounds):
-            self.reducer(self.rows[:, lo:hi], weights, self.partial[c * self.chunk_len: c * self.chunk_len + (hi - lo)])
+            part = self.partial[c * self.chunk_len: c * self.chunk_len + (hi - lo)]
+            if self.K == 0:
+                part.zero_()
+            else:
+                self.reducer(self.rows[:, lo:hi], weights, part)
             src = self.partial[c * self.chunk_len:(c + 1) * self.chunk_len]
             dst = self.shard[c * self.piece:(c + 1) * self.piece]
-            if self.world > 1:
+            if self.collective:
                 dist.reduce_scatter_tensor(dst, src, op=dist.ReduceOp.SUM, group=self.group)
             else:
                 dst.copy_(src)
@@ -161,7 +171,7 @@ class ClientAxisAggregator:
     def gather_full(self) -> torch.Tensor:
         """Reassemble the full [length] result on every rank (all-gather of the
         shards; used by tests and when the model must be replicated)."""
-        if self.world == 1:
+        if not self.collective:
             parts = [self.shard]
         elif self.host_staged:
             parts = [torch.empty_like(self.shard, device="cpu") for _ in range(self.world)]
@@ -220,6 +230,24 @@ class ParamAxisAggregator:
         return self.out[:self.length]
 
 
+def buffer_ranges(layout, param_names: Sequence[str]) -> List[Tuple[int, int]]:
+    """Element ranges [lo, hi) of the fp32 row that hold BUFFERS (every key
+    not among the named parameters: BatchNorm running stats, integer
+    counters promoted into the fp32 row), merged where adjacent.  layout: a
+    ClientBucket or RowLayout."""
+    g = layout.groups[torch.float32]
+    params = set(param_names)
+    out: List[Tuple[int, int]] = []
+    for key, off, n in zip(g.keys, g.offsets, g.numels):
+        if n == 0 or key in params:
+            continue
+        if out and out[-1][1] == off:
+            out[-1] = (out[-1][0], off + n)
+        else:
+            out.append((off, off + n))
+    return out
+
+
 class ShardedFedOpt:
     """Config 5 on G GPUs: FedOpt with the client axis sharded.
 
@@ -233,15 +261,24 @@ class ShardedFedOpt:
 
     The step is the fused FedAvg + optimizer kernel with ONE source, the
     reduced shard, at weight 1.0 (fl(x * 1.0) == x), so it is the single-GPU
-    server step applied to the multi-GPU average.  Every element is treated as
-    a parameter: a LoRA adapter set (config 5) has no buffers.
+    server step applied to the multi-GPU average.  As in the reference
+    (FedOptAggregator.set_model_global_grads, FedOptAggregator.py:118-130)
+    only named parameters are stepped: ``buffers`` lists the element ranges of
+    the flat fp32 layout that hold buffers (``buffer_ranges(layout,
+    param_names)``), and those take the plain average.  The step runs over
+    the whole shard in one launch and the buffer elements are then
+    overwritten with the average in one gather/scatter, so a model with
+    hundreds of interleaved BatchNorm buffers still costs two launches; the
+    optimizer state at buffer positions is never read back.  A LoRA adapter
+    set (config 5) has no buffers.
 
     stepper: test hook ``stepper(param, state: dict, avg)`` replacing the HIP
     step (gloo tests on host rows, tests/test_sharded_gloo.py).
     """
 
     def __init__(self, rows: torch.Tensor, length: int, global_flat: torch.Tensor, optimizer: str = "sgd",
-                 lr: float = 1.0, momentum: float = 0.0, group=None, chunks: int = 8, reducer=None, stepper=None):
+                 lr: float = 1.0, momentum: float = 0.0, group=None, chunks: int = 8, reducer=None, stepper=None,
+                 buffers: Sequence[Tuple[int, int]] = ()):
         self.optimizer = optimizer.lower()
         if self.optimizer not in ("sgd", "adam", "adagrad"):
             raise NotImplementedError(f"server_optimizer {optimizer!r}: 'sgd', 'adam' and 'adagrad'")
@@ -259,6 +296,15 @@ class ShardedFedOpt:
             a2, b2 = min(a, length), min(b, length)
             if b2 > a2:
                 self.param[c * self.agg.piece: c * self.agg.piece + (b2 - a2)].copy_(global_flat[a2:b2])
+        # shard positions of the buffer elements this rank owns
+        idx = []
+        for c, (a, b) in enumerate(self.agg.owned_ranges()):
+            for lo, hi in buffers:
+                x, y = max(a, lo), min(b, hi, length)
+                if y > x:
+                    base = c * self.agg.piece - a
+                    idx.append(torch.arange(base + x, base + y, dtype=torch.int64))
+        self.buffer_idx = torch.cat(idx).to(dev) if idx else None
         z = lambda: torch.zeros(n, dtype=torch.float32, device=dev)  # noqa: E731
         self.state = {"sgd": {"momentum_buffer": z()} if self.momentum else {},
                       "adam": {"exp_avg": z(), "exp_avg_sq": z()} if self.optimizer == "adam" else {},
@@ -287,6 +333,8 @@ class ShardedFedOpt:
                                     self.state["exp_avg_sq"], sc, first, True)
             else:
                 kn.wsum_fedopt_adagrad(self._src, one, 1, n, self.param, self.state["sum"], self.lr, self.eps, True)
+        if self.buffer_idx is not None:  # buffers take the average (FedOptAggregator.py:126-130)
+            self.param.index_copy_(0, self.buffer_idx, avg.index_select(0, self.buffer_idx))
         self.step_count = step
         return self.param
 
@@ -294,7 +342,7 @@ class ShardedFedOpt:
         """The full [length] global model on every rank (all-gather of the
         parameter shards, reassembled like ClientAxisAggregator.gather_full)."""
         agg = self.agg
-        if agg.world == 1:
+        if not agg.collective:
             parts = [self.param]
         elif agg.host_staged:
             parts = [torch.empty_like(self.param, device="cpu") for _ in range(agg.world)]

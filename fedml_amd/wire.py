@@ -109,8 +109,7 @@ def encode(state_dict, sample_num, promote_ints: bool = True) -> bytearray:
     return buf
 
 
-def parse_header(buf) -> Tuple[dict, int]:
-    """(header dict, payload start offset); raises WireFormatError."""
+def _parse(buf) -> Tuple[dict, int, int]:
     mv = memoryview(buf)
     if len(mv) < _PRE:
         raise WireFormatError("message shorter than the fixed preamble")
@@ -121,8 +120,52 @@ def parse_header(buf) -> Tuple[dict, int]:
         raise WireFormatError(f"unsupported version {ver}")
     if len(mv) < _PRE + H + P:
         raise WireFormatError(f"truncated message: {len(mv)} < {_PRE + H + P}")
-    header = json.loads(bytes(mv[_PRE:_PRE + H]).decode())
-    return header, _PRE + H
+    try:
+        header = json.loads(bytes(mv[_PRE:_PRE + H]).decode())
+    except (UnicodeDecodeError, ValueError) as e:
+        raise WireFormatError(f"header is not JSON: {e}") from None
+    if not isinstance(header, dict):
+        raise WireFormatError("header is not a JSON object")
+    return header, _PRE + H, P
+
+
+def parse_header(buf) -> Tuple[dict, int]:
+    """(header dict, payload start offset); raises WireFormatError."""
+    header, base, _ = _parse(buf)
+    return header, base
+
+
+def _check_regions(header: dict, layout: RowLayout, P: int) -> None:
+    """The header's region and side-table lists against the layout and the
+    payload length: the message comes from the network, so a short list
+    (zip would truncate and leave a group's row stale), a wrong size or an
+    extent past the payload is a WireFormatError, never a silent partial
+    ingest."""
+    try:
+        regions = [(str(d), int(o), int(n)) for d, o, n in header["regions"]]
+        ints = [(str(k), str(d), int(o), int(n)) for k, d, o, n in header["ints"]]
+    except (KeyError, TypeError, ValueError):
+        raise WireFormatError("malformed regions / ints lists") from None
+    if len(regions) != len(layout.groups):
+        raise WireFormatError(f"{len(regions)} regions for {len(layout.groups)} dtype groups")
+    for (dtn, off, nbytes), (dt, g) in zip(regions, layout.groups.items()):
+        if dtn != _dt_name(dt):
+            raise WireFormatError("region order does not match the layout")
+        if nbytes != g.padded * g.esize:
+            raise WireFormatError(f"region {dtn}: {nbytes} bytes, layout needs {g.padded * g.esize}")
+        if off < 0 or off % g.esize or off + nbytes > P:
+            raise WireFormatError(f"region {dtn} [{off}, {off + nbytes}) outside the {P}-byte payload")
+    want = {k: dt for k, _, dt in layout.entries if k in layout.int_keys}
+    if len(ints) != len(want) or {k for k, _, _, _ in ints} != set(want):
+        raise WireFormatError("integer side table does not list the layout's integer keys")
+    shapes = {k: s for k, s, _ in layout.entries}
+    for key, dtn, off, nb in ints:
+        if dtn not in _DTYPES or _DTYPES[dtn] != want[key]:
+            raise WireFormatError(f"integer key {key!r}: dtype {dtn}")
+        if nb != numel(shapes[key]) * torch.empty((), dtype=want[key]).element_size():
+            raise WireFormatError(f"integer key {key!r}: {nb} bytes")
+        if off < 0 or off + nb > P:
+            raise WireFormatError(f"integer key {key!r} outside the payload")
 
 
 def layout_of(header: dict) -> RowLayout:
@@ -136,8 +179,9 @@ def layout_of(header: dict) -> RowLayout:
 def decode(buf) -> Tuple[object, "OrderedDict[str, torch.Tensor]"]:
     """(sample_num, state dict).  Float keys are zero-copy views into buf (keep
     it alive); integer keys come exactly from the side table."""
-    header, base = parse_header(buf)
+    header, base, P = _parse(buf)
     lay = layout_of(header)
+    _check_regions(header, lay, P)
     regions = {r[0]: r for r in header["regions"]}
     ints = {k: (dtn, off, nb) for k, dtn, off, nb in header["ints"]}
     out = OrderedDict()
@@ -163,12 +207,11 @@ def decode(buf) -> Tuple[object, "OrderedDict[str, torch.Tensor]"]:
 def row_regions(buf, layout: RowLayout):
     """For ClientBucket.put_encoded: [(dtype, host tensor of the row image)]
     after checking that the message was encoded for exactly this layout."""
-    header, base = parse_header(buf)
-    if header["signature"] != layout.signature():
+    header, base, P = _parse(buf)
+    if header.get("signature") != layout.signature():
         raise WireFormatError("update was encoded for a different model layout")
+    _check_regions(header, layout, P)
     out = []
     for (dtn, off, nbytes), (dt, g) in zip(header["regions"], layout.groups.items()):
-        if dtn != _dt_name(dt):
-            raise WireFormatError("region order does not match the layout")
         out.append((dt, torch.frombuffer(buf, dtype=dt, count=g.length, offset=base + off) if g.length else None))
     return header["sample_num"], out

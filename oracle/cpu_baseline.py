@@ -35,11 +35,48 @@ def fedavg(raw_grad_list: List[Tuple[float, "OrderedDict[str, torch.Tensor]"]]) 
     return avg_params
 
 
+def host_cpus() -> dict:
+    """What this process may run on: os.cpu_count() (the machine), the
+    affinity mask, the cgroup CPU quota, and the CPU model.  On the GPU box
+    os.cpu_count() reports the whole machine while the job's share is
+    smaller, so `usable` = min(affinity, quota) is the thread count a fair
+    baseline uses."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = info["nproc"]
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota_cpus"] = quota
+    usable = info["affinity"]
+    if quota is not None:
+        usable = min(usable, max(1, int(quota + 0.5)))
+    info["usable"] = usable
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    info["model"] = model
+    return info
+
+
 def time_fedavg(raw_grad_list, reps: int = 5, threads: int | None = None) -> dict:
     """Median wall time of fedavg over `reps` runs after one warm-up.  Client
     0's dict is rebuilt before each run because the loop rebinds its keys."""
     if threads is None:
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpus()["usable"]
     old = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:

@@ -120,6 +120,22 @@ def wsum(tensors: Sequence[torch.Tensor], ws: Sequence[float]) -> torch.Tensor:
     raise TypeError(f"oracle: unsupported dtype {dt}")
 
 
+def wsum_acc32(tensors: Sequence[torch.Tensor], ws: Sequence[float]) -> torch.Tensor:
+    """fedml_amd's `fedagg_low_precision_acc="fp32"` mode for bf16/f16 keys
+    (not a reference behaviour; the definition its kernels are checked
+    against): acc = fl32(x_0 * fl32(w_0)); acc = fl32(acc + fl32(x_i * fl32(w_i)))
+    in fp32, one RNE to the key's dtype at the end."""
+    dt = tensors[0].dtype
+    conv = bf16_bits_to_f32 if dt == torch.bfloat16 else (lambda a: a.astype(np.float32))
+    w32 = [np.float32(w) for w in ws]
+    acc = conv(to_np(tensors[0])) * w32[0]
+    for t, w in zip(tensors[1:], w32[1:]):
+        acc = acc + conv(to_np(t)) * w
+    if dt == torch.bfloat16:
+        return from_np(f32_to_bf16_bits(acc), torch.bfloat16, tensors[0].shape)
+    return from_np(acc.astype(np.float16), torch.float16, tensors[0].shape)
+
+
 def seqsum(tensors: Sequence[torch.Tensor]) -> np.ndarray:
     """avg = p_0 ; avg += p_i in the source dtype (agg_operator.py:58-63)."""
     dt = tensors[0].dtype
@@ -185,6 +201,15 @@ def torch_aggregator(args, raw_grad_list, training_num):
     if opt == "SCAFFOLD":
         total_weights_delta, total_c_delta_para = raw_grad_list[0][1], raw_grad_list[0][2]
         for k in list(total_weights_delta.keys()):
+            # :110,113: at i == 0 the key is bound to client 0's own c_delta
+            # tensor, then `+=` adds every other client's into it in place
+            if K > 1:
+                c0 = total_c_delta_para[k]
+                res = seqsum([c0] + [raw_grad_list[i][2][k] for i in range(1, K)])
+                if c0.dtype == torch.bfloat16:
+                    c0.view(torch.int16).copy_(torch.from_numpy(res.view(np.int16)).reshape(c0.shape))
+                else:
+                    c0.copy_(torch.from_numpy(np.ascontiguousarray(res)).reshape(c0.shape))
             # The weighted sums of :106-115 are computed and then discarded by
             # :116-117; only the last client's tensors survive.
             _, weights_delta, c_delta_para = raw_grad_list[K - 1]

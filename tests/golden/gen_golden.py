@@ -85,6 +85,10 @@ def run_agg_case(FedMLAggOperator, spec, aggregate=None):
     sha = fingerprint(raw)
     client0_before = OrderedDict((k, t.clone()) for k, t in raw[0][1].items())
     client0_objs = dict(raw[0][1])
+    # 3-tuple optimizers (SCAFFOLD, Mime): client 0's second dict too
+    # (SCAFFOLD's `total_c_delta_para[k] += c_delta_para[k]` adds into its tensors)
+    third_before = OrderedDict((k, t.clone()) for k, t in raw[0][2].items()) if len(raw[0]) > 2 else None
+    third_objs = dict(raw[0][2]) if len(raw[0]) > 2 else None
     meta = {"spec": spec, "in_sha256": sha, "error": None}
     arrays = {}
     try:
@@ -109,6 +113,12 @@ def run_agg_case(FedMLAggOperator, spec, aggregate=None):
                                   else client0_before[k])
                and not (t.is_floating_point() and torch.isnan(t).any())]
     meta["client0_tensors_mutated"] = mutated
+    if third_objs is not None:
+        mutated2 = [k for k, t in third_objs.items() if not torch.equal(t, third_before[k])
+                    and not (t.is_floating_point() and torch.isnan(t).any())]
+        meta["client0_third_tensors_mutated"] = mutated2
+        for k in mutated2:  # the mutated tensors' values after the call
+            arrays[f"m2:{k}"] = tensor_bytes(third_objs[k])
     save(spec["name"], meta, arrays)
 
 

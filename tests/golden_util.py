@@ -83,3 +83,32 @@ def assert_groups(actual, meta, arrays, what="") -> None:
         assert list(gd.keys()) == list(ed.keys()), f"{what}: key order differs"
         for k in ed:
             assert_same(gd[k], ed[k], f"{what}[{g}][{k}]")
+
+
+def snapshot_third(raw):
+    """(tensor objects, clones) of client 0's second dict of a 3-tuple round."""
+    if len(raw[0]) < 3:
+        return None
+    objs = dict(raw[0][2])
+    return objs, {k: t.clone() for k, t in objs.items()}
+
+
+def assert_third_mutation(snap, meta, arrays, what="") -> None:
+    """SCAFFOLD's in-place `total_c_delta_para[k] += c_delta_para[k]`
+    (agg_operator.py:110,113): which of client 0's c_delta tensors the
+    reference mutated, and their values afterwards."""
+    if snap is None or "client0_third_tensors_mutated" not in meta:
+        return
+    objs, before = snap
+    want = set(meta["client0_third_tensors_mutated"])
+    names = meta["array_names"]
+    for k, t in objs.items():
+        t = t.cpu()
+        if t.is_floating_point() and torch.isnan(t).any():
+            continue
+        changed = not torch.equal(t, before[k].cpu())
+        assert changed == (k in want), f"{what}: c_delta[{k}] mutated={changed}"
+        if k in want:
+            a = arrays[f"m2:{k}"]
+            e = to_tensor(a, str(t.dtype).replace("torch.", ""), t.shape)
+            assert_same(t, e, f"{what}: c_delta[{k}] after the call")

@@ -57,13 +57,151 @@ def test_create_server_aggregator_picks_by_dataset():
     class A:
         dataset = "mnist"
 
+    from fedml_amd.server_aggregator import MI355XServerAggregatorNWP, MI355XServerAggregatorTAGPred
+
     agg = create_server_aggregator(torch.nn.Linear(2, 2), A())
-    assert type(agg) is MI355XServerAggregator and agg.test(None, None, A()) is None
+    assert type(agg) is MI355XServerAggregator
     A.dataset = "stackoverflow_nwp"
-    agg = create_server_aggregator(torch.nn.Linear(2, 2), A())
-    assert isinstance(agg, MI355XServerAggregator)
-    try:
-        agg.test(None, None, A())
-        raise AssertionError("task evaluation should raise")
-    except NotImplementedError:
-        pass
+    assert type(create_server_aggregator(torch.nn.Linear(2, 2), A())) is MI355XServerAggregatorNWP
+    A.dataset = "fed_shakespeare"
+    assert type(create_server_aggregator(torch.nn.Linear(2, 2), A())) is MI355XServerAggregatorNWP
+    A.dataset = "stackoverflow_lr"
+    assert type(create_server_aggregator(torch.nn.Linear(2, 2), A())) is MI355XServerAggregatorTAGPred
+
+
+class _EvalArgs:
+    federated_optimizer = "FedAvg"
+    dataset = "mnist"
+    round_idx = 0
+    enable_wandb = False
+
+
+def _loader(n=37, d=8, classes=3, seed=0, batch=10):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, d, generator=g)
+    y = torch.randint(0, classes, (n,), generator=g)
+    return torch.utils.data.DataLoader(torch.utils.data.TensorDataset(x, y), batch_size=batch), x, y
+
+
+def test_server_test_returns_the_reference_metrics():
+    """default_aggregator.py:25-106: test() evaluates the server model and
+    returns (acc, loss, None, None): acc = correct / total, loss = the
+    batch-mean cross entropy re-weighted by batch size, over the set."""
+    from fedml_amd.server_aggregator import MI355XServerAggregator
+
+    torch.manual_seed(1)
+    model = torch.nn.Linear(8, 3)
+    loader, x, y = _loader()
+    res = MI355XServerAggregator(model, _EvalArgs()).test(loader, torch.device("cpu"), _EvalArgs())
+    assert isinstance(res, tuple) and len(res) == 4 and res[2] is None and res[3] is None
+    with torch.no_grad():
+        pred = model(x)
+        acc = (pred.argmax(1) == y).sum().item() / len(y)
+        loss = sum(torch.nn.functional.cross_entropy(model(x[i:i + 10]), y[i:i + 10]).item() * len(y[i:i + 10])
+                   for i in range(0, len(y), 10)) / len(y)
+    assert res[0] == acc
+    assert abs(res[1] - loss) < 1e-12
+
+
+def test_server_test_tag_prediction_and_nwp():
+    """The multi-label (stackoverflow_lr) and next-word (padding id 0
+    ignored) evaluations of my_server_aggregator_prediction.py:19-60 and
+    my_server_aggregator_nwp.py:19-43."""
+    from fedml_amd.server_aggregator import create_server_aggregator
+
+    class A(_EvalArgs):
+        dataset = "stackoverflow_lr"
+
+    torch.manual_seed(2)
+    model = torch.nn.Sequential(torch.nn.Linear(6, 4), torch.nn.Sigmoid())
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(20, 6, generator=g)
+    y = (torch.rand(20, 4, generator=g) > 0.5).float()
+    loader = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(x, y), batch_size=7)
+    acc, loss, _, _ = create_server_aggregator(model, A()).test(loader, torch.device("cpu"), A())
+    with torch.no_grad():
+        p = model(x)
+        exp_acc = ((p > 0.5).int().eq(y).sum(-1) == 4).sum().item() / 20
+        exp_loss = sum(torch.nn.functional.binary_cross_entropy(model(x[i:i + 7]), y[i:i + 7], reduction="sum").item()
+                       * len(y[i:i + 7]) for i in range(0, 20, 7)) / 20
+    assert acc == exp_acc and abs(loss - exp_loss) < 1e-9
+
+    A.dataset = "stackoverflow_nwp"
+    emb = torch.nn.Sequential(torch.nn.Embedding(11, 5), torch.nn.Flatten(), torch.nn.Linear(15, 11))
+    xs = torch.randint(0, 11, (12, 3), generator=g)
+    ys = torch.randint(0, 11, (12,), generator=g)
+    ys[::3] = 0  # padding targets do not count
+    loader = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(xs, ys), batch_size=5)
+    acc, loss, _, _ = create_server_aggregator(emb, A()).test(loader, torch.device("cpu"), A())
+    with torch.no_grad():
+        pred = emb(xs).argmax(1)
+        pos = ys != 0
+        exp_acc = ((pred == ys) & pos).sum().item() / pos.sum().item()
+    assert acc == exp_acc and loss > 0
+
+
+class _RoundArgs:
+    federated_optimizer = "FedAvg"
+    dataset = "mnist"
+    enable_wandb = False
+
+    def __init__(self, K, comm_round=3, freq=2):
+        self.round_idx = 0
+        self.comm_round = comm_round
+        self.frequency_of_the_test = freq
+        self.client_num_per_round = K
+        self.client_num_in_total = K
+
+
+def test_server_manager_sequence_on_a_cpu_server():
+    """fedml_server_manager.py:174-251 replayed for three rounds (add xK ->
+    check -> aggregate -> test_on_server_for_all_clients -> assess_contribution
+    -> client_selection / data_silo_selection): no AttributeError, the
+    Context holds the round's client list (fedml_aggregator.py:86) and the
+    server metrics of the tested rounds (:193-202), the server model holds
+    the average.  The reduction here is the oracle (a CPU server has no
+    HBM); tests/test_gpu_cross_silo.py runs the same sequence on the GPU."""
+    import copy
+
+    from replay_util import replay_rounds
+
+    from fedml_amd.context import Context
+    from fedml_amd.server_aggregator import MI355XServerAggregator
+    from fedml_amd.synth import host_clients
+    from oracle import fedavg_oracle as orc
+
+    class _OracleAggregator(MI355XServerAggregator):
+        def aggregate(self, raw):
+            return orc.agg(self.args, raw)
+
+    Context.reset()
+    K = 3
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
+    args = _RoundArgs(K)
+    loader, _, _ = _loader()
+    server = FedMLAggregator(None, loader, 0, {}, {}, {}, K, torch.device("cpu"), args,
+                             _OracleAggregator(model, args))
+    assert Context().get(Context.KEY_TEST_DATA) is loader  # :35
+    entries = [(k, tuple(t.shape), t.dtype) for k, t in model.state_dict().items()]
+    expected = {}
+
+    def updates(r):
+        raw = host_clients(entries, K, seed=50 + r, round_idx=r)
+        expected[r] = orc.agg(args, copy.deepcopy(raw))
+        return raw
+
+    out = replay_rounds(server, args, [11, 12, 13], updates, rounds=3)
+    assert args.round_idx == 3
+    for o in out:
+        r = o["round_idx"]
+        assert o["ctx_model_list"] is o["model_list"] and o["idxes"] == [0, 1, 2]
+        assert o["ids"] == [11, 12, 13] and o["silos"] == [0, 1, 2]
+        for k, e in expected[r].items():
+            assert torch.equal(o["global"][k], e)
+    # rounds 0 and 2 are tested (freq 2, last round 2); round 1 is not
+    m0, m2 = out[0]["metrics"], out[2]["metrics"]
+    assert out[1]["metrics"] is m0 and len(m0) == 4 and m0[2] is None
+    assert m2 is not m0 and out[2]["metrics_last"] is m0
+    for k, e in expected[2].items():
+        assert torch.equal(model.state_dict()[k], e)

@@ -161,3 +161,56 @@ def test_int32_key_moves_key_by_key(cuda_device):
     averaged, _, _ = server.aggregate()
     for k in exp:
         gu.assert_same(averaged[k].cpu(), exp[k], k)
+
+
+class _RoundArgs(_Args):
+    dataset = "mnist"
+    enable_wandb = False
+
+    def __init__(self, K, comm_round=2, freq=1):
+        self.round_idx = 0
+        self.comm_round = comm_round
+        self.frequency_of_the_test = freq
+        self.client_num_per_round = K
+        self.client_num_in_total = K
+
+
+@pytest.mark.parametrize("K", [2, 5])
+def test_server_manager_sequence(K, cuda_device):
+    """The class swap of INTEGRATION.md §3 inside FedML's real round loop
+    (fedml_server_manager.py:174-251, replayed by tests/replay_util.py) for
+    two rounds: add xK -> check -> aggregate -> test_on_server_for_all_clients
+    -> assess_contribution -> client_selection.  No AttributeError; every
+    round's average is bit-exact vs the oracle; the Context holds the round's
+    model list and the GPU-evaluated server metrics (acc, loss, None, None)."""
+    from replay_util import replay_rounds
+
+    from fedml_amd.context import Context
+
+    Context.reset()
+    model = _model().to(cuda_device)
+    args = _RoundArgs(K)
+    g = torch.Generator().manual_seed(5)
+    test_set = torch.utils.data.TensorDataset(torch.randn(40, 37, generator=g), torch.randint(0, 3, (40,), generator=g))
+    loader = torch.utils.data.DataLoader(test_set, batch_size=16)
+    server = FedMLAggregator(None, loader, 0, {}, {}, {}, K, cuda_device, args, MI355XServerAggregator(model, args))
+    expected = {}
+
+    def updates(r):
+        raw = _round(model, K, seed=70 + r, round_idx=r)
+        expected[r] = orc.agg(_Args(), copy.deepcopy(raw))
+        return raw
+
+    out = replay_rounds(server, args, list(range(1, K + 1)), updates, rounds=2)
+    for o in out:
+        for k, e in expected[o["round_idx"]].items():
+            gu.assert_same(o["global"][k].cpu(), e, f"round {o['round_idx']} {k}")
+        assert o["ctx_model_list"] is o["model_list"]
+        acc, loss, a, b = o["metrics"]
+        assert a is None and b is None and 0.0 <= acc <= 1.0 and loss > 0
+    assert out[1]["metrics_last"] == out[0]["metrics"]
+    # round 1's metrics are those of the model holding round 1's average
+    with torch.no_grad():
+        x, y = test_set.tensors
+        pred = model(x.to(cuda_device)).argmax(1).cpu()
+    assert out[1]["metrics"][0] == (pred == y).sum().item() / len(y)

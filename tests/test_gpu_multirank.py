@@ -87,3 +87,77 @@ def test_two_ranks_one_gpu(cuda_device):
         full, (lo, hi, ps) = res[r]
         assert np.array_equal(full.view(np.uint32), (p0 + p1).view(np.uint32))  # one rounding per element
         assert np.array_equal(ps.view(np.uint32), chain[lo:hi].view(np.uint32))  # param axis: bit-exact
+
+
+def _rccl_worker(port, L, q):
+    """One rank, RCCL backend: ClientAxisAggregator with the process group
+    handed in takes the collective path (comm stream, async
+    reduce_scatter_tensor, work.wait(), stream join) and all_gather."""
+    try:
+        import torch.distributed as dist
+
+        from fedml_amd.sharded import ClientAxisAggregator, ShardedFedOpt
+        from oracle import fedavg_oracle as orc
+
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+        group = dist.group.WORLD
+        calls = {"rs": 0, "ag": 0}
+        rs, ag = dist.reduce_scatter_tensor, dist.all_gather
+
+        def count_rs(*a, **k):
+            calls["rs"] += 1
+            return rs(*a, **k)
+
+        def count_ag(*a, **k):
+            calls["ag"] += 1
+            return ag(*a, **k)
+
+        dist.reduce_scatter_tensor, dist.all_gather = count_rs, count_ag
+        K = 7
+        host = _rows(K, L)
+        ws = [(i + 1.0) / 28.0 for i in range(K)]
+        chain = orc.wsum([host[i] for i in range(K)], ws).numpy()
+        rows = torch.zeros(K, (L + 63) // 64 * 64, device=dev)
+        rows[:, :L] = host.to(dev)
+        out = {}
+        for chunks in (1, 3, 8):
+            agg = ClientAxisAggregator(rows, L, group=group, chunks=chunks)
+            assert agg.collective and agg.comm_stream is not None and not agg.host_staged
+            before = calls["rs"]
+            agg.aggregate(ws)
+            out[chunks] = agg.gather_full().cpu().numpy()
+            assert calls["rs"] - before == len(agg.bounds)
+        # the sharded FedOpt on the same group (step after the exchange)
+        sh = ShardedFedOpt(rows, L, torch.zeros(L, device=dev), "sgd", 1.0, 0.9, group=group, chunks=3)
+        sh.aggregate(ws)
+        p1 = sh.gather_params().cpu().numpy()
+        torch.cuda.synchronize()
+        backend = dist.get_backend()
+        dist.destroy_process_group()
+        q.put((out, chain, p1, calls, backend, None))
+    except Exception:  # pragma: no cover
+        q.put((None, None, None, None, None, traceback.format_exc()))
+
+
+def test_rccl_branch_one_rank(cuda_device):
+    """The RCCL (NCCL backend) path of the client-axis mode, executed: a
+    one-rank process group on the box's GPU.  Results are bit-exact with the
+    single chain for 1, 3 and 8 chunks (one rank: the reduce-scatter is the
+    identity), and the first SGD step (lr 1, fresh momentum) returns the
+    average itself."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    L = 300_007
+    p = ctx.Process(target=_rccl_worker, args=(_port(), L, q))
+    p.start()
+    out, chain, p1, calls, backend, err = q.get(timeout=300)
+    p.join(timeout=60)
+    assert err is None, err
+    assert backend == "nccl"
+    assert calls["rs"] >= 1 + 3 + 8 and calls["ag"] >= 4
+    for chunks, full in out.items():
+        assert np.array_equal(full.view(np.uint32), chain.view(np.uint32)), chunks
+    # SGD lr=1, first step: p_new = fl(p_old - fl(p_old - avg)) with p_old = 0 -> avg
+    assert np.array_equal(p1.view(np.uint32), chain.view(np.uint32))

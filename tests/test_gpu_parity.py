@@ -52,8 +52,10 @@ def test_host_inputs_match_reference(name, cuda_device):
             ao.FedMLAggOperator.agg(cases.Args(spec), raw)
         assert type(ei.value).__name__ == meta["error"]
         return
+    third = gu.snapshot_third(raw)
     res = ao.FedMLAggOperator.agg(cases.Args(spec), raw)
     gu.assert_groups(res, meta, arrays, name)
+    gu.assert_third_mutation(third, meta, arrays, name)
     first = res[0] if isinstance(res, tuple) else res
     assert (first is client0) == meta["result_is_client0_dict"]
     for o in meta["outputs"]:
@@ -78,11 +80,13 @@ def test_device_inputs_match_reference(name, cuda_device):
             ao.FedMLAggOperator.agg(cases.Args(spec), raw)
         assert type(ei.value).__name__ == meta["error"]
         return
+    third = gu.snapshot_third(raw)
     res = ao.FedMLAggOperator.agg(cases.Args(spec), raw)
     first = res[0] if isinstance(res, tuple) else res
     for t in first.values():
         assert t.is_cuda
     gu.assert_groups(_cpu(res), meta, arrays, name)
+    gu.assert_third_mutation(third, meta, arrays, name)
 
 
 @pytest.mark.parametrize("name", [c["name"] for c in cases.CASES
@@ -512,3 +516,22 @@ def test_tight_tensors_every_tile_config(K, N, cuda_device):
         kn.wsum_tensors(group, w, out)
         exp = orc.wsum([t.cpu() for t in group], w)
         gu.assert_same(out.cpu(), exp, f"K={K} N={N}")
+
+
+def test_put_interleaved_host_and_device_keys(cuda_device):
+    """One dtype group holding host AND device keys in alternation: the host
+    keys' staged H2D must not overwrite the device keys copied D2D between
+    them (each stretch of host keys is its own copy).  Two rounds on the same
+    slots, so stale staging bytes would show."""
+    K = 3
+    entries = [(f"k{j}", (n,), torch.float32) for j, n in enumerate([5, 70, 1, 64, 4099, 3, 129, 2])]
+    bucket = ClientBucket(entries, K, cuda_device)
+    for r in range(2):
+        raw = host_clients(entries, K, seed=90 + r)
+        exp = orc.agg(type("A", (), {"federated_optimizer": "FedAvg"})(), copy.deepcopy(raw))
+        for i, (n, d) in enumerate(raw):
+            mixed = OrderedDict((k, t.to(cuda_device) if (j + i + r) % 2 else t) for j, (k, t) in enumerate(d.items()))
+            bucket.put(i, mixed, n)
+        res = bucket.aggregate()
+        for k, e in exp.items():
+            gu.assert_same(res[k].cpu(), e, f"round {r} {k}")

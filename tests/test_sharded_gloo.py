@@ -11,6 +11,7 @@ import multiprocessing as mp
 import os
 import socket
 import traceback
+from collections import OrderedDict
 
 import numpy as np
 import pytest
@@ -194,3 +195,118 @@ def test_sharded_fedopt(world, K_local, L, chunks):
         for rank, out, _ in res:
             np.testing.assert_array_equal(out[r][0], res[0][1][r][0])  # every rank gathers the same average
             np.testing.assert_array_equal(out[r][1], p.numpy())
+
+
+def _bn_rounds(spec_name):
+    """The reference's own FedOpt rounds on its BatchNorm model (fixture
+    fedopt_sgd_m09_*): per round, the clients' flat fp32 rows (integer
+    counters promoted, as the bucket stores them) built from the fixture's
+    global model of the previous round, and the fixture's result."""
+    import cases
+    import golden_util as gu
+
+    from fedml_amd.layout import RowLayout
+
+    spec = next(c for c in cases.FEDOPT_CASES if c["name"] == spec_name)
+    meta, arrays = gu.load(spec_name)
+    init = cases.fedopt_global_init(spec)
+    lay = RowLayout(cases._entries(cases.FEDOPT_MODEL))
+    g = lay.groups[torch.float32]
+
+    def flat(sd):
+        out = torch.zeros(g.length, dtype=torch.float32)
+        for k, o, n in zip(g.keys, g.offsets, g.numels):
+            out[o:o + n] = sd[k].reshape(-1).to(torch.float32)
+        return out
+
+    def fixture(tag):
+        return OrderedDict((k, gu.to_tensor(arrays[f"{tag}:{k}"], str(t.dtype).replace("torch.", ""), t.shape))
+                           for k, t in init.items())
+
+    gsd = fixture("init")
+    rounds = []
+    for r in range(spec["rounds"]):
+        raw = cases.fedopt_round_inputs(spec, gsd, r)
+        rows = torch.stack([flat(d) for _, d in raw])
+        ns = [n for n, _ in raw]
+        exp = fixture(f"r{r}")
+        rounds.append((rows, ns, exp))
+        gsd = exp
+    return spec, lay, flat(fixture("init")), rounds
+
+
+def _bn_worker(rank, world, port, spec_name, chunks, q):
+    try:
+        from fedml_amd.sharded import ShardedFedOpt, buffer_ranges
+
+        import cases
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        spec, lay, g0, rounds = _bn_rounds(spec_name)
+        K = spec["K"]
+        per = (K + world - 1) // world
+        mine = list(range(rank * per, min(K, (rank + 1) * per)))
+        L = lay.groups[torch.float32].length
+        srv = ShardedFedOpt(torch.zeros(len(mine), L), L, g0, "sgd", lr=spec["lr"], momentum=spec["momentum"],
+                            chunks=chunks, reducer=_oracle_reducer,
+                            stepper=_sgd_stepper(spec["lr"], spec["momentum"]),
+                            buffers=buffer_ranges(lay, cases.FEDOPT_PARAMS))
+        out = []
+        for rows, ns, _ in rounds:
+            srv.agg.rows = rows[mine].clone()
+            ws = [n / sum(ns) for n in ns]
+            srv.aggregate([ws[i] for i in mine])
+            out.append((srv.agg.gather_full().numpy().copy(), srv.gather_params().numpy().copy()))
+        q.put((rank, out, None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("spec_name", ["fedopt_sgd_m09_lr1", "fedopt_sgd_m09_lr1e-3"])
+def test_sharded_fedopt_steps_parameters_only(world, spec_name):
+    """Multi-GPU FedOpt on the reference's BatchNorm model: only named
+    parameters take the SGD(momentum 0.9) step; running stats and the
+    promoted num_batches_tracked take the plain average
+    (FedOptAggregator.py:118-130).  On one rank the chain order is the
+    reference's, so every round equals the reference's fixture bit for bit;
+    on 2 and 3 ranks the average's addition order changes, so buffers equal
+    the gathered average exactly and parameters stay within a few fp32 ulps
+    of the fixture across the three rounds (state carried)."""
+    import cases
+    import golden_util as gu
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bn_worker, args=(r, world, port, spec_name, 3, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [err for _, _, err in res if err]
+    assert not errs, "\n".join(errs)
+    spec, lay, _, rounds = _bn_rounds(spec_name)
+    g = lay.groups[torch.float32]
+    params = set(cases.FEDOPT_PARAMS)
+    for r, (_, _, exp) in enumerate(rounds):
+        avg, got = res[0][1][r]
+        for rank, out, _ in res:
+            np.testing.assert_array_equal(out[r][1], got)  # every rank gathers the same model
+        for k, o, n in zip(g.keys, g.offsets, g.numels):
+            e = exp[k]
+            v = torch.from_numpy(got[o:o + n].copy()).reshape(e.shape)
+            if k not in params:  # a buffer: exactly the average, never stepped
+                np.testing.assert_array_equal(got[o:o + n], avg[o:o + n])
+            if e.dtype == torch.int64:
+                v = v.to(torch.int64)  # load_state_dict's truncating copy_
+            if world == 1:
+                gu.assert_same(v, e, f"{spec_name} round {r} {k}")
+            elif e.dtype == torch.int64:
+                assert torch.equal(v, e), k
+            else:
+                tol = 64 * 2.0 ** -24 * (e.abs() + 1e-3)
+                assert torch.all((v - e).abs() <= tol), (k, r, (v - e).abs().max())

@@ -68,3 +68,47 @@ def test_no_pickle_in_messages():
     d = OrderedDict(w=torch.randn(10))
     msg = wire.encode(d, 1)
     assert bytes(msg[:2]) != b"\x80\x04" and msg[:4] == b"FAGG"  # not a pickle
+
+
+def _with_header(msg, edit):
+    """msg with its JSON header edited in place (same header length)."""
+    import json
+
+    hdr, base = wire.parse_header(msg)
+    edit(hdr)
+    hb = json.dumps(hdr, separators=(",", ":")).encode()
+    assert len(hb) <= base - 64
+    out = bytearray(msg)
+    out[64:base] = hb + b" " * (base - 64 - len(hb))
+    return out
+
+
+@pytest.mark.parametrize("edit", [
+    lambda h: h["regions"].pop(),                                   # a dtype group missing
+    lambda h: h["regions"][0].__setitem__(2, h["regions"][0][2] - 64),  # short region
+    lambda h: h["regions"][0].__setitem__(1, 1 << 30),             # past the payload
+    lambda h: h["regions"][0].__setitem__(1, -64),                 # negative offset
+    lambda h: h["ints"].pop(),                                      # integer key missing
+    lambda h: h["ints"][0].__setitem__(3, 1),                      # wrong side-table size
+    lambda h: h["ints"][0].__setitem__(2, 1 << 30),                # side table past the payload
+    lambda h: h.__setitem__("regions", "x"),                        # not a list of triples
+])
+def test_rejects_malformed_headers(edit):
+    """Headers from the network are checked against the layout and the
+    payload length before any ingest: a short regions list used to leave a
+    dtype group's row holding the previous round's bytes (zip truncation)."""
+    d = OrderedDict(a=torch.ones(5), h=torch.ones(3, dtype=torch.bfloat16), n=torch.tensor(3))
+    msg = wire.encode(d, 7)
+    bad = _with_header(msg, edit)
+    with pytest.raises(wire.WireFormatError):
+        wire.decode(bad)
+    with pytest.raises(wire.WireFormatError):
+        wire.row_regions(bad, RowLayout(d))
+    wire.row_regions(msg, RowLayout(d))  # the unedited message passes
+
+
+def test_rejects_non_json_header():
+    msg = bytearray(wire.encode(OrderedDict(a=torch.ones(5)), 1))
+    msg[64:68] = b"\xff\xfe{["
+    with pytest.raises(wire.WireFormatError):
+        wire.decode(msg)
