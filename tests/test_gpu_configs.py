@@ -63,8 +63,10 @@ def _sample_columns(bucket, n_random: int = 200_000) -> torch.Tensor:
     counts = np.asarray(g.numels, dtype=np.int64)
     for o, n in zip(starts, counts):
         ends += [o, o + n - 2, o + n - 1]
-    which = rng.integers(0, len(starts), n_random)
-    rand = starts[which] + (rng.random(n_random) * counts[which]).astype(np.int64)
+    cum = np.cumsum(counts)
+    flat = rng.choice(int(cum[-1]), n_random, replace=False)  # uniform over the model's elements
+    which = np.searchsorted(cum, flat, side="right")
+    rand = starts[which] + flat - (cum[which] - counts[which])
     return torch.from_numpy(np.unique(np.concatenate([rand, np.asarray(ends, dtype=np.int64)])))
 
 
