@@ -1020,100 +1020,215 @@ __device__ __forceinline__ void pairwise_sort(T (&v)[N]) {
   net_apply<N, T>(v, std::make_integer_sequence<int, PairwiseNet<N>::M>{});
 }
 
-// Element types of the median kernels.  bf16 / f16 columns are widened to
-// fp32 exactly, selected there, and the selected value narrowed back exactly
-// (it is one of the inputs), so the network is the same for all three.
+// Element types of the median kernels.  Every column value becomes an fp32
+// "selection value" whose float order is the element's order, the networks
+// select on those, and the selected value maps back to the input's bits
+// exactly (it is one of the inputs).  fp32 and bf16 widen exactly (bf16 is
+// the top half of an fp32).  f16 maps to an order-preserving 16-bit key
+// placed in the mantissa of [1, 2): x ^ 0x8000 for positive, ~x for negative
+// values, so -inf < -finite < -0 < +0 < +finite < +inf as keys, all normal
+// floats, and the ±inf pads stay below / above every key.  (Widening f16 to
+// fp32 with v_cvt kept both forms live and took the K = 128 kernel to 256
+// VGPRs, occupancy 1.)  nan() tests a selection value for NaN.
 struct MedF32 {
   using S = float;
   static __device__ __forceinline__ float widen(S x) { return x; }
   static __device__ __forceinline__ S narrow(float v) { return v; }
+  static __device__ __forceinline__ bool nan(float v) { return __builtin_isnan(v); }
+  static __device__ __forceinline__ bool raw_nan(S x) { return __builtin_isnan(x); }
+  static constexpr bool kReloadNan = false;
+  // running "any NaN so far" over the column's selection values
+  using NanAcc = bool;
+  static __device__ __forceinline__ void nan_add(NanAcc& a, float v) { a |= __builtin_isnan(v); }
+  static __device__ __forceinline__ bool nan_any(NanAcc a) { return a; }
   static constexpr uint32_t kNegInf = 0xff800000u, kPosInf = 0x7f800000u;
 };
-struct MedBF16 {
+struct IsNanAcc {
+  using NanAcc = bool;
+  static __device__ __forceinline__ void nan_add(NanAcc& a, float v) { a |= __builtin_isnan(v); }
+  static __device__ __forceinline__ bool nan_any(NanAcc a) { return a; }
+};
+struct MedBF16 : IsNanAcc {
   using S = uint16_t;
+  static __device__ __forceinline__ bool raw_nan(S x) { return (x & 0x7fffu) > 0x7f80u; }
+  static constexpr bool kReloadNan = true;
   static __device__ __forceinline__ float widen(S x) { return __uint_as_float(uint32_t(x) << 16); }
   static __device__ __forceinline__ S narrow(float v) { return S(__float_as_uint(v) >> 16); }
+  static __device__ __forceinline__ bool nan(float v) { return __builtin_isnan(v); }
   static constexpr uint32_t kNegInf = 0xff80u, kPosInf = 0x7f80u;
 };
 struct MedF16 {
   using S = uint16_t;
+  static __device__ __forceinline__ bool raw_nan(S x) { return (x & 0x7fffu) > 0x7c00u; }
+  static constexpr bool kReloadNan = true;
+  // The value arrives in the high half (as bf16 does: a d16_hi load), its
+  // order key is built there (x ^ 0x8000 for positive, ~x for negative values)
+  // and shifted down two bits: a positive float below 2.0 whose float order
+  // is the key order (normal for every non-NaN key: -inf's key 0x03ff gives
+  // 0x00ffc000).
   static __device__ __forceinline__ float widen(S x) {
-    _Float16 h;
-    __builtin_memcpy(&h, &x, 2);
-    return float(h);
+    const uint32_t u = uint32_t(x) << 16;
+    const uint32_t neg = uint32_t(int32_t(u) >> 31);
+    return __uint_as_float((u ^ (0x80000000u | (neg & 0x7fff0000u))) >> 2);
   }
   static __device__ __forceinline__ S narrow(float v) {
-    const _Float16 h = _Float16(v);
-    S x;
-    __builtin_memcpy(&x, &h, 2);
-    return x;
+    const uint32_t k = (__float_as_uint(v) << 2) >> 16;  // the 16-bit key
+    const uint32_t neg = ~uint32_t(int32_t(k << 16) >> 31);  // key below 0x8000: a negative value
+    return S(k ^ ((neg & 0x7fffu) | 0x8000u));
   }
+  static __device__ __forceinline__ uint32_t key(float v) { return (__float_as_uint(v) << 2) >> 16; }
+  // NaN keys: +NaN 0x7c01..0x7fff -> 0xfc01..0xffff, -NaN 0xfc01..0xffff -> 0x0000..0x03fe
+  static __device__ __forceinline__ bool nan(float v) {
+    const uint32_t k = key(v);
+    return __float_as_uint(v) < 0x40000000u && (k > 0xfc00u || k < 0x03ffu);
+  }
+  // rotated key (k - 0x3ff) mod 2^16: NaN keys land above 0xf801, every other
+  // key at or below it, so one unsigned compare per value
+  using NanAcc = bool;
+  static __device__ __forceinline__ void nan_add(NanAcc& a, float v) { a |= ((key(v) - 0x3ffu) & 0xffffu) > 0xf801u; }
+  static __device__ __forceinline__ bool nan_any(NanAcc a) { return a; }
   static constexpr uint32_t kNegInf = 0xfc00u, kPosInf = 0x7c00u;
 };
 
-template <int KMAX, bool FULL, int BS, bool PRIO = false, class E = MedF32>
+// -inf / +inf in each element type: what a padded slot's load returns
+template <class E>
+__device__ typename E::S g_median_pad[2] = {__builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
+                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kNegInf)),
+                                            __builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
+                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kPosInf))};
+
+// Row base of client row p for a launch starting at column col0 (> 0 only
+// past 2^30 columns): an opaque SGPR pair, so the loads keep the
+// SGPR-base + 32-bit VGPR-offset form (left visible, the compiler folds col0
+// into a per-lane 64-bit address: 2.2x slower at K = 128).
+template <class T>
+__device__ __forceinline__ const char __attribute__((address_space(1)))* row_base(const T* p, int64_t col0) {
+  uint64_t b = reinterpret_cast<uint64_t>(p) + uint64_t(col0) * sizeof(T);
+  asm("" : "+s"(b));
+  return reinterpret_cast<const char __attribute__((address_space(1)))*>(b);
+}
+
+// Columns [col0, col0 + N) of the rows; out points at column col0's slot.
+// Launches cover at most 2^30 columns (kMedianChunk) so that a lane's byte
+// offset from the (wave-uniform) row base + col0 fits in 32 bits.
+template <int KMAX, bool FULL, int BS, bool PRIO = false, class E = MedF32, bool OFF = false>
 __global__ __launch_bounds__(BS) void median_kernel(const typename E::S* const* __restrict__ src, int K, int64_t N,
-                                                    typename E::S* __restrict__ out) {
+                                                    typename E::S* __restrict__ out, int64_t col0 = 0) {
   const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;
+  if constexpr (FULL) K = KMAX;  // K == KMAX: no padding, no per-client conditions
+  const int below = (KMAX - 1) / 2 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
+  // K < KMAX: the KMAX slot pointers (pads point at a ±inf constant) staged
+  // in LDS once per block.  Read per slot at a wave-uniform address and moved
+  // to SGPRs, they keep the loads in the SGPR-base form and batched; reading
+  // src[min(c, K - 1)] instead issued one s_load per client and waited for
+  // each (2.3x the K == KMAX time at K = 100).
+  __shared__ const typename E::S* tab[FULL ? 1 : KMAX];
+  if constexpr (!FULL) {
+    for (int i = threadIdx.x; i < KMAX; i += BS) tab[i] = i < K ? src[i] : &g_median_pad<E>[i - K < below ? 0 : 1];
+    __syncthreads();
+  }
   if (e >= N) return;
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // issue this wave's loads ahead of others' sorting
-  if constexpr (FULL) K = KMAX;  // K == KMAX: no padding, no per-client conditions
   // The host guarantees N * 4 < 2^32: a 32-bit byte offset on each
   // wave-uniform row base lets every load use the SGPR-base + VGPR-offset
   // form, with no per-client 64-bit address arithmetic on the VALU.
   const uint32_t boff = uint32_t(e) * uint32_t(sizeof(typename E::S));
-  const int below = (KMAX - 1) / 2 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
   float v[KMAX];
-  bool has_nan = false;
+  typename E::NanAcc nacc{};
 #pragma unroll
   for (int c = 0; c < KMAX; ++c) {
     // Keep at most 16 row pointers live in SGPRs: without the barrier the
     // scheduler hoists all K pointer loads to the top and spills them.
     if (c % 16 == 0 && c) __builtin_amdgcn_sched_barrier(0);
-    // Padded slots (c >= K) load client K-1's element again (a cache hit on
-    // the line just requested) and select the pad value: no branches, so the
-    // pointer loads batch and nothing spills.
-    const int ci = (FULL || c < K) ? c : K - 1;
-    const auto row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
-    const float x = E::widen(__builtin_nontemporal_load(
-        reinterpret_cast<const typename E::S __attribute__((address_space(1)))*>(row + boff)));
-    // torch returns the first NaN of the column (client order) if there is
-    // one.  The common case pays one compare per client (on x itself, which
-    // also keeps CodeGenPrepare from turning the select below into a branch
-    // around a single-use load).
-    has_nan |= __builtin_isnan(x);
-    if constexpr (FULL)
-      v[c] = x;
+    // A padded slot (c >= K) reads a ±inf constant: its row pointer is the
+    // pad and its lane offset is 0, so the load itself yields the pad.
+    // Nothing per slot waits for a load here: all KMAX loads are in flight
+    // before the first value is used.
+    const bool live = FULL || c < K;
+    const typename E::S* p;
+    if constexpr (FULL) {
+      p = src[c];
+    } else {
+      // readfirstlane returns int: go through uint32_t, or a low word with
+      // its top bit set sign-extends over the high word
+      const uint64_t t = reinterpret_cast<uint64_t>(tab[c]);
+      const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(t >> 32))));
+      const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(t))));
+      p = reinterpret_cast<const typename E::S*>((uint64_t(hi) << 32) | uint64_t(lo));
+    }
+    const char __attribute__((address_space(1)))* row;
+    if constexpr (OFF)
+      row = live ? row_base(p, col0) : reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(p));
     else
-      v[c] = (c < K) ? x : ((c - K < below) ? -__builtin_huge_valf() : __builtin_huge_valf());
+      row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(p));
+    v[c] = E::widen(__builtin_nontemporal_load(
+        reinterpret_cast<const typename E::S __attribute__((address_space(1)))*>(row + (live ? boff : 0u))));
+    if constexpr (sizeof(typename E::S) == 2) E::nan_add(nacc, v[c]);
+  }
+  // torch returns the first NaN of the column (client order) if there is
+  // one; the common case pays one test per client.  fp32 tests after every
+  // load is in flight (testing inside the load loop waited for each pair of
+  // loads); 16-bit rows test as they widen (with all loads in flight first,
+  // the raw and widened values are both live: 259 VGPRs; this kernel is
+  // their unaligned-row path, the packed kernel takes aligned rows).
+  // Pads are ±inf, never NaN.
+  if constexpr (sizeof(typename E::S) == 4) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < KMAX; ++c) E::nan_add(nacc, v[c]);
   }
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-  // The search runs only in waves holding a NaN column (skipped on an empty
-  // exec mask otherwise).
-  float nan_v = 0.f;
+  // Only a lane holding a NaN column searches.  fp32 tests the registers (one
+  // unordered compare); for 16-bit rows that search got speculated above the
+  // branch and kept both the loaded and the widened values live (259-267
+  // VGPRs), so they re-read the column in client order (cache hits).
+  typename E::S nan_raw{};
+  const bool has_nan = E::nan_any(nacc);
   if (has_nan) {
-    bool found = false;
+    if constexpr (E::kReloadNan) {
+#pragma unroll 1
+      for (int c = 0; c < K; ++c) {
+        const auto row = row_base(src[c], col0);
+        const typename E::S r = *reinterpret_cast<const typename E::S __attribute__((address_space(1)))*>(row + boff);
+        if (E::raw_nan(r)) {
+          nan_raw = r;
+          break;
+        }
+      }
+    } else {
+      float nan_v = 0.f;
+      bool found = false;
 #pragma unroll
-    for (int c = 0; c < KMAX; ++c) {
-      const bool n = (FULL || c < K) && !found && __builtin_isnan(v[c]);
-      nan_v = n ? v[c] : nan_v;
-      found = found || n;
+      for (int c = 0; c < KMAX; ++c) {
+        const bool n = (FULL || c < K) && !found && E::nan(v[c]);
+        nan_v = n ? v[c] : nan_v;
+        found = found || n;
+      }
+      nan_raw = E::narrow(nan_v);
     }
   }
   pairwise_sort<KMAX>(v);
-  out[e] = E::narrow(has_nan ? nan_v : v[(KMAX - 1) / 2]);
+  out[e] = has_nan ? nan_raw : E::narrow(v[(KMAX - 1) / 2]);
 }
+
+constexpr int64_t kMedianChunk = int64_t(1) << 30;  // columns per launch of the 32-bit-offset kernels
 
 template <int KMAX, class E = MedF32>
 int launch_median(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
   constexpr int BS = 64;  // 3 % faster than 256 at config 3 (tools/median_probe.py, two boxes)
-  const int64_t grid = (N + BS - 1) / BS;
-  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
-  if (K == KMAX)
-    hipLaunchKernelGGL((median_kernel<KMAX, true, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
-  else
-    hipLaunchKernelGGL((median_kernel<KMAX, false, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
-                       out);
+  for (int64_t c0 = 0; c0 < N; c0 += kMedianChunk) {
+    const int64_t n = N - c0 < kMedianChunk ? N - c0 : kMedianChunk;
+    const int64_t grid = (n + BS - 1) / BS;
+    if (K == KMAX && c0 == 0)
+      hipLaunchKernelGGL((median_kernel<KMAX, true, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
+                         out, c0);
+    else if (c0 == 0)
+      hipLaunchKernelGGL((median_kernel<KMAX, false, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
+                         out, c0);
+    else  // past 2^30 columns: the padded kernel (correct for K == KMAX too) with the row offset
+      hipLaunchKernelGGL((median_kernel<KMAX, false, BS, false, E, true>), dim3(unsigned(grid)), dim3(BS), 0, st, src,
+                         K, n, out + c0, c0);
+  }
   return check_launch("fedagg_median");
 }
 
@@ -1135,9 +1250,9 @@ __device__ __forceinline__ uint32_t pk16_bits(short2_t k) {
   return __builtin_bit_cast(uint32_t, k ^ ((k >> short(15)) & short(0x7fff)));
 }
 
-template <int KMAX, bool FULL, class E, bool TAIL>
+template <int KMAX, bool FULL, class E, bool TAIL, bool OFF>
 __device__ __forceinline__ void median_pk16_pair(const uint16_t* const* __restrict__ src, int K, int64_t e,
-                                                 uint16_t* __restrict__ out) {
+                                                 uint16_t* __restrict__ out, int64_t col0) {
   if constexpr (FULL) K = KMAX;
   const uint32_t boff = uint32_t(e) * 4u;
   const int below = (KMAX - 1) / 2 - (K - 1) / 2;
@@ -1147,14 +1262,22 @@ __device__ __forceinline__ void median_pk16_pair(const uint16_t* const* __restri
   for (int c = 0; c < KMAX; ++c) {
     if (c % 16 == 0 && c) __builtin_amdgcn_sched_barrier(0);
     const int ci = (FULL || c < K) ? c : K - 1;
-    const auto row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
+    const char __attribute__((address_space(1)))* row;
+    if constexpr (OFF)
+      row = row_base(src[ci], col0);
+    else
+      row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
     uint32_t x;
     if constexpr (!TAIL)
       x = __builtin_nontemporal_load(reinterpret_cast<const uint32_t __attribute__((address_space(1)))*>(row + boff));
     else  // the odd last column alone, duplicated into both halves
       x = *reinterpret_cast<const uint16_t __attribute__((address_space(1)))*>(row + boff) * 0x10001u;
     raw[c] = x;
-    const uint32_t mag = x & 0x7fff7fffu;
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test (see median_kernel)
+#pragma unroll
+  for (int c = 0; c < KMAX; ++c) {
+    const uint32_t mag = raw[c] & 0x7fff7fffu;
     nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
                                                                      __builtin_bit_cast(ushort2_t, mag)));
   }
@@ -1164,9 +1287,12 @@ __device__ __forceinline__ void median_pk16_pair(const uint16_t* const* __restri
     bool f_lo = false, f_hi = false;
 #pragma unroll
     for (int c = 0; c < KMAX; ++c) {
-      if (!FULL && c >= K) break;
+      // predicated, not `break`: a data-dependent exit stops the full unroll
+      // and puts raw[] in scratch (272-528 B/lane before)
+      const bool live = FULL || c < K;
       const uint32_t x = raw[c];
-      const bool n_lo = !f_lo && (x & 0x7fffu) > E::kPosInf, n_hi = !f_hi && ((x >> 16) & 0x7fffu) > E::kPosInf;
+      const bool n_lo = live && !f_lo && (x & 0x7fffu) > E::kPosInf;
+      const bool n_hi = live && !f_hi && ((x >> 16) & 0x7fffu) > E::kPosInf;
       if (n_lo) nan_bits = (nan_bits & 0xffff0000u) | (x & 0xffffu);
       if (n_hi) nan_bits = (nan_bits & 0xffffu) | (x & 0xffff0000u);
       f_lo = f_lo || n_lo;
@@ -1191,29 +1317,35 @@ __device__ __forceinline__ void median_pk16_pair(const uint16_t* const* __restri
     out[2 * e] = uint16_t(m);
 }
 
-template <int KMAX, bool FULL, class E, int BS = 256>
+template <int KMAX, bool FULL, class E, int BS = 256, bool OFF = false>
 __global__ __launch_bounds__(BS) void median_pk16_kernel(const uint16_t* const* __restrict__ src, int K, int64_t N,
-                                                         uint16_t* __restrict__ out) {
+                                                         uint16_t* __restrict__ out, int64_t col0) {
   static_assert(sizeof(typename E::S) == 2, "16-bit rows");
   const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;  // column pair
   const int64_t pairs = (N + 1) / 2;
   if (e >= pairs) return;
   if ((N & 1) && e == pairs - 1)
-    median_pk16_pair<KMAX, FULL, E, true>(src, K, e, out);
+    median_pk16_pair<KMAX, FULL, E, true, OFF>(src, K, e, out, col0);
   else
-    median_pk16_pair<KMAX, FULL, E, false>(src, K, e, out);
+    median_pk16_pair<KMAX, FULL, E, false, OFF>(src, K, e, out, col0);
 }
 
 template <int KMAX, class E>
 int launch_median_pk16(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
   constexpr int BS = 64;
-  const int64_t grid = ((N + 1) / 2 + BS - 1) / BS;
-  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
-  if (K == KMAX)
-    hipLaunchKernelGGL((median_pk16_kernel<KMAX, true, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N, out);
-  else
-    hipLaunchKernelGGL((median_pk16_kernel<KMAX, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
-                       out);
+  for (int64_t c0 = 0; c0 < N; c0 += kMedianChunk) {  // even chunk starts: 4-byte pairs stay aligned
+    const int64_t n = N - c0 < kMedianChunk ? N - c0 : kMedianChunk;
+    const int64_t grid = ((n + 1) / 2 + BS - 1) / BS;
+    if (K == KMAX && c0 == 0)
+      hipLaunchKernelGGL((median_pk16_kernel<KMAX, true, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
+                         out, c0);
+    else if (c0 == 0)
+      hipLaunchKernelGGL((median_pk16_kernel<KMAX, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
+                         out, c0);
+    else
+      hipLaunchKernelGGL((median_pk16_kernel<KMAX, false, E, BS, true>), dim3(unsigned(grid)), dim3(BS), 0, st, src,
+                         K, n, out + c0, c0);
+  }
   return check_launch("fedagg_median");
 }
 
@@ -1298,13 +1430,6 @@ __device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
   }
 }
 
-// -inf / +inf in each element type: what a padded slot's load returns
-template <class E>
-__device__ typename E::S g_median_pad[2] = {__builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
-                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kNegInf)),
-                                            __builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
-                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kPosInf))};
-
 template <int P, int R, bool FULL, class E = MedF32, int BS = 256>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
     const typename E::S* const* __restrict__ src, int K, int64_t N, typename E::S* __restrict__ out) {
@@ -1337,7 +1462,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   const int64_t e = (int64_t(blockIdx.x) * BS + t) / P;
   const uint64_t boff = uint64_t(e < N ? e : N - 1) * sizeof(S);
   float v[R];
-  bool has_nan = false;
+  typename E::NanAcc nacc{};
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     if (j % 16 == 0 && j) __builtin_amdgcn_sched_barrier(0);
@@ -1345,26 +1470,37 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
     const uint64_t off = FULL ? boff : (boff & offmask[q]);
     const auto row = reinterpret_cast<const char*>(rows[q]);
     v[j] = E::widen(__builtin_nontemporal_load(as_global(reinterpret_cast<const S*>(row + off))));
-    has_nan |= __builtin_isnan(v[j]);
   }
+  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test (see median_kernel)
+#pragma unroll
+  for (int j = 0; j < R; ++j) E::nan_add(nacc, v[j]);
+  const bool has_nan = E::nan_any(nacc);
   // first NaN of the column in client (= slot) order, only in waves holding
   // one (pads are ±inf, never NaN)
   int nan_slot = KMAX;
-  float nan_v = 0.f;
+  S nan_raw{};
   if (__ballot(has_nan)) {
-#pragma unroll
-    for (int j = R - 1; j >= 0; --j) {
-      const bool n = __builtin_isnan(v[j]);
-      nan_slot = n ? sub * R + j : nan_slot;
-      nan_v = n ? v[j] : nan_v;
+    // re-read this lane's slots in client order (cache hits; see median_kernel)
+#pragma unroll 1
+    for (int j = 0; j < R; ++j) {
+      const int q = sub * (R + PAD) + j;
+      const uint64_t off = FULL ? boff : (boff & offmask[q]);
+      const S r = *as_global(reinterpret_cast<const S*>(reinterpret_cast<const char*>(rows[q]) + off));
+      if (E::raw_nan(r)) {
+        nan_slot = sub * R + j;
+        nan_raw = r;
+        break;
+      }
     }
 #pragma unroll
     for (int m = 1; m < P; m <<= 1) {
       const int os = __shfl_xor(nan_slot, m, 64);
-      const float ov = __shfl_xor(nan_v, m, 64);
+      using U = std::conditional_t<sizeof(S) == 4, uint32_t, uint16_t>;  // move the bits, not the value
+      const S ov = __builtin_bit_cast(
+          S, U(__shfl_xor(int(uint32_t(__builtin_bit_cast(U, nan_raw))), m, 64)));
       if (os < nan_slot) {
         nan_slot = os;
-        nan_v = ov;
+        nan_raw = ov;
       }
     }
   }
@@ -1379,7 +1515,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   if constexpr (P >= 4) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
   if constexpr (P >= 8) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
   if constexpr (P >= 16) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima across the two quads
-  if (sub == 0 && e < N) out[e] = E::narrow(nan_slot < KMAX ? nan_v : m);
+  if (sub == 0 && e < N) out[e] = nan_slot < KMAX ? nan_raw : E::narrow(m);
 }
 
 template <int P, int R, class E = MedF32, int BS = 256>
@@ -1392,6 +1528,101 @@ int launch_median_lanes(const typename E::S* const* src, int K, int64_t N, typen
   else
     hipLaunchKernelGGL((median_lanes_kernel<P, R, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
                        out);
+  return check_launch("fedagg_median");
+}
+
+// Any number of clients (the path above 1024, where the lane-group sort runs
+// out of lanes per column): MSD radix select over 32-bit order keys, the
+// column tile streamed from memory once per 8-bit digit.  A block owns 64
+// consecutive columns; its 4 waves read rows q, q + 4, ... of all 64 (one
+// coalesced 64-column segment per wave instruction) and count the keys that
+// match the digits chosen so far into a per-column 256-bin LDS histogram;
+// then, per column, the bin holding the remaining rank gives the next digit.
+// Four passes fix all 32 bits.  Passes 2-4 re-read the tile (K x 256 B per
+// row group), mostly from L2 / MALL.  The NaN rule is the register kernels':
+// the column's first NaN in client order (an LDS atomic min on the row, pass
+// one).  Exact for every input; a ±0 tie at the median may return the other
+// zero than torch's nth_element, as everywhere.
+constexpr int kRsCols = 64;
+__device__ __forceinline__ uint32_t f32_order_key(uint32_t u) { return (u & 0x80000000u) ? ~u : (u | 0x80000000u); }
+__device__ __forceinline__ uint32_t f32_from_order_key(uint32_t k) { return (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k; }
+
+template <class E>
+__global__ __launch_bounds__(256) void median_radix_stream_kernel(const typename E::S* const* __restrict__ src, int K,
+                                                                  int64_t N, typename E::S* __restrict__ out) {
+  constexpr int HS = 257;  // bins per column + 1: column c starts c banks apart
+  __shared__ uint32_t hist[kRsCols * HS];
+  __shared__ uint32_t part[4][kRsCols];
+  __shared__ uint32_t s_prefix[kRsCols];
+  __shared__ int s_rank[kRsCols];
+  __shared__ int nan_row[kRsCols];
+  const int t = threadIdx.x, c = t & (kRsCols - 1), q = t >> 6;
+  const int64_t col = int64_t(blockIdx.x) * kRsCols + c;
+  const int64_t colc = col < N ? col : N - 1;  // columns past the end recompute the last one
+  if (q == 0) {
+    nan_row[c] = K;
+    s_prefix[c] = 0;
+    s_rank[c] = (K - 1) / 2;
+  }
+  uint32_t pmask = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = t; i < kRsCols * HS; i += 256) hist[i] = 0;
+    __syncthreads();
+    const uint32_t prefix = s_prefix[c];
+    int first_nan = K;
+    int r = q;
+    for (; r + 12 < K; r += 16) {  // 4 rows in flight per lane
+      typename E::S x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load(as_global(src[r + 4 * u]) + colc);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float v = E::widen(x[u]);
+        const uint32_t k = f32_order_key(__float_as_uint(v));
+        if (shift == 24 && E::raw_nan(x[u]) && first_nan == K) first_nan = r + 4 * u;
+        if ((k & pmask) == prefix) atomicAdd(&hist[c * HS + ((k >> shift) & 0xffu)], 1u);
+      }
+    }
+    for (; r < K; r += 4) {
+      const typename E::S x = __builtin_nontemporal_load(as_global(src[r]) + colc);
+      const uint32_t k = f32_order_key(__float_as_uint(E::widen(x)));
+      if (shift == 24 && E::raw_nan(x) && first_nan == K) first_nan = r;
+      if ((k & pmask) == prefix) atomicAdd(&hist[c * HS + ((k >> shift) & 0xffu)], 1u);
+    }
+    if (first_nan < K) atomicMin(&nan_row[c], first_nan);
+    __syncthreads();
+    // lane (c, q) owns bins [64q, 64q + 64) of column c
+    uint32_t own = 0;
+    for (int b = 0; b < 64; ++b) own += hist[c * HS + 64 * q + b];
+    part[q][c] = own;
+    __syncthreads();
+    const int rank = s_rank[c];
+    int below = 0;
+    for (int j = 0; j < q; ++j) below += int(part[j][c]);
+    if (below <= rank && rank < below + int(own)) {  // exactly one q per column
+      int b = 0;
+      for (; b < 63; ++b) {
+        const int h = int(hist[c * HS + 64 * q + b]);
+        if (below + h > rank) break;
+        below += h;
+      }
+      s_prefix[c] = prefix | (uint32_t(64 * q + b) << shift);
+      s_rank[c] = rank - below;
+    }
+    pmask |= 0xffu << shift;
+    __syncthreads();
+  }
+  if (q == 0 && col < N) {
+    const int nr = nan_row[c];
+    out[col] = nr < K ? as_global(src[nr])[col] : E::narrow(__uint_as_float(f32_from_order_key(s_prefix[c])));
+  }
+}
+
+template <class E>
+int launch_median_radix_stream(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
+  const int64_t grid = (N + kRsCols - 1) / kRsCols;
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
+  hipLaunchKernelGGL((median_radix_stream_kernel<E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
   return check_launch("fedagg_median");
 }
 
@@ -1484,17 +1715,16 @@ template <bool FUSED_CAP, class C, class EPI, class WS>
 void launch_fused_cfg(const Seg<OpF32>& s, const EPI& epi, const WS& w, int32_t K, bool aligned, hipStream_t st) {
   const int64_t grid = ((s.numel + 3) / 4 + int64_t(C::BS) * C::V - 1) / (int64_t(C::BS) * C::V);
   const dim3 g{unsigned(grid)}, b{unsigned(C::BS)};
-  if (FUSED_CAP) {
-    if (aligned)
+  // The cap only pays on the aligned fast path (the prefetched operands live
+  // across the client loop there); the unaligned edge path keeps V*E chains
+  // in flight and spills under it, so it runs uncapped.
+  if (aligned) {
+    if constexpr (FUSED_CAP)
       hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, EPI, WS>), g, b, 0, st, s, epi, w, K);
     else
-      hipLaunchKernelGGL((reduce_fused_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, EPI, WS>), g, b, 0, st, s, epi, w,
-                         K);
-  } else {
-    if (aligned)
       hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, true, C::BS, EPI, WS>), g, b, 0, st, s, epi, w, K);
-    else
-      hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, EPI, WS>), g, b, 0, st, s, epi, w, K);
+  } else {
+    hipLaunchKernelGGL((reduce_kernel<OpF32, C::U, C::V, C::NT, false, C::BS, EPI, WS>), g, b, 0, st, s, epi, w, K);
   }
 }
 
@@ -1526,10 +1756,8 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
     if (K <= 256) return launch_median_lanes<4, 64, E>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
     if (K <= 512) return launch_median_lanes<4, 128, E>(d_src, K, N, d_out, st);
     if (K <= 1024) return launch_median_lanes<8, 128, E>(d_src, K, N, d_out, st);
-    return set_error(FEDAGG_EINVAL, "fedagg_median: K > 1024 clients is not supported");
+    return launch_median_radix_stream<E>(d_src, K, N, d_out, st);  // no bound on K
   }
-  // the register kernels address rows with 32-bit byte offsets
-  if (N > (int64_t(1) << 30)) return set_error(FEDAGG_EINVAL, "fedagg_median: N > 2^30 elements per row");
   if constexpr (sizeof(typename E::S) == 2) {
     if (aligned) {  // two columns per lane on packed int16 keys
       if (K <= 32) return launch_median_pk16<32, E>(d_src, K, N, d_out, st);

@@ -207,10 +207,13 @@ int fedagg_wsum_fedopt_adagrad_f32(const float* const* d_src, const float* d_w,
  * core/security/defense/coordinate_wise_median_defense.py:24-32:
  * torch.median(stack, dim=-1).values): out[e] = the LOWER median (sorted
  * element (K-1)/2) of {src_i[e]}; if the column holds a NaN, the first NaN in
- * client order.  K <= 1024 (K <= 128: one lane per element, a pruned sorting
- * network in registers; 128 < K <= 1024: 2, 4 or 8 lanes per element, each
- * sorting 128 values in registers, merged across lanes).  Where +0.0 and -0.0 tie at the median the sign of the zero
- * returned may differ from torch's (nth_element order). */
+ * client order.  Any K >= 1 and N (K <= 128: one lane per element, a pruned
+ * sorting network in registers, launched in chunks of 2^30 columns;
+ * 128 < K <= 1024: 4 or 8 lanes per element, each sorting 64 or 128 values in
+ * registers, merged across lanes; K > 1024: an 8-bit MSD radix select per
+ * column over LDS histograms, the column re-read per digit).  Where +0.0 and
+ * -0.0 tie at the median the sign of the zero returned may differ from
+ * torch's (nth_element order). */
 int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N,
                       float* d_out, uint32_t flags, fedagg_stream_t stream);
 

@@ -113,13 +113,52 @@ def test_median_lanes_large_sampled(cuda_device):
     gu.assert_same(out[idx].cpu(), torch.from_numpy(exp), "median K=512 sampled")
 
 
-def test_median_rejects_too_many_clients(cuda_device):
-    from fedml_amd import _native as nat
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K", [1025, 1500, 2048, 4097])
+def test_median_more_than_1024_clients(dtype, K, cuda_device):
+    """No client bound, as torch.median has none (coordinate_wise_median_
+    defense.py:24-32): above 1024 clients the radix-select kernel, every
+    dtype, with duplicates, infinities, NaN columns (first NaN in client
+    order) and -0.0, a ragged last tile."""
+    N = 1_037
+    g = torch.Generator(device=cuda_device).manual_seed(K)
+    rows = (torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125).to(dtype)
+    rows[:, 17:29] = torch.randn(K, 12, generator=g, device=cuda_device).to(dtype)
+    rows[:, :7] = float("inf")
+    rows[:, 7:9] = -float("inf")
+    rows[K // 2, 100:110] = float("nan")
+    rows[K - 1, 105:115] = -float("nan")
+    rows[:, 200:203] = -0.0
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, dtype=dtype, device=cuda_device)
+    dfn.median_rows(d_ptrs, K, N, out, aligned=True)
+    exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
+    gu.assert_same(out.cpu(), exp, f"median {dtype} K={K}")
 
-    rows = torch.zeros(1025, 64, device=cuda_device)
-    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(1025)], cuda_device)
-    with pytest.raises(nat.FedAggNativeError):
-        dfn.median_f32(d_ptrs, 1025, 64, torch.empty(64, device=cuda_device))
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_median_more_than_2_30_columns(dtype, cuda_device):
+    """A row longer than 2^30 elements (a whole-model stack past a billion
+    parameters): the 32-bit-offset kernels run in chunks of 2^30 columns;
+    columns on both sides of the chunk boundary and the ragged end vs the
+    oracle."""
+    K, N = 3, (1 << 30) + 4_099
+    g = torch.Generator(device=cuda_device).manual_seed(30)
+    L = (N + 127) // 64 * 64  # 256-B row stride: aligned rows, as bucket rows are
+    rows = torch.empty((K, L), dtype=dtype, device=cuda_device)
+    for i in range(K):
+        rows[i].copy_(torch.randint(-1000, 1000, (L,), generator=g, device=cuda_device, dtype=torch.int32)
+                      .to(dtype) * 0.001)
+    rows = rows[:, :N]
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, dtype=dtype, device=cuda_device)
+    dfn.median_rows(d_ptrs, K, N, out, aligned=True)
+    idx = torch.cat([torch.arange(0, 64), torch.arange((1 << 30) - 64, (1 << 30) + 64), torch.arange(N - 64, N),
+                     torch.randint(0, N, (20_000,), generator=torch.Generator().manual_seed(1))]).to(cuda_device)
+    exp = torch.from_numpy(orc.lower_median_cols(rows[:, idx].float().cpu().numpy())).to(dtype)
+    gu.assert_same(out[idx].cpu(), exp, f"median {dtype} N > 2^30")
+    del rows, out
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("aligned", [False, True])

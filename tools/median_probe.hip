@@ -19,12 +19,7 @@ namespace {
 // atomic min while the tile is loaded).
 constexpr int kRadixCols = 32;
 
-__device__ __forceinline__ uint32_t f32_order_key(uint32_t u) {
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ uint32_t f32_from_order_key(uint32_t k) {
-  return (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
-}
+// f32_order_key / f32_from_order_key: fedagg.hip (the radix-stream kernel)
 
 // Column stride in LDS: >= KCAP and = 9 (mod 64), so the column-major writes
 // of 64 consecutive columns hit 64 different banks and the 8 columns a wave
