@@ -55,6 +55,7 @@ SIGNATURES = {
     "fedagg_lsa_reconstruct_f32": (ctypes.c_int, [_P, _I32, _I64, _P, _I64, _I32, _F, _P, _U32, _P]),
     "fedagg_host_pack": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32]),
     "fedagg_host_unpack": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32]),
+    "fedagg_host_round_f32": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P]),
     "fedagg_last_error": (ctypes.c_char_p, []),
     "fedagg_version": (_I32, []),
     "fedagg_wsum_f32_variant": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _I32, _P]),

@@ -278,6 +278,30 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
     return OrderedDict((k, results[k]) for k in keys)
 
 
+_HOST_ROUND_MAX_BYTES = 32 << 20  # host rounds up to this size: one native call, host to host
+_HOST_ROUND_FN: "int | None" = None
+
+
+def _reduce_host_round(w, dicts, keys, weights) -> "OrderedDict[str, torch.Tensor] | None":
+    """Small host rounds of fp32 / int64 keys (configs 1 and 2): the whole
+    round in ONE native call, fedagg_host_round_f32 (pack into pinned memory,
+    reduce on the GPU, results into new fp32 host tensors; no torch copies,
+    events or stream bookkeeping around it).  None when the walker declines
+    (other dtypes, a non-contiguous or device tensor, K > 256, a bigger round)."""
+    global _HOST_ROUND_FN
+    if _HOST_ROUND_FN is None:
+        import ctypes
+
+        _HOST_ROUND_FN = ctypes.cast(nat.lib().fedagg_host_round_f32, ctypes.c_void_p).value
+    # stream 0: the library's own non-blocking stream (host in, host out)
+    got = w.host_round(dicts, keys, weights, _HOST_ROUND_FN, 0, _HOST_ROUND_MAX_BYTES)
+    if got is None:
+        return None
+    rc, outs = got
+    nat.check(rc, "fedagg_host_round_f32")
+    return OrderedDict(zip(keys, outs))
+
+
 _BATCH_MAX_BYTES = 256 << 20  # host rounds up to this size stage every client in one pack + one H2D
 _ROW_ESZ = {nat.DT_F32: 4, nat.DT_BF16: 2, nat.DT_F16: 2, nat.DT_F64: 8, nat.DT_I64: 8}
 
@@ -319,10 +343,17 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
     acc_mode = _acc_mode(args)
     w = _walker()
     if w is not None and keys:
-        res = _reduce_device_walked(w, list(dicts), list(keys), weights, acc_mode)
+        dicts, keys = list(dicts), list(keys)
+        t0 = dicts[0].get(keys[0]) if isinstance(dicts[0], dict) else None
+        if isinstance(t0, torch.Tensor) and not t0.is_cuda and getattr(args, "fedagg_device", None) is None \
+                and torch.cuda.is_available():
+            res = _reduce_host_round(w, dicts, keys, weights)
+            if res is not None:
+                return res
+        res = _reduce_device_walked(w, dicts, keys, weights, acc_mode)
         if res is not None:
             return res
-        res = _reduce_host_batched(w, list(dicts), list(keys), weights, args, acc_mode)
+        res = _reduce_host_batched(w, dicts, keys, weights, args, acc_mode)
         if res is not None:
             return res
     per_key = _gather(dicts, keys)

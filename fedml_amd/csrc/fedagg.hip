@@ -36,6 +36,11 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -1703,6 +1708,166 @@ int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, c
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// One small host-resident round, host to host (fedagg_host_round_f32).
+//
+// Config 1 (4 clients x 7,850 fp32) is 125 KB: a PCIe round trip plus the
+// launch and completion latencies, not bytes, decide its time, and every
+// torch-level step around them (pinned copies, events, stream bookkeeping)
+// costs as much as the reduction.  So the whole round is one call: pack the
+// clients into a coherent pinned image [K][L] (L = the model's keys, 16-byte
+// aligned, padded to 64 elements), reduce, and unpack the result into the
+// caller's host tensors.  Up to kZeroCopyBytes of clients the kernel reads the
+// pinned image itself over PCIe (no copy call); larger rounds (config 2:
+// 7.9 MB) go up with one DMA into cached device rows.  Either way the kernel
+// writes the result straight into pinned memory and its last workgroup raises
+// a completion word there, which the host spins on: no stream synchronise.
+// Same arithmetic as every FedAvg kernel: acc = x_0*w_0; acc = acc + x_i*w_i.
+
+constexpr int64_t kZeroCopyBytes = int64_t(1) << 20;
+constexpr int kRoundBlock = 256;
+
+__global__ __launch_bounds__(kRoundBlock) void host_round_kernel(const float* __restrict__ rows, int64_t L, int K,
+                                                                 InlW<float> w, float* __restrict__ res,
+                                                                 unsigned int* __restrict__ counter,
+                                                                 unsigned int* __restrict__ flag, unsigned int seq) {
+  const int64_t e = int64_t(blockIdx.x) * kRoundBlock + threadIdx.x;
+  if (e < L) {
+    // 8 client loads in flight, the last group predicated: read over PCIe
+    // from pinned memory each is a full round trip, so latency, not bytes,
+    // is the cost
+    float acc = 0.f;
+    for (int c = 0; c < K; c += 8) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = (c + u < K) ? rows[int64_t(c + u) * L + e] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c + u < K) acc = (c + u == 0) ? x[u] * w[0] : acc + x[u] * w[c + u];
+    }
+    res[e] = acc;
+  }
+  // every workgroup's result stores are visible system-wide before it is
+  // counted; the last one resets the counter and raises the host's word
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int prev = atomicAdd(counter, 1u);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// A persistent pool for the host copies of a round (spawning threads per call
+// costs more than a config-2 pack).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool(std::max(1u, std::min(8u, std::thread::hardware_concurrency())) - 1);
+    return *p;
+  }
+  int size() const { return int(workers_.size()) + 1; }
+  void run(int parts, const std::function<void(int)>& fn) {
+    parts = std::max(1, std::min(parts, size()));
+    if (parts == 1) {
+      fn(0);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &fn;
+      parts_ = parts;
+      next_.store(1);
+      pending_ = parts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0 && active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  explicit HostPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
+    workers_.resize(n);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (!job_) continue;
+      const std::function<void(int)>* fn = job_;
+      const int parts = parts_;
+      ++active_;
+      lk.unlock();
+      int done = 0;
+      for (int part = next_.fetch_add(1); part < parts; part = next_.fetch_add(1), ++done) (*fn)(part);
+      lk.lock();
+      pending_ -= done;
+      --active_;
+      if (pending_ == 0 && active_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::vector<char> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  int parts_ = 0, pending_ = 0, active_ = 0;
+  std::atomic<int> next_{1};
+  uint64_t gen_ = 0;
+};
+
+// Buffers of one device, grown on demand and kept (a server runs the same
+// round shape every round): the pinned image, the pinned result, the device
+// rows of the DMA path, the completion word and the workgroup counter.
+struct RoundCtx {
+  float* stage = nullptr;
+  size_t stage_n = 0;
+  float* res = nullptr;
+  size_t res_n = 0;
+  float* rows = nullptr;
+  size_t rows_n = 0;
+  unsigned int* flag = nullptr;
+  unsigned int* counter = nullptr;
+  unsigned int seq = 0;
+  hipStream_t own = nullptr;
+};
+std::mutex g_round_mu;
+std::vector<RoundCtx> g_round_ctx;
+
+int grow_pinned(float** p, size_t* have, size_t need) {
+  if (*have >= need) return FEDAGG_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *have = 0;
+  const size_t n = need + need / 4;
+  if (hipHostMalloc(reinterpret_cast<void**>(p), n * sizeof(float), hipHostMallocCoherent | hipHostMallocMapped) !=
+      hipSuccess)
+    return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: pinned allocation failed");
+  *have = n;
+  return FEDAGG_OK;
+}
+
+template <class F>
+void split_rows(int64_t bytes, int n, const F& fn) {  // fn(i) for i in [0, n), across the pool for big copies
+  if (bytes < (int64_t(2) << 20) || n < 2) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  HostPool& pool = HostPool::get();
+  const int parts = std::min(pool.size(), n);
+  pool.run(parts, [&](int part) {
+    for (int i = part; i < n; i += parts) fn(i);
+  });
+}
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -2068,6 +2233,123 @@ int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_of
   parallel_ranges(
       n, nbytes, threads, [&](int32_t i) { return static_cast<const char*>(src) + src_offs[i]; },
       [&](int32_t i) { return static_cast<char*>(dsts[i]); });
+  return FEDAGG_OK;
+}
+
+int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes, const int64_t* numels, int32_t T,
+                          int32_t K, const float* weights, void* const* h_out, fedagg_stream_t stream) {
+  if (K < 1 || K > kInlineK || T < 0 || (T && (!h_src || !codes || !numels || !h_out)) || !weights)
+    return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: bad argument (1 <= K <= 256)");
+  std::vector<int64_t> off(size_t(T) + 1);
+  int64_t L = 0;
+  for (int32_t t = 0; t < T; ++t) {
+    if (codes[t] != FEDAGG_DT_F32 && codes[t] != FEDAGG_DT_I64)
+      return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: keys must be fp32 or int64");
+    if (numels[t] < 0) return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: negative numel");
+    off[t] = L;
+    L = (L + numels[t] + 3) / 4 * 4;  // next key 16-byte aligned
+  }
+  if (L == 0) return FEDAGG_OK;
+  L = (L + 63) / 64 * 64;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: no device");
+  std::lock_guard<std::mutex> lock(g_round_mu);
+  if (g_round_ctx.size() <= size_t(dev)) g_round_ctx.resize(size_t(dev) + 1);
+  RoundCtx& cx = g_round_ctx[size_t(dev)];
+  const int64_t elems = int64_t(K) * L, bytes = elems * 4;
+  const bool zero_copy = bytes <= kZeroCopyBytes;
+  if (int rc = grow_pinned(&cx.stage, &cx.stage_n, size_t(elems))) return rc;
+  if (int rc = grow_pinned(&cx.res, &cx.res_n, size_t(L))) return rc;
+  if (!cx.flag) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&cx.flag), 64, hipHostMallocCoherent | hipHostMallocMapped) !=
+            hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&cx.counter), 64) != hipSuccess ||
+        hipMemset(cx.counter, 0, 64) != hipSuccess)
+      return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: allocation failed");
+    __atomic_store_n(cx.flag, 0u, __ATOMIC_RELEASE);
+  }
+  if (!zero_copy && cx.rows_n < size_t(elems)) {
+    if (cx.rows) (void)hipFree(cx.rows);
+    cx.rows = nullptr;
+    cx.rows_n = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&cx.rows), size_t(elems) * 4) != hipSuccess)
+      return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: device allocation failed");
+    cx.rows_n = size_t(elems);
+  }
+  // pack: client i's key t goes to stage[i][off[t]] (int64 keys as fl32(v),
+  // the reference's int64 * float promotion)
+  auto pack = [&](int i0, int i1) {
+    split_rows(int64_t(i1 - i0) * L * 4, i1 - i0, [&](int ii) {
+      const int i = i0 + ii;
+      float* row = cx.stage + int64_t(i) * L;
+      for (int32_t t = 0; t < T; ++t) {
+        const void* src = h_src[size_t(t) * K + size_t(i)];
+        if (codes[t] == FEDAGG_DT_F32) {
+          memcpy(row + off[t], src, size_t(numels[t]) * 4);
+        } else {
+          const int64_t* v = static_cast<const int64_t*>(src);
+          for (int64_t j = 0; j < numels[t]; ++j) row[off[t] + j] = static_cast<float>(v[j]);
+        }
+      }
+    });
+  };
+  InlW<float> iw;
+  for (int i = 0; i < K; ++i) iw.v[i] = weights[i];
+  // no stream given: the library's own non-blocking stream (host inputs and
+  // outputs; nothing on the caller's streams to order against)
+  if (!stream) {
+    if (!cx.own) {
+      if (hipStreamCreateWithFlags(&cx.own, hipStreamNonBlocking) != hipSuccess)
+        return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: stream creation failed");
+    }
+    stream = cx.own;
+  }
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  const float* rows = nullptr;
+  float* res_d = nullptr;
+  unsigned int* flag_d = nullptr;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&res_d), cx.res, 0) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&flag_d), cx.flag, 0) != hipSuccess)
+    return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: pinned memory not device-mapped");
+  if (zero_copy) {
+    pack(0, K);
+    float* stage_d = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&stage_d), cx.stage, 0) != hipSuccess)
+      return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: pinned memory not device-mapped");
+    rows = stage_d;
+  } else {
+    // ~2 MiB of clients per DMA: packing the next group overlaps the copy of
+    // this one
+    const int per = int(std::max<int64_t>(1, (int64_t(2) << 20) / (L * 4)));
+    for (int i0 = 0; i0 < K; i0 += per) {
+      const int i1 = std::min<int>(K, i0 + per);
+      pack(i0, i1);
+      if (hipMemcpyAsync(cx.rows + int64_t(i0) * L, cx.stage + int64_t(i0) * L, size_t(int64_t(i1 - i0) * L * 4),
+                         hipMemcpyHostToDevice, st) != hipSuccess)
+        return check_launch("fedagg_host_round_f32 (H2D)");
+    }
+    rows = cx.rows;
+  }
+  const unsigned int seq = ++cx.seq == 0 ? ++cx.seq : cx.seq;  // never 0, the word's initial value
+  const unsigned grid = unsigned((L + kRoundBlock - 1) / kRoundBlock);
+  hipLaunchKernelGGL(host_round_kernel, dim3(grid), dim3(kRoundBlock), 0, st, rows, L, int(K), iw, res_d,
+                     cx.counter, flag_d, seq);
+  if (int rc = check_launch("fedagg_host_round_f32")) return rc;
+  // the completion word; a bounded spin, then the stream's own error
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(cx.flag, __ATOMIC_ACQUIRE) != seq) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      const hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return set_error(static_cast<int>(e), "fedagg_host_round_f32: " + std::string(hipGetErrorString(e)));
+      if (__atomic_load_n(cx.flag, __ATOMIC_ACQUIRE) != seq)
+        return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: completion word never arrived");
+      break;
+    }
+  }
+  // unpack into the caller's per-key host tensors (fp32 results)
+  split_rows(L * 4, T, [&](int t) {
+    if (numels[t]) memcpy(h_out[t], cx.res + off[t], size_t(numels[t]) * 4);
+  });
   return FEDAGG_OK;
 }
 

@@ -348,7 +348,105 @@ fail:
   return nullptr;
 }
 
+// host_round(dicts: list, keys: list, weights: list of float, fn: int, stream: int,
+//            max_bytes: int) -> None | (rc, outs)
+//   One small host round through libfedagg's fedagg_host_round_f32 (fn is
+//   its address): every key of every client a contiguous CPU tensor of fp32
+//   or int64, same shapes across clients, K <= 256.  outs[t] is a new fp32
+//   host tensor shaped like client 0's key t (the reference's result dtype
+//   for both), filled when rc == 0.  None for anything else, or for rounds
+//   of more than max_bytes of client elements (as fp32) (the caller's
+//   general path then runs and raises the reference's errors).  The GIL is
+//   released while the round runs.
+using HostRoundFn = int (*)(const void* const*, const int32_t*, const int64_t*, int32_t, int32_t, const float*,
+                            void* const*, void*);
+
+PyObject* host_round(PyObject*, PyObject* args) {
+  PyObject* dicts;
+  PyObject* keys;
+  PyObject* weights;
+  unsigned long long fn_addr = 0, stream = 0;
+  long long max_bytes = 0;
+  if (!PyArg_ParseTuple(args, "O!O!O!KKL", &PyList_Type, &dicts, &PyList_Type, &keys, &PyList_Type, &weights,
+                        &fn_addr, &stream, &max_bytes))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(dicts), T = PyList_GET_SIZE(keys);
+  if (K < 1 || K > 256 || PyList_GET_SIZE(weights) != K || !fn_addr) Py_RETURN_NONE;
+  try {
+    for (Py_ssize_t i = 0; i < K; ++i)
+      if (!plain_lookup(PyList_GET_ITEM(dicts, i))) Py_RETURN_NONE;
+    std::vector<float> w(static_cast<size_t>(K));
+    for (Py_ssize_t i = 0; i < K; ++i) {
+      const double v = PyFloat_AsDouble(PyList_GET_ITEM(weights, i));  // a Python float: n_i / sum n
+      if (v == -1.0 && PyErr_Occurred()) {
+        PyErr_Clear();
+        Py_RETURN_NONE;
+      }
+      w[size_t(i)] = static_cast<float>(v);  // RNE, as torch rounds the scalar of p * w
+    }
+    std::vector<const void*> src(size_t(T) * K);
+    std::vector<int32_t> codes(T);
+    std::vector<int64_t> numels(T);
+    std::vector<at::Tensor> outs;
+    std::vector<void*> optr(T);
+    outs.reserve(T);
+    int64_t total = 0;
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      const at::Tensor* x0 = nullptr;
+      for (Py_ssize_t i = 0; i < K; ++i) {
+        PyObject* v = PyDict_GetItemWithError(PyList_GET_ITEM(dicts, i), PyList_GET_ITEM(keys, t));
+        if (!v) {
+          if (PyErr_Occurred()) return nullptr;
+          Py_RETURN_NONE;
+        }
+        if (Py_TYPE(v) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) Py_RETURN_NONE;
+        const at::Tensor& x = THPVariable_Unpack(v);
+        if (!x.defined() || x.layout() != c10::kStrided || x.device().type() != c10::DeviceType::CPU ||
+            !x.is_contiguous())
+          Py_RETURN_NONE;
+        if (i == 0) {
+          x0 = &x;
+          const auto st = x.scalar_type();
+          if (st != c10::ScalarType::Float && st != c10::ScalarType::Long) Py_RETURN_NONE;
+          codes[t] = st == c10::ScalarType::Float ? 0 : 4;
+          numels[t] = x.numel();
+        } else if (x.scalar_type() != x0->scalar_type() || x.sizes() != x0->sizes()) {
+          Py_RETURN_NONE;
+        }
+        src[size_t(t) * K + i] = x.data_ptr();
+      }
+      total += numels[t];
+      if (total * 4 * K > max_bytes) Py_RETURN_NONE;  // a big round: the staging-ring path
+    }
+    for (Py_ssize_t t = 0; t < T; ++t) {  // outputs only once every key has passed
+      const at::Tensor& x0 = THPVariable_Unpack(PyDict_GetItem(PyList_GET_ITEM(dicts, 0), PyList_GET_ITEM(keys, t)));
+      outs.push_back(at::empty(x0.sizes(), x0.options().dtype(at::kFloat)));
+      optr[t] = outs.back().data_ptr();
+    }
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = reinterpret_cast<HostRoundFn>(fn_addr)(src.data(), codes.data(), numels.data(), int32_t(T), int32_t(K),
+                                                 w.data(), optr.data(), reinterpret_cast<void*>(stream));
+    Py_END_ALLOW_THREADS
+    PyObject* py_outs = PyList_New(T);
+    if (!py_outs) return nullptr;
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      PyObject* o = THPVariable_Wrap(std::move(outs[t]));
+      if (!o) {
+        Py_DECREF(py_outs);
+        return nullptr;
+      }
+      PyList_SET_ITEM(py_outs, t, o);
+    }
+    return Py_BuildValue("(iN)", rc, py_outs);
+  } catch (const std::exception&) {
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+}
+
 PyMethodDef kMethods[] = {
+    {"host_round", host_round, METH_VARARGS, "One small host round through fedagg_host_round_f32, or None."},
     {"walk", walk, METH_VARARGS, "Pointer tables of K device state dicts for fedagg_wsum_multi, or None."},
     {"order_by_size", order_by_size, METH_VARARGS, "Key indices of a state dict, largest tensor first, or None."},
     {"walk_host", walk_host, METH_VARARGS, "Host pointer tables of K CPU state dicts for one batched pack, or None."},

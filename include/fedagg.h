@@ -263,6 +263,31 @@ int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs
 int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_offs,
                        const int64_t* nbytes, int32_t n, int32_t threads);
 
+/* ---- Small host-resident rounds ----------------------------------------- */
+
+/* One whole FedAvg round of HOST tensors, host to host, in one call: the
+ * reference call shape FedMLAggOperator.agg(args, [(n_i, cpu_state_dict)])
+ * (agg_operator.py:35-44; the SP simulation's FedAvgAPI._aggregate,
+ * simulation/sp/fedavg/fedavg_api.py:144-159) for rounds small enough that a
+ * PCIe round trip, not bytes, is the cost (configs 1 and 2).
+ *   h_src   : host pointers [T][K], key-major: key t of client i at t*K + i
+ *   codes   : FEDAGG_DT_F32 or FEDAGG_DT_I64 per key (int64 values enter as
+ *             fl32(v) and give fp32 results, the reference's promotion)
+ *   weights : K fp32 weights fl32(n_i / sum n), K <= 256
+ *   h_out   : T host fp32 buffers of numels[t] elements, written on return
+ * The library packs the clients into pinned memory it keeps per device
+ * (allocated on first use and grown when a bigger round arrives), reduces on
+ * the device (the kernel reads rounds up to 1 MiB straight from pinned
+ * memory; larger ones go up in one DMA), and copies the result out.
+ * Synchronous (returns when h_out holds the result).  stream NULL runs it
+ * on a non-blocking stream of the library's own (nothing on the caller's
+ * streams is involved: host in, host out); a stream orders it after the
+ * caller's work there.  Bit-identical to the reference chain. */
+int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes,
+                          const int64_t* numels, int32_t T, int32_t K,
+                          const float* weights, void* const* h_out,
+                          fedagg_stream_t stream);
+
 /* ---- Introspection ------------------------------------------------------ */
 const char* fedagg_last_error(void);
 int32_t fedagg_version(void);

@@ -535,3 +535,44 @@ def test_put_interleaved_host_and_device_keys(cuda_device):
         res = bucket.aggregate()
         for k, e in exp.items():
             gu.assert_same(res[k].cpu(), e, f"round {r} {k}")
+
+
+@pytest.mark.parametrize("model,K", [("lr_mnist", 4), ("cnn_web", 32), ("lr_mnist", 256), ("lr_mnist", 257),
+                                     ("cnn_web", 1)])
+def test_small_host_rounds_take_one_native_call(model, K, cuda_device, monkeypatch):
+    """Configs 1 and 2 on host dicts: the whole round is fedagg_host_round_f32
+    (zero-copy kernel at config 1's 125 KB, one DMA at config 2's 7.9 MB),
+    bit-exact vs the oracle; results are new independent fp32 host tensors;
+    K = 257 (beyond the inline weights) takes the staging path instead."""
+    calls = []
+    real = ao._reduce_host_round
+
+    def spy(*a, **k):
+        r = real(*a, **k)
+        calls.append(r is not None)
+        return r
+
+    monkeypatch.setattr(ao, "_reduce_host_round", spy)
+    raw = host_clients(shapes.MODELS[model](), K, seed=K)
+    exp = orc.agg(type("A", (), {"federated_optimizer": "FedAvg"})(), copy.deepcopy(raw))
+    c0 = raw[0][1]
+    res = ao.FedMLAggOperator.agg(type("A", (), {"federated_optimizer": "FedAvg"})(), raw)
+    assert res is c0 and calls == [K <= 256]
+    ptrs = set()
+    for k, e in exp.items():
+        assert not res[k].is_cuda and res[k].dtype == torch.float32 and res[k].is_contiguous()
+        gu.assert_same(res[k], e, f"{model} K={K} {k}")
+        ptrs.add(res[k].data_ptr())
+    assert len(ptrs) == len(exp)
+
+
+def test_host_round_mixed_int64_and_buffer_growth(cuda_device):
+    """int64 keys enter as fl32(v) (|v| up to 2^40) with fp32 results, as
+    the reference promotes them; consecutive rounds of different sizes
+    (growing, then shrinking the library's pinned buffers) stay exact."""
+    A = type("A", (), {"federated_optimizer": "FedAvg"})
+    for name in ["resnet_mini_bigint_k3", "cfg2_cnn_web_k32", "cfg1_lr_mnist_k4", "resnet_mini_k5"]:
+        meta, arrays = gu.load(name)
+        raw = cases.build_inputs(meta["spec"])
+        res = ao.FedMLAggOperator.agg(A(), raw)
+        gu.assert_groups(res, meta, arrays, name)

@@ -45,7 +45,12 @@ def _eager(raw):
     return avg
 
 
-def _time(fn, make, reps, sync):
+def _time(fn, make, reps, sync, sync_after=None):
+    """sync: drain the device before the call; sync_after (default: sync):
+    also inside the timed region after it (device results).  A host-dict
+    agg() returns host tensors that already hold the result, like the
+    reference loop, so it is timed without a trailing synchronize."""
+    sync_after = sync if sync_after is None else sync_after
     ts = []
     for r in range(reps + 5):
         lst = make()
@@ -53,12 +58,21 @@ def _time(fn, make, reps, sync):
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         out = fn(lst)
-        if sync:
+        if sync_after:
             torch.cuda.synchronize()
         t1 = time.perf_counter()
         if r >= 5:
             ts.append((t1 - t0) * 1e6)
     return round(statistics.median(ts), 1)
+
+
+def _one_thread(fn):
+    old = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        return fn()
+    finally:
+        torch.set_num_threads(old)
 
 
 def main():
@@ -75,17 +89,28 @@ def main():
             return [(n, OrderedDict(d)) for n, d in draw]
 
         args = _Args()
+        from fedml_amd import agg_operator as ao
+
+        wk = ao._walker()
+        keys = list(raw[0][1].keys())
+        ws = [n / sum(n for n, _ in raw) for n, _ in raw]
+        ao._reduce_host_round(wk, [d for _, d in raw], keys, ws)  # resolve the function pointer once
         r = {
-            "agg_host_dicts_us": _time(lambda l: FedMLAggOperator.agg(args, l), host_list, 200, True),
+            "native_host_round_us": _time(lambda l: wk.host_round([d for _, d in l], keys, ws, ao._HOST_ROUND_FN, 0,
+                                                                  ao._HOST_ROUND_MAX_BYTES), host_list, 500, True,
+                                          False),
+            "agg_host_dicts_us": _time(lambda l: FedMLAggOperator.agg(args, l), host_list, 500, True, False),
             "agg_device_dicts_us": _time(lambda l: FedMLAggOperator.agg(args, l), dev_list, 200, True),
-            "reference_loop_cpu_us": _time(_eager, host_list, 200, False),
+            "reference_loop_cpu_us": _time(_eager, host_list, 500, False),
+            "reference_loop_cpu_1thread_us": _one_thread(lambda: _time(_eager, host_list, 500, False)),
             "reference_loop_gpu_eager_us": _time(_eager, dev_list, 200, True),
             "cpu_threads": torch.get_num_threads(),
         }
         res[cfg] = r
         print(cfg, r, flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
-    json.dump(res, open("gpurun_out/small_agg_bench.json", "w"), indent=1)
+    out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/small_agg_bench.json"
+    json.dump(res, open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
