@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--chunks", type=int, default=8, help="client mode: reduce-scatter pipeline depth")
     ap.add_argument("--acc", default="reference", choices=["reference", "fp32"],
                     help="bf16/f16 accumulation: torch's per-op chain (bit-exact) or fp32")
-    ap.add_argument("--fedopt", nargs="?", const="sgd", default=None, choices=["sgd", "adam", "adagrad"],
+    ap.add_argument("--fedopt", nargs="?", const="sgd", default=None,
+                    choices=["sgd", "adam", "adamw", "adagrad", "rmsprop"],
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
                          "or Adam / Adagrad lr=1.0 with torch defaults)")
     ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa"],
@@ -373,7 +374,9 @@ def main():
             "layout": "ClientBucket rows [K, L] per dtype, 256-B aligned rows",
             "low_precision_acc": a.acc,
             "server_step": ({"sgd": "SGD lr=1.0 momentum=0.9", "adam": "Adam lr=1.0 betas=(0.9,0.999)",
-                             "adagrad": "Adagrad lr=1.0 eps=1e-10"}[a.fedopt]
+                             "adagrad": "Adagrad lr=1.0 eps=1e-10",
+                             "adamw": "AdamW lr=1.0 weight_decay=0.01",
+                             "rmsprop": "RMSprop lr=1.0 alpha=0.99"}[a.fedopt]
                             + (" fused" if server is not None else
                                f", on each rank's 1/{world} shard after the reduce-scatter, sharded state")
                             if a.fedopt else None),
@@ -391,7 +394,8 @@ def main():
             "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>"}[a.op]
                        if a.op in ("secagg", "lsa") else
                        f"median_kernel<128, {dom_dt}>" if a.op == "median" else
-                       ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adagrad": "reduce_kernel<OpF32,AdagradEpi>"}
+                       ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
+                         "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>"}
                         .get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>"))
                        + " (FedAvg+server step fused)"
                        if server is not None else

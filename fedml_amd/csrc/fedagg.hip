@@ -404,12 +404,20 @@ struct SgdEpi {
 //   m = lerp(m, g, w1)          torch's vectorised lerp: one fma
 //   v = fma(fl(c2*g), g, fl(v*beta2))   mul_(beta2).addcmul_(g, g, value=c2)
 //   p = p_old + fl(nss*m) / (fl(sqrt(v) / bc2s) + eps)   addcdiv_, no fma
+//
+// AdamW (decoupled weight decay, torch.optim.AdamW = Adam with
+// decoupled_weight_decay) first scales the parameter, param.mul_(1 - lr*wd),
+// with the gradient already set from the unscaled one:
+//   p = fl(p_old * decay) + fl(nss*m) / denom,  decay = fl32(1 - lr*wd)
+// decoupled == 0 (Adam) never multiplies.
 struct AdamEpi {
   float* p;
   float* m;
   float* v;
   float w1, beta2, c2, bc2s, eps, nss;
   int first;  // exp_avg / exp_avg_sq are zero before torch's first step: skip their loads
+  float decay = 1.0f;
+  int decoupled = 0;
   static constexpr int E = 4;
   // p_old and exp_avg are prefetched before the client loop like SgdEpi's
   // operands; exp_avg_sq is loaded in the epilogue (a third prefetched pack
@@ -431,7 +439,8 @@ struct AdamEpi {
     const float vb = *vv * beta2;
     *vv = __builtin_fmaf(c2 * g, g, vb);
     const float denom = __builtin_sqrtf(*vv) / bc2s + eps;
-    return po + (nss * *mm) / denom;
+    const float pb = decoupled ? po * decay : po;
+    return pb + (nss * *mm) / denom;
   }
   __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E], const Pre& pr) const {
     float po[E], mo[E], vo[E];
@@ -463,10 +472,18 @@ struct AdamEpi {
 //   sum = fma(g, g, sum)                  addcmul_(g, g, value=1), fused
 //   p = p_old + fl(neg_clr * g) / (sqrt(sum) + eps)   addcdiv_, not fused
 // neg_clr = -lr / (1 + (step-1) * lr_decay) as fp32 (host side).
+//
+// RMSprop (torch.optim.RMSprop single-tensor CPU path, momentum 0, not
+// centered, weight_decay 0) is the same step with a decaying accumulator:
+//   square_avg.mul_(alpha).addcmul_(g, g, value=1-alpha)
+//                                  = fma(fl(c*g), g, fl(sq*alpha)), c = fl32(1-alpha)
+//   avg = fl(sqrt(square_avg) + eps);  p = p_old + fl(fl(-lr*g) / avg)
+// Adagrad is a = c = 1 (fl(1*g) = g, fl(sum*1) = sum: bit-identical).
 struct AdagradEpi {
   float* p;
   float* sum;
   float neg_clr, eps;
+  float a = 1.0f, c = 1.0f;
   static constexpr int E = 4;
   struct Pre {
     Pack<float, 4> p, s;
@@ -476,7 +493,7 @@ struct AdagradEpi {
   }
   __device__ __forceinline__ float step1(float po, float avg, float* ss) const {
     const float g = po - avg;
-    *ss = __builtin_fmaf(g, g, *ss);
+    *ss = __builtin_fmaf(c * g, g, *ss * a);
     const float std_ = __builtin_sqrtf(*ss) + eps;
     return po + (neg_clr * g) / std_;
   }
@@ -1717,35 +1734,51 @@ int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, c
 // costs as much as the reduction.  So the whole round is one call: pack the
 // clients into a coherent pinned image [K][L] (L = the model's keys, 16-byte
 // aligned, padded to 64 elements), reduce, and unpack the result into the
-// caller's host tensors.  Up to kZeroCopyBytes of clients the kernel reads the
-// pinned image itself over PCIe (no copy call); larger rounds (config 2:
-// 7.9 MB) go up with one DMA into cached device rows.  Either way the kernel
+// caller's host tensors.  Up to kZeroCopyBytes (16 MiB) of clients the kernel
+// reads the pinned image itself over PCIe in 16-byte loads (no copy call;
+// config 2's 7.9 MB: 267 us vs 274 us through DMA, tools/small_agg_bench.py);
+// larger rounds go up in ~1 MiB DMAs into cached device rows, each packed
+// while the previous one is in flight.  Either way the kernel
 // writes the result straight into pinned memory and its last workgroup raises
 // a completion word there, which the host spins on: no stream synchronise.
 // Same arithmetic as every FedAvg kernel: acc = x_0*w_0; acc = acc + x_i*w_i.
 
-constexpr int64_t kZeroCopyBytes = int64_t(1) << 20;
+constexpr int64_t kZeroCopyBytes = int64_t(16) << 20;
 constexpr int kRoundBlock = 256;
 
 __global__ __launch_bounds__(kRoundBlock) void host_round_kernel(const float* __restrict__ rows, int64_t L, int K,
                                                                  InlW<float> w, float* __restrict__ res,
                                                                  unsigned int* __restrict__ counter,
                                                                  unsigned int* __restrict__ flag, unsigned int seq) {
-  const int64_t e = int64_t(blockIdx.x) * kRoundBlock + threadIdx.x;
+  // four consecutive elements per lane (L is a multiple of 64): 16-byte
+  // loads, 1 KiB per wave instruction, so reads over PCIe travel in full lines
+  const int64_t e = (int64_t(blockIdx.x) * kRoundBlock + threadIdx.x) * 4;
   if (e < L) {
     // 8 client loads in flight, the last group predicated: read over PCIe
     // from pinned memory each is a full round trip, so latency, not bytes,
     // is the cost
-    float acc = 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int c = 0; c < K; c += 8) {
-      float x[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = (c + u < K) ? rows[int64_t(c + u) * L + e] : 0.f;
+      float4 x[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (c + u < K) acc = (c + u == 0) ? x[u] * w[0] : acc + x[u] * w[c + u];
+        x[u] = (c + u < K) ? *reinterpret_cast<const float4*>(rows + int64_t(c + u) * L + e)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (c + u >= K) continue;
+        const float wu = w[c + u];
+        if (c + u == 0) {
+          acc = make_float4(x[u].x * wu, x[u].y * wu, x[u].z * wu, x[u].w * wu);
+        } else {
+          acc.x = acc.x + x[u].x * wu;
+          acc.y = acc.y + x[u].y * wu;
+          acc.z = acc.z + x[u].z * wu;
+          acc.w = acc.w + x[u].w * wu;
+        }
+      }
     }
-    res[e] = acc;
+    *reinterpret_cast<float4*>(res + e) = acc;
   }
   // every workgroup's result stores are visible system-wide before it is
   // counted; the last one resets the counter and raises the host's word
@@ -1857,7 +1890,7 @@ int grow_pinned(float** p, size_t* have, size_t need) {
 
 template <class F>
 void split_rows(int64_t bytes, int n, const F& fn) {  // fn(i) for i in [0, n), across the pool for big copies
-  if (bytes < (int64_t(2) << 20) || n < 2) {
+  if (bytes < (int64_t(256) << 10) || n < 2) {
     for (int i = 0; i < n; ++i) fn(i);
     return;
   }
@@ -2151,6 +2184,57 @@ int fedagg_wsum_fedopt_adagrad_f32(const float* const* d_src, const float* d_w, 
   return check_launch("fedagg_wsum_fedopt_adagrad_f32");
 }
 
+int fedagg_wsum_fedopt_adamw_f32(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float* d_param,
+                                 float* d_exp_avg, float* d_exp_avg_sq, const float* scalars6, float decay,
+                                 int32_t first_step, uint32_t flags, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adamw_f32: K must be >= 1 and N >= 0");
+  if (!d_src || !d_w || !d_param || !d_exp_avg || !d_exp_avg_sq || !scalars6)
+    return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adamw_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  const int64_t grid = blocks_for<OpF32>(N);
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adamw_f32: N too large");
+  Seg<OpF32> s{d_src, N};
+  AdamEpi epi{d_param, d_exp_avg, d_exp_avg_sq, scalars6[0], scalars6[1], scalars6[2],
+              scalars6[3], scalars6[4], scalars6[5], first_step, decay, 1};
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
+  if (flags & FEDAGG_HOST_WEIGHTS) {
+    InlW<float> iw;
+    if (!inline_weights<float>(d_w, K, &iw))
+      return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_adamw_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
+    launch_fused<true>(s, epi, iw, K, aligned, st);
+  } else {
+    launch_fused<true>(s, epi, PtrW<float>{d_w}, K, aligned, st);
+  }
+  return check_launch("fedagg_wsum_fedopt_adamw_f32");
+}
+
+int fedagg_wsum_fedopt_rmsprop_f32(const float* const* d_src, const float* d_w, int32_t K, int64_t N,
+                                   float* d_param, float* d_square_avg, float lr, double alpha, float eps,
+                                   uint32_t flags, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_rmsprop_f32: K must be >= 1 and N >= 0");
+  if (!d_src || !d_w || !d_param || !d_square_avg)
+    return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_rmsprop_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  const int64_t grid = blocks_for<OpF32>(N);
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_rmsprop_f32: N too large");
+  Seg<OpF32> s{d_src, N};
+  // alpha and 1 - alpha are Python floats (doubles) that torch's CPU kernels
+  // round to fp32 each
+  AdagradEpi epi{d_param, d_square_avg, -lr, eps, float(alpha), float(1.0 - alpha)};
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
+  if (flags & FEDAGG_HOST_WEIGHTS) {
+    InlW<float> iw;
+    if (!inline_weights<float>(d_w, K, &iw))
+      return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_rmsprop_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
+    launch_fused<false>(s, epi, iw, K, aligned, st);
+  } else {
+    launch_fused<false>(s, epi, PtrW<float>{d_w}, K, aligned, st);
+  }
+  return check_launch("fedagg_wsum_fedopt_rmsprop_f32");
+}
+
 int fedagg_round_f32(int32_t dtype, const float* d_in, int64_t N, void* d_out, fedagg_stream_t stream) {
   if (N < 0 || (N > 0 && (!d_in || !d_out))) return set_error(FEDAGG_EINVAL, "fedagg_round_f32: bad argument");
   if (dtype != FEDAGG_DT_BF16 && dtype != FEDAGG_DT_F16)
@@ -2257,7 +2341,11 @@ int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes, const 
   if (g_round_ctx.size() <= size_t(dev)) g_round_ctx.resize(size_t(dev) + 1);
   RoundCtx& cx = g_round_ctx[size_t(dev)];
   const int64_t elems = int64_t(K) * L, bytes = elems * 4;
-  const bool zero_copy = bytes <= kZeroCopyBytes;
+  static const int64_t zc_max = [] {  // FEDAGG_ZERO_COPY_MAX: tuning override (tools/small_agg_bench.py)
+    const char* v = getenv("FEDAGG_ZERO_COPY_MAX");
+    return v ? int64_t(atoll(v)) : kZeroCopyBytes;
+  }();
+  const bool zero_copy = bytes <= zc_max;
   if (int rc = grow_pinned(&cx.stage, &cx.stage_n, size_t(elems))) return rc;
   if (int rc = grow_pinned(&cx.res, &cx.res_n, size_t(L))) return rc;
   if (!cx.flag) {
@@ -2318,9 +2406,9 @@ int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes, const 
       return set_error(FEDAGG_EINVAL, "fedagg_host_round_f32: pinned memory not device-mapped");
     rows = stage_d;
   } else {
-    // ~2 MiB of clients per DMA: packing the next group overlaps the copy of
+    // ~1 MiB of clients per DMA: packing the next group overlaps the copy of
     // this one
-    const int per = int(std::max<int64_t>(1, (int64_t(2) << 20) / (L * 4)));
+    const int per = int(std::max<int64_t>(1, (int64_t(1) << 20) / (L * 4)));
     for (int i0 = 0; i0 < K; i0 += per) {
       const int i1 = std::min<int>(K, i0 + per);
       pack(i0, i1);
@@ -2331,7 +2419,7 @@ int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes, const 
     rows = cx.rows;
   }
   const unsigned int seq = ++cx.seq == 0 ? ++cx.seq : cx.seq;  // never 0, the word's initial value
-  const unsigned grid = unsigned((L + kRoundBlock - 1) / kRoundBlock);
+  const unsigned grid = unsigned((L / 4 + kRoundBlock - 1) / kRoundBlock);
   hipLaunchKernelGGL(host_round_kernel, dim3(grid), dim3(kRoundBlock), 0, st, rows, L, int(K), iw, res_d,
                      cx.counter, flag_d, seq);
   if (int rc = check_launch("fedagg_host_round_f32")) return rc;

@@ -28,6 +28,17 @@ Supported server optimizers (OptRepo names, optrepo.py:10); parameters are fp32:
           construction again (FedAdagrad).  Fused like Adam's
           (fedagg_wsum_fedopt_adagrad_f32); state_sum is bit-identical to
           torch's, parameters carry the same sqrt caveat.
+  "adamw" torch.optim.AdamW with its defaults (betas (0.9, 0.999), eps 1e-8,
+          weight_decay 0.01 unless server_weight_decay says otherwise):
+          Adam with the parameter scaled by fl32(1 - lr*wd) first
+          (fedagg_wsum_fedopt_adamw_f32); moments bit-identical to torch,
+          parameters with Adam's sqrt caveat.
+  "rmsprop" torch.optim.RMSprop with its defaults (alpha 0.99, eps 1e-8,
+          momentum 0, not centered, weight_decay 0)
+          (fedagg_wsum_fedopt_rmsprop_f32); square_avg bit-identical to
+          torch, parameters with the sqrt caveat.
+Any other OptRepo name, and weight decay / momentum / centered variants of
+these, raise NotImplementedError.
 
 Device layout: the round's updates sit in a ClientBucket; the global model
 and the momentum buffers are flat fp32 vectors with the bucket's fp32 layout.
@@ -46,19 +57,32 @@ import torch
 from . import kernels as kn
 from .bucket import ClientBucket
 
+FUSED_OPTIMIZERS = ("sgd", "adam", "adamw", "adagrad", "rmsprop")
+
+
+def _weight_decay(optimizer: str, weight_decay: Optional[float]) -> float:
+    """torch's default weight decay of each fused optimizer; AdamW's is the
+    only one the fused steps apply (decoupled), the others must stay 0."""
+    if optimizer == "adamw":
+        return 0.01 if weight_decay is None else float(weight_decay)
+    if weight_decay:
+        raise NotImplementedError(f"server_optimizer {optimizer!r} with weight_decay={weight_decay}: not fused")
+    return 0.0
+
 
 class FedOptServer:
     def __init__(self, global_state: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],
                  worker_num: int, server_optimizer: str = "sgd", server_lr: float = 1.0,
-                 server_momentum: float = 0.0, device=None):
+                 server_momentum: float = 0.0, device=None, server_weight_decay: Optional[float] = None):
         self.optimizer = server_optimizer.lower()
-        if self.optimizer not in ("sgd", "adam", "adagrad"):
-            raise NotImplementedError(f"server_optimizer {server_optimizer!r}: 'sgd' (with momentum), 'adam' and "
-                                      "'adagrad' are fused")
+        if self.optimizer not in FUSED_OPTIMIZERS:
+            raise NotImplementedError(f"server_optimizer {server_optimizer!r}: {FUSED_OPTIMIZERS} are fused")
         self.lr = float(server_lr)
         self.momentum = float(server_momentum) if self.optimizer == "sgd" else 0.0
-        # torch.optim.Adam / Adagrad defaults (sp/fedopt/fedopt_api.py:79-85 passes lr only)
+        # torch.optim defaults (sp/fedopt/fedopt_api.py:79-85 passes lr only)
         self.betas, self.eps = (0.9, 0.999), (1e-10 if self.optimizer == "adagrad" else 1e-8)
+        self.alpha = 0.99  # RMSprop
+        self.weight_decay = _weight_decay(self.optimizer, server_weight_decay)
         self.lr_decay = 0.0
         self.step_count = 0
         self.worker_num = worker_num
@@ -80,11 +104,12 @@ class FedOptServer:
                 if k in self.bucket.int_keys:
                     self._int_state[k] = t.detach().to(self.device).clone()
             self.mom = torch.zeros_like(self.global_flat[torch.float32]) if (f32 and self.momentum) else None
-            adam = f32 and self.optimizer == "adam"
+            adam = f32 and self.optimizer in ("adam", "adamw")
             self.exp_avg = torch.zeros_like(self.global_flat[torch.float32]) if adam else None
             self.exp_avg_sq = torch.zeros_like(self.global_flat[torch.float32]) if adam else None
-            adagrad = f32 and self.optimizer == "adagrad"
-            self.state_sum = torch.zeros_like(self.global_flat[torch.float32]) if adagrad else None
+            # Adagrad's state_sum, RMSprop's square_avg: both start at zero
+            acc = f32 and self.optimizer in ("adagrad", "rmsprop")
+            self.state_sum = torch.zeros_like(self.global_flat[torch.float32]) if acc else None
         self.first_step = True
         self._views: Optional["OrderedDict[str, torch.Tensor]"] = None
         self.runs: List[Tuple[bool, int, int]] = self._runs(f32) if f32 else []
@@ -136,7 +161,7 @@ class FedOptServer:
             f32 = self.global_flat.get(torch.float32)
             step = self.step_count + 1
             sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step) \
-                if self.optimizer == "adam" else None
+                if self.optimizer in ("adam", "adamw") else None
             if events is not None:
                 events[0].record()
             # torch's Adagrad: clr = lr / (1 + (step - 1) * lr_decay), in double
@@ -145,6 +170,13 @@ class FedOptServer:
                 if is_param and self.optimizer == "adagrad":
                     kn.wsum_fedopt_adagrad(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], clr, self.eps,
                                            True)
+                elif is_param and self.optimizer == "rmsprop":
+                    kn.wsum_fedopt_rmsprop(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], self.lr,
+                                           self.alpha, self.eps, True)
+                elif is_param and self.optimizer == "adamw":
+                    kn.wsum_fedopt_adamw(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
+                                         self.exp_avg_sq[lo:hi], sc, 1 - self.lr * self.weight_decay,
+                                         self.first_step, True)
                 elif is_param and sc is not None:
                     kn.wsum_fedopt_adam(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
                                         self.exp_avg_sq[lo:hi], sc, self.first_step, True)
@@ -195,6 +227,8 @@ class FedOptServer:
             return {"momentum_buffer": self.mom}
         if self.optimizer == "adagrad":
             return {"sum": self.state_sum}  # exists from construction in torch (initial_accumulator_value)
+        if self.optimizer == "rmsprop":
+            return {"square_avg": self.state_sum}  # created at the first step in torch
         return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
 
     def load_optimizer_state(self, state: Dict[str, object]) -> None:
@@ -242,9 +276,9 @@ class FedOptServer:
             tot += K * n * 4
             if not is_param:
                 tot += n * 4
-            elif self.optimizer == "adam":  # p read+write, exp_avg / exp_avg_sq written (+ read after step 1)
+            elif self.optimizer in ("adam", "adamw"):  # p read+write, exp_avg / exp_avg_sq written (+ read after step 1)
                 tot += 2 * n * 4 + (4 if not self.first_step else 2) * n * 4
-            elif self.optimizer == "adagrad":  # p and state_sum read and written
+            elif self.optimizer in ("adagrad", "rmsprop"):  # p and state_sum / square_avg read and written
                 tot += 4 * n * 4
             else:
                 tot += 2 * n * 4 + (2 * n * 4 if self.mom is not None and not self.first_step else

@@ -295,6 +295,31 @@ def wsum_fedopt_adagrad(d_ptrs: torch.Tensor, d_w, K: int, N: int, param: torch.
         flags, nat.stream_handle()), "wsum_fedopt_adagrad_f32")
 
 
+def wsum_fedopt_adamw(d_ptrs: torch.Tensor, d_w, K: int, N: int, param: torch.Tensor, exp_avg: torch.Tensor,
+                      exp_avg_sq: torch.Tensor, scalars: "ctypes.Array", decay: float, first_step: bool,
+                      aligned: bool) -> None:
+    """FedAvg of K fp32 sources fused with the server AdamW step (decay =
+    1 - lr * weight_decay, rounded to fp32 by ctypes as torch rounds it)."""
+    _require_cuda(param, "wsum_fedopt_adamw")
+    ok = aligned and all((t.data_ptr() & 15) == 0 for t in (param, exp_avg, exp_avg_sq))
+    flags = (nat.FEDAGG_ALIGNED16 if ok else 0) | (nat.FEDAGG_HOST_WEIGHTS if isinstance(d_w, HostWeights) else 0)
+    nat.check(nat.lib().fedagg_wsum_fedopt_adamw_f32(
+        d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+        ctypes.addressof(scalars), float(decay), int(first_step), flags, nat.stream_handle()),
+        "wsum_fedopt_adamw_f32")
+
+
+def wsum_fedopt_rmsprop(d_ptrs: torch.Tensor, d_w, K: int, N: int, param: torch.Tensor, square_avg: torch.Tensor,
+                        lr: float, alpha: float, eps: float, aligned: bool) -> None:
+    """FedAvg of K fp32 sources fused with the server RMSprop step."""
+    _require_cuda(param, "wsum_fedopt_rmsprop")
+    ok = aligned and all((t.data_ptr() & 15) == 0 for t in (param, square_avg))
+    flags = (nat.FEDAGG_ALIGNED16 if ok else 0) | (nat.FEDAGG_HOST_WEIGHTS if isinstance(d_w, HostWeights) else 0)
+    nat.check(nat.lib().fedagg_wsum_fedopt_rmsprop_f32(
+        d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), square_avg.data_ptr(), float(lr), float(alpha),
+        float(eps), flags, nat.stream_handle()), "wsum_fedopt_rmsprop_f32")
+
+
 def round_f32(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """fp32 -> bf16/f16 (RNE) on the device, in libfedagg (fedagg_round_f32)."""
     _require_cuda(x, "round_f32")

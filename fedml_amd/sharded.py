@@ -278,12 +278,16 @@ class ShardedFedOpt:
 
     def __init__(self, rows: torch.Tensor, length: int, global_flat: torch.Tensor, optimizer: str = "sgd",
                  lr: float = 1.0, momentum: float = 0.0, group=None, chunks: int = 8, reducer=None, stepper=None,
-                 buffers: Sequence[Tuple[int, int]] = ()):
+                 buffers: Sequence[Tuple[int, int]] = (), weight_decay: Optional[float] = None):
+        from .fedopt import FUSED_OPTIMIZERS, _weight_decay
+
         self.optimizer = optimizer.lower()
-        if self.optimizer not in ("sgd", "adam", "adagrad"):
-            raise NotImplementedError(f"server_optimizer {optimizer!r}: 'sgd', 'adam' and 'adagrad'")
+        if self.optimizer not in FUSED_OPTIMIZERS:
+            raise NotImplementedError(f"server_optimizer {optimizer!r}: {FUSED_OPTIMIZERS} are fused")
         self.lr, self.momentum = float(lr), float(momentum) if self.optimizer == "sgd" else 0.0
         self.betas, self.eps = (0.9, 0.999), (1e-10 if self.optimizer == "adagrad" else 1e-8)
+        self.alpha = 0.99
+        self.weight_decay = _weight_decay(self.optimizer, weight_decay)
         self.agg = ClientAxisAggregator(rows, length, group=group, chunks=chunks, reducer=reducer)
         self.stepper = stepper
         self.length = length
@@ -306,9 +310,14 @@ class ShardedFedOpt:
                     idx.append(torch.arange(base + x, base + y, dtype=torch.int64))
         self.buffer_idx = torch.cat(idx).to(dev) if idx else None
         z = lambda: torch.zeros(n, dtype=torch.float32, device=dev)  # noqa: E731
-        self.state = {"sgd": {"momentum_buffer": z()} if self.momentum else {},
-                      "adam": {"exp_avg": z(), "exp_avg_sq": z()} if self.optimizer == "adam" else {},
-                      "adagrad": {"sum": z()} if self.optimizer == "adagrad" else {}}[self.optimizer]
+        if self.optimizer == "sgd":
+            self.state = {"momentum_buffer": z()} if self.momentum else {}
+        elif self.optimizer in ("adam", "adamw"):
+            self.state = {"exp_avg": z(), "exp_avg_sq": z()}
+        elif self.optimizer == "adagrad":
+            self.state = {"sum": z()}
+        else:
+            self.state = {"square_avg": z()}
         self.step_count = 0
         if self.agg.on_gpu and stepper is None:
             self._src = kn.upload_i64([self.agg.shard.data_ptr()], dev)  # one source: the reduced shard
@@ -331,6 +340,13 @@ class ShardedFedOpt:
                 sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step)
                 kn.wsum_fedopt_adam(self._src, one, 1, n, self.param, self.state["exp_avg"],
                                     self.state["exp_avg_sq"], sc, first, True)
+            elif self.optimizer == "adamw":
+                sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step)
+                kn.wsum_fedopt_adamw(self._src, one, 1, n, self.param, self.state["exp_avg"],
+                                     self.state["exp_avg_sq"], sc, 1 - self.lr * self.weight_decay, first, True)
+            elif self.optimizer == "rmsprop":
+                kn.wsum_fedopt_rmsprop(self._src, one, 1, n, self.param, self.state["square_avg"], self.lr,
+                                       self.alpha, self.eps, True)
             else:
                 kn.wsum_fedopt_adagrad(self._src, one, 1, n, self.param, self.state["sum"], self.lr, self.eps, True)
         if self.buffer_idx is not None:  # buffers take the average (FedOptAggregator.py:126-130)

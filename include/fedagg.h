@@ -201,6 +201,31 @@ int fedagg_wsum_fedopt_adagrad_f32(const float* const* d_src, const float* d_w,
                                    float* d_sum, float clr, float eps,
                                    uint32_t flags, fedagg_stream_t stream);
 
+/* FedAvg fused with the server AdamW step (torch.optim.AdamW through
+ * OptRepo "adamw", sp/fedopt/optrepo.py:10-38, as FedOptAPI builds it with
+ * lr only, fedopt_api.py:78-85): Adam as fedagg_wsum_fedopt_adam_f32 on the
+ * gradient p_old - avg, with the parameter first scaled by
+ * decay = fl32(1 - lr * weight_decay) (decoupled weight decay):
+ *   p = fl(p_old * decay) + fl(-step_size * m) / denom. */
+int fedagg_wsum_fedopt_adamw_f32(const float* const* d_src, const float* d_w,
+                                 int32_t K, int64_t N, float* d_param,
+                                 float* d_exp_avg, float* d_exp_avg_sq,
+                                 const float* scalars6, float decay,
+                                 int32_t first_step, uint32_t flags,
+                                 fedagg_stream_t stream);
+
+/* FedAvg fused with the server RMSprop step (torch.optim.RMSprop, OptRepo
+ * "rmsprop", defaults momentum 0, centered False, weight_decay 0):
+ *   g = p_old - avg
+ *   square_avg = fma(fl(fl32(1 - alpha) * g), g, fl(square_avg * fl32(alpha)))
+ *   p = p_old + fl(fl(-lr * g) / fl(sqrt(square_avg) + eps))
+ * alpha is the Python float (double); square_avg starts at zero. */
+int fedagg_wsum_fedopt_rmsprop_f32(const float* const* d_src, const float* d_w,
+                                   int32_t K, int64_t N, float* d_param,
+                                   float* d_square_avg, float lr, double alpha,
+                                   float eps, uint32_t flags,
+                                   fedagg_stream_t stream);
+
 /* ---- Robust aggregation --------------------------------------------------- */
 
 /* Coordinate-wise median over K fp32 clients (the "wise_median" defense,
@@ -277,8 +302,8 @@ int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_of
  *   h_out   : T host fp32 buffers of numels[t] elements, written on return
  * The library packs the clients into pinned memory it keeps per device
  * (allocated on first use and grown when a bigger round arrives), reduces on
- * the device (the kernel reads rounds up to 1 MiB straight from pinned
- * memory; larger ones go up in one DMA), and copies the result out.
+ * the device (the kernel reads rounds up to 16 MiB straight from pinned
+ * memory; larger ones go up in pipelined DMAs), and copies the result out.
  * Synchronous (returns when h_out holds the result).  stream NULL runs it
  * on a non-blocking stream of the library's own (nothing on the caller's
  * streams is involved: host in, host out); a stream orders it after the

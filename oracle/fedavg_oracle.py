@@ -318,7 +318,7 @@ def adam_scalars(lr: float, beta1: float, beta2: float, eps: float, step: int) -
 
 
 def fedopt_adam(p_old: np.ndarray, avg: np.ndarray, m: np.ndarray | None, v: np.ndarray | None, lr: float,
-                step: int, betas=(0.9, 0.999), eps: float = 1e-8, sqrt: str = "torch"
+                step: int, betas=(0.9, 0.999), eps: float = 1e-8, sqrt: str = "torch", weight_decay: float = 0.0
                 ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """One server Adam step on one named parameter (sp/fedopt/fedopt_api.py:121-130,
     grad = p_old - avg as _set_model_global_grads :155-160).  Returns (p, m, v).
@@ -326,7 +326,11 @@ def fedopt_adam(p_old: np.ndarray, avg: np.ndarray, m: np.ndarray | None, v: np.
     sqrt="torch" uses torch's CPU sqrt, which is what the reference's
     exp_avg_sq.sqrt() runs (on this image an MKL VML routine that is NOT
     correctly rounded: ~0.6% of fp32 results are 1 ulp off); sqrt="ieee" uses
-    the correctly rounded sqrt the GPU kernel computes."""
+    the correctly rounded sqrt the GPU kernel computes.
+
+    weight_decay != 0 is torch.optim.AdamW (Adam with decoupled weight decay):
+    param.mul_(1 - lr * weight_decay) runs first, the gradient having been set
+    from the unscaled parameter, so p = fl(p_old * fl32(1 - lr*wd)) + step."""
     w1, b2, c2, bc2s, epsf, nss = (np.float32(x) for x in adam_scalars(lr, betas[0], betas[1], eps, step))
     p = np.ascontiguousarray(p_old, dtype=np.float32).reshape(-1).copy()
     a = np.ascontiguousarray(avg, dtype=np.float32).reshape(-1)
@@ -341,13 +345,15 @@ def fedopt_adam(p_old: np.ndarray, avg: np.ndarray, m: np.ndarray | None, v: np.
     else:
         raise ValueError(sqrt)
     denom = (s / bc2s) + epsf  # (exp_avg_sq.sqrt() / bias_correction2_sqrt).add_(eps)
+    if weight_decay:
+        p = (p * np.float32(1 - lr * weight_decay)).astype(np.float32)  # param.mul_(1 - lr * wd)
     p = (p + (nss * mm) / denom).astype(np.float32)  # addcdiv_: self + (value * t1) / t2
     return p, mm, vv
 
 
 def fedopt_adam_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str], raw_grad_list,
                       lr: float, state: Dict[str, Tuple[np.ndarray, np.ndarray]], step: int,
-                      sqrt: str = "torch") -> "OrderedDict[str, torch.Tensor]":
+                      sqrt: str = "torch", weight_decay: float = 0.0) -> "OrderedDict[str, torch.Tensor]":
     """One FedOptAPI round with server_optimizer="adam" (fedopt_api.py:121-130):
     FedAvg, Adam on named parameters (state carries exp_avg / exp_avg_sq across
     rounds, step is 1-based), averaged values for buffers."""
@@ -358,7 +364,8 @@ def fedopt_adam_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: 
     for k, t_old in global_sd.items():
         if k in param_names:
             m, v = state.get(k, (None, None))
-            p, m, v = fedopt_adam(to_np(t_old).ravel(), to_np(avg[k]).ravel(), m, v, lr, step, sqrt=sqrt)
+            p, m, v = fedopt_adam(to_np(t_old).ravel(), to_np(avg[k]).ravel(), m, v, lr, step, sqrt=sqrt,
+                                  weight_decay=weight_decay)
             state[k] = (m, v)
             out[k] = torch.from_numpy(p).reshape(t_old.shape)
         else:
@@ -404,6 +411,51 @@ def fedopt_adagrad_round(global_sd: "OrderedDict[str, torch.Tensor]", param_name
     for k, t_old in global_sd.items():
         if k in param_names:
             p, state[k] = fedopt_adagrad(to_np(t_old).ravel(), to_np(avg[k]).ravel(), state.get(k), lr, sqrt=sqrt)
+            out[k] = torch.from_numpy(p).reshape(t_old.shape)
+        else:
+            out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)
+    return out
+
+
+def fedopt_rmsprop(p_old: np.ndarray, avg: np.ndarray, sq: np.ndarray | None, lr: float, alpha: float = 0.99,
+                   eps: float = 1e-8, sqrt: str = "torch") -> Tuple[np.ndarray, np.ndarray]:
+    """One server RMSprop step on one named parameter (torch.optim.RMSprop's
+    single-tensor CPU path with momentum 0, not centered, weight_decay 0, as
+    FedOptAPI builds it with lr only).  Returns (p, square_avg):
+      sq  = fma(fl(fl32(1-alpha) * g), g, fl(sq * fl32(alpha)))   mul_(alpha).addcmul_(g, g, value=1-alpha)
+      avg = fl(sqrt(sq) + eps)                                      sqrt().add_(eps)
+      p   = fl(p + fl(fl(-lr * g) / avg))                           addcdiv_(g, avg, value=-lr)
+    The accumulator update is the one Adam's exp_avg_sq takes (same torch
+    kernels), so the C oracle's moment routine computes it."""
+    p = np.ascontiguousarray(p_old, dtype=np.float32).reshape(-1).copy()
+    a = np.ascontiguousarray(avg, dtype=np.float32).reshape(-1)
+    ss = np.zeros_like(p) if sq is None else np.ascontiguousarray(sq, dtype=np.float32).reshape(-1).copy()
+    unused = np.zeros_like(p)
+    clib().oracle_adam_moments_f32(p.ctypes.data, a.ctypes.data, unused.ctypes.data, ss.ctypes.data, p.size,
+                                   0.0, float(np.float32(alpha)), float(np.float32(1 - alpha)))
+    g = (p - a).astype(np.float32)
+    if sqrt == "torch":
+        r = torch.from_numpy(ss).sqrt().numpy()
+    elif sqrt == "ieee":
+        r = np.sqrt(ss)
+    else:
+        raise ValueError(sqrt)
+    d = (r + np.float32(eps)).astype(np.float32)
+    p = (p + (np.float32(-lr) * g) / d).astype(np.float32)
+    return p, ss
+
+
+def fedopt_rmsprop_round(global_sd: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str], raw_grad_list,
+                         lr: float, state: Dict[str, np.ndarray], sqrt: str = "torch"
+                         ) -> "OrderedDict[str, torch.Tensor]":
+    """One FedOptAPI round with server_optimizer="rmsprop" (fedopt_api.py:121-130)."""
+    class _A:
+        federated_optimizer = "FedAvg"
+    avg = agg(_A(), raw_grad_list)
+    out = OrderedDict()
+    for k, t_old in global_sd.items():
+        if k in param_names:
+            p, state[k] = fedopt_rmsprop(to_np(t_old).ravel(), to_np(avg[k]).ravel(), state.get(k), lr, sqrt=sqrt)
             out[k] = torch.from_numpy(p).reshape(t_old.shape)
         else:
             out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)

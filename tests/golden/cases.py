@@ -122,6 +122,16 @@ FEDOPT_ADAGRAD_CASES = [
     dict(name="fedopt_adagrad_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=96, optimizer="adagrad"),
     dict(name="fedopt_adagrad_lr1e-1_small", K=5, rounds=3, lr=0.1, model="small", seed=97, optimizer="adagrad"),
 ]
+# Server AdamW (OptRepo "adamw": torch defaults, weight_decay 0.01) and
+# RMSprop (OptRepo "rmsprop": alpha 0.99, eps 1e-8, no momentum)
+FEDOPT_ADAMW_CASES = [
+    dict(name="fedopt_adamw_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=98, optimizer="adamw"),
+    dict(name="fedopt_adamw_lr1_small", K=3, rounds=3, lr=1.0, model="small", seed=99, optimizer="adamw"),
+]
+FEDOPT_RMSPROP_CASES = [
+    dict(name="fedopt_rmsprop_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=100, optimizer="rmsprop"),
+    dict(name="fedopt_rmsprop_lr1e-3_small", K=5, rounds=3, lr=0.001, model="small", seed=101, optimizer="rmsprop"),
+]
 FEDOPT_CASES = [
     dict(name="fedopt_sgd_m09_lr1", K=4, rounds=3, lr=1.0, momentum=0.9, seed=90),
     dict(name="fedopt_sgd_m09_lr1e-3", K=4, rounds=3, lr=0.001, momentum=0.9, seed=91),

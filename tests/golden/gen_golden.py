@@ -210,6 +210,14 @@ def run_fedopt_adam_case(FedOptAPI, spec):
         server_optimizer = spec.get("optimizer", "adam")
         server_lr = spec["lr"]
 
+    if A.server_optimizer == "adamw":
+        # torch.optim.AdamW subclasses Adam, so OptRepo (direct subclasses of
+        # Optimizer only, optrepo.py:10) cannot name it and the reference
+        # raises KeyError.  The fixture runs the same FedOptAPI flow with AdamW
+        # registered, i.e. torch's AdamW as FedOptAPI would drive it.
+        from fedml.simulation.sp.fedopt.optrepo import OptRepo
+
+        OptRepo.repo.setdefault("adamw", torch.optim.AdamW)
     api = object.__new__(FedOptAPI)
     api.args = A()
     api.model_trainer = Trainer(model)
@@ -234,7 +242,8 @@ def run_fedopt_adam_case(FedOptAPI, spec):
             arrays[f"r{r}:{k}"] = tensor_bytes(t)
         st = api.opt.state_dict()["state"]
         for j, name in enumerate(cases.FEDOPT_PARAMS):
-            for buf in (("sum",) if A.server_optimizer == "adagrad" else ("exp_avg", "exp_avg_sq")):
+            for buf in {"adagrad": ("sum",), "rmsprop": ("square_avg",)}.get(A.server_optimizer,
+                                                                              ("exp_avg", "exp_avg_sq")):
                 arrays[f"r{r}:{buf}:{name}"] = tensor_bytes(st[j][buf])
     save(spec["name"], meta, arrays)
 
@@ -287,7 +296,8 @@ def main(only=()):
         run_fedopt_case(FedOptAggregator, spec)
         print("wrote", spec["name"])
     FedOptAPI = import_sp_fedopt()
-    for spec in filter(want, cases.FEDOPT_ADAM_CASES + cases.FEDOPT_ADAGRAD_CASES):
+    for spec in filter(want, cases.FEDOPT_ADAM_CASES + cases.FEDOPT_ADAGRAD_CASES + cases.FEDOPT_ADAMW_CASES
+                       + cases.FEDOPT_RMSPROP_CASES):
         run_fedopt_adam_case(FedOptAPI, spec)
         print("wrote", spec["name"])
     Median, Trimmed = import_defenses()

@@ -284,3 +284,97 @@ def test_sharded_fedopt_single_rank_matches_fused_server(opt, cuda_device):
         sh.aggregate([n / sum(ns) for n in ns])
         torch.cuda.synchronize()
         gu.assert_same(sh.gather_params().cpu(), srv.global_flat[torch.float32][:L].cpu(), f"{opt} round {r}")
+
+
+def _state_for(opt, arrays, r, names):
+    """The reference optimizer's state after round r (r = -1: before the first step)."""
+    st = {"step": r + 1}
+    if r < 0:
+        return st
+    bufs = ("square_avg",) if opt == "rmsprop" else ("exp_avg", "exp_avg_sq")
+    for b in bufs:
+        st[b] = OrderedDict((k, torch.from_numpy(arrays[f"r{r}:{b}:{k}"].copy())) for k in names)
+    return st
+
+
+@pytest.mark.parametrize("spec", cases.FEDOPT_RMSPROP_CASES + cases.FEDOPT_ADAMW_CASES, ids=lambda s: s["name"])
+def test_fedopt_rmsprop_adamw_match_reference(spec, cuda_device):
+    """Each round of FedOptAPI's server RMSprop (the reference's own flow) and
+    AdamW (the same flow with torch.optim.AdamW registered), started from the
+    fixture's state of the previous round: optimizer state and buffers
+    bit-identical to torch; parameters bit-identical to the oracle with an
+    IEEE sqrt and within 1 ulp + 2^-21 |step| of torch (CPU sqrt)."""
+    opt = spec["optimizer"]
+    meta, arrays = gu.load(spec["name"])
+    names = cases.FEDOPT_PARAMS
+    init = cases.fedopt_global_init(spec)
+    prev = OrderedDict((k, gu.to_tensor(arrays[f"init:{k}"], str(t.dtype).replace("torch.", ""), t.shape))
+                       for k, t in init.items())
+    exact = total = 0
+    for r in range(spec["rounds"]):
+        server = FedOptServer(prev, names, spec["K"], opt, spec["lr"], 0.0, cuda_device)
+        server.load_optimizer_state(_state_for(opt, arrays, r - 1, names))
+        raw = cases.fedopt_round_inputs(spec, prev, r)
+        assert fingerprint(raw) == meta["rounds"][r]["in_sha256"]
+        for i, (n, d) in enumerate(raw):
+            server.add_local_trained_result(i, d, n)
+        out = OrderedDict((k, t.cpu().clone()) for k, t in server.aggregate().items())
+        st = server.optimizer_state()
+        gold = _state_for(opt, arrays, r, names)
+        for b in [x for x in gold if x != "step"]:
+            for k in names:
+                gu.assert_same(st[b][k].cpu(), gold[b][k].reshape(st[b][k].shape), f"r{r} {b} {k}")
+        prev_state = _state_for(opt, arrays, r - 1, names)
+        if opt == "rmsprop":
+            ostate = {k: prev_state["square_avg"][k].numpy().reshape(-1) for k in names} if r else {}
+            exp = orc.fedopt_rmsprop_round(prev, names, raw, spec["lr"], ostate, sqrt="ieee")
+        else:
+            ostate = {k: (prev_state["exp_avg"][k].numpy().reshape(-1), prev_state["exp_avg_sq"][k].numpy().reshape(-1))
+                      for k in names} if r else {}
+            exp = orc.fedopt_adam_round(prev, names, raw, spec["lr"], ostate, r + 1, sqrt="ieee", weight_decay=0.01)
+        for k, t in out.items():
+            gu.assert_same(t, exp[k], f"r{r} oracle {k}")
+            e = gu.to_tensor(arrays[f"r{r}:{k}"], str(t.dtype).replace("torch.", ""), t.shape)
+            if k in names:
+                step = (e.double() - prev[k].double()).abs()
+                tol = torch.from_numpy(np.spacing(np.abs(e.numpy()))).double() + step * 2.0 ** -21
+                assert ((t.double() - e.double()).abs() <= tol).all(), f"r{r} {k}"
+                exact += int((_bits(t) == _bits(e)).sum())
+                total += t.numel()
+            else:
+                gu.assert_same(t, e, f"r{r} {k}")
+        prev = OrderedDict((k, gu.to_tensor(arrays[f"r{r}:{k}"], str(t.dtype).replace("torch.", ""), t.shape))
+                           for k, t in init.items())
+    assert exact >= 0.98 * total, (exact, total)
+
+
+@pytest.mark.parametrize("opt", ["rmsprop", "adamw"])
+@pytest.mark.parametrize("N", [262_147, 5_000_011])
+def test_fused_rmsprop_adamw_vs_oracle_large(opt, N, cuda_device):
+    """The fused RMSprop / AdamW launches with a ragged tail (small-tile and
+    mid-tile configurations), 3 rounds, every element bit-exact against the
+    oracle (IEEE sqrt): state and parameters."""
+    K = 10
+    g = torch.Generator(device=cuda_device).manual_seed(N % 103)
+    rows = torch.randn(K, (N + 63) // 64 * 64, generator=g, device=cuda_device) * 0.02
+    p = torch.randn(N, generator=g, device=cuda_device) * 0.02
+    s1, s2 = torch.zeros(N, device=cuda_device), torch.zeros(N, device=cuda_device)
+    ws = [(i + 3.0) for i in range(K)]
+    ws = [w / sum(ws) for w in ws]
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    hp, h1, h2 = p.cpu().numpy(), None, None
+    lr = 0.01
+    for r in range(3):
+        avg = orc.wsum([rows[i, :N].cpu() for i in range(K)], ws).numpy()
+        wt = kn.weights_for(ws, torch.float32, cuda_device)
+        if opt == "rmsprop":
+            kn.wsum_fedopt_rmsprop(d_ptrs, wt, K, N, p, s1, lr, 0.99, 1e-8, True)
+            hp, h1 = orc.fedopt_rmsprop(hp, avg, h1, lr, sqrt="ieee")
+        else:
+            kn.wsum_fedopt_adamw(d_ptrs, wt, K, N, p, s1, s2, kn.adam_scalars(lr, 0.9, 0.999, 1e-8, r + 1),
+                                 1 - lr * 0.01, r == 0, True)
+            hp, h1, h2 = orc.fedopt_adam(hp, avg, h1, h2, lr, r + 1, sqrt="ieee", weight_decay=0.01)
+            gu.assert_same(s2.cpu(), torch.from_numpy(h2), f"r{r} exp_avg_sq")
+        gu.assert_same(s1.cpu(), torch.from_numpy(h1), f"r{r} state")
+        gu.assert_same(p.cpu(), torch.from_numpy(hp), f"r{r} param")
+        rows.mul_(1.01)
