@@ -67,7 +67,7 @@ def kernels(co: bytes):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r02_kernel_resources.tsv")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r02", "kernel_resources.tsv")
     ks = sorted(kernels(code_object()), key=lambda k: k["kernel"])
     cols = ["kernel", "vgpr_count", "agpr_count", "occupancy", "sgpr_count", "vgpr_spill_count",
             "sgpr_spill_count", "private_segment_fixed_size", "group_segment_fixed_size"]
