@@ -1,6 +1,6 @@
 """Resource usage of every kernel that SHIPS in fedml_amd/lib/libfedagg.so (tool only).
 
-    python tools/kernel_resources.py [out.tsv]      # default profiles/r02_kernel_resources.tsv
+    python tools/kernel_resources.py [out.tsv]      # default profiles/r02/kernel_resources.tsv
 
 Reads the gfx950 code object out of the library's offload bundle and its
 AMDGPU metadata note (llvm-readelf --notes): per kernel the VGPR / AGPR / SGPR
