@@ -330,9 +330,7 @@ def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDic
             t2d = {c: np.frombuffer(t, dtype=np.int64).reshape(-1, K) for c, t in tables.items()}
             for i in range(K):
                 bucket.put_from_table(i, t2d, dicts[i], 1)
-        outs = bucket.new_outputs()
-        bucket.reduce_into(outs, weights)
-        return bucket.to_host(outs)
+        return bucket.reduce_to_host(weights)  # reduce, D2H and host scatter overlapped
 
 
 def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights: Sequence[float], args
@@ -370,9 +368,7 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
             bucket = _cached_bucket(layout, K, device, _ACC_NAME[acc_mode])
             for i in range(K):
                 bucket.put(i, {k: per_key[k][i] for k in host_keys}, 1)
-            outs = bucket.new_outputs()
-            bucket.reduce_into(outs, weights)
-            results.update(bucket.to_host(outs))
+            results.update(bucket.reduce_to_host(weights))
 
     # ---- device-resident inputs: read in place --------------------------------
     if dev_keys:

@@ -19,8 +19,10 @@ client rows + 102 MB of result, well inside 288 GB; capacity can grow to about
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -86,6 +88,11 @@ class ClientBucket:
         self._staging: Dict[torch.dtype, dict] = {}
         self._result_host: Dict[torch.dtype, torch.Tensor] = {}
         self._pending = False
+        self._d2h: Optional[torch.cuda.Stream] = None
+        self._round_outs: Optional[Dict[torch.dtype, torch.Tensor]] = None
+        self._plans: Dict[tuple, list] = {}
+        self._pool: Optional[Dict[str, torch.Tensor]] = None
+        self._pool_thread = None
 
     # ---- ingest ---------------------------------------------------------------
 
@@ -491,4 +498,188 @@ class ClientBucket:
         for key, _, _ in self.entries:
             res[key] = per_key[key]
         return res
+
+    # ---- round end, pipelined ------------------------------------------------------
+
+    def reduce_to_host(self, weights: Sequence[float], num_clients: Optional[int] = None,
+                       into: Optional[Dict[str, torch.Tensor]] = None, chunks: int = 8,
+                       timings: Optional[dict] = None) -> "OrderedDict[str, torch.Tensor]":
+        """reduce_into + to_host with the three stages overlapped: the dominant
+        group is reduced in ``chunks`` column ranges on the current stream;
+        each range's D2H into pinned memory runs on a copy stream as soon as
+        its kernel ends, and the host scatters a range into the per-key
+        tensors as soon as its D2H lands, while the GPU reduces and copies the
+        next ones.  Serially the three are ~2 ms (HBM) + ~2 ms (PCIe) + the
+        scatter at config 3.  The per-key host tensors come from a pool
+        allocated and touched by a background thread after the previous call
+        (a fresh tensor pays a page fault per 4 KiB on first write, the bulk
+        of the scatter); ``into`` as in to_host.  Same results as
+        reduce_into + to_host (the chunked launches are the same per-element
+        chains)."""
+        K = num_clients if num_clients is not None else self.capacity
+        if not 1 <= K <= self.capacity:
+            raise ValueError(f"num_clients {K} outside [1, {self.capacity}]")
+        if len(weights) != K:
+            raise ValueError("one weight per client")
+        pooled = into is None
+        if pooled:
+            into = self._take_result_pool()
+        per_key = self._host_results(into)
+        dom = self.dominant_dtype()
+        g = self.groups[dom]
+        t = {} if timings is None else timings
+        with torch.cuda.device(self.device):
+            self.sync_ingest()
+            cur = torch.cuda.current_stream(self.device)
+            if self._d2h is None:
+                self._d2h = torch.cuda.Stream(self.device)
+            w32 = kn.weights_for(weights, torch.float32, self.device)
+            w64 = kn.weights_for(weights, torch.float64, self.device) if torch.float64 in self.groups else None
+            outs = self._round_outputs()
+            plan = self._chunk_plan(dom, chunks)
+            done = []
+            for lo, hi, d_ptrs, _ in plan:
+                kn.wsum_ptrs(dom, d_ptrs, w64 if dom == torch.float64 else w32, K, hi - lo, outs[dom][lo:hi], True,
+                             self.acc_mode)
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                self._d2h.wait_event(ev)
+                h = self._pinned_result(dom)
+                with torch.cuda.stream(self._d2h):
+                    h[lo:hi].copy_(outs[dom][lo:hi], non_blocking=True)
+                    fin = torch.cuda.Event()
+                    fin.record(self._d2h)
+                done.append(fin)
+            # the small groups behind the dominant one (e.g. ResNet's counters
+            # are promoted into it; bf16 models' fp32 keys are not)
+            minor = [dt for dt, gg in self.groups.items() if dt != dom and gg.length]
+            for dt in minor:
+                gg = self.groups[dt]
+                kn.wsum_ptrs(dt, gg.d_ptrs, w64 if dt == torch.float64 else w32, K, gg.length, outs[dt], True,
+                             self.acc_mode)
+            t["launched"] = True
+            dst = np.array([per_key[k].data_ptr() for k in g.keys], dtype=np.int64)
+            src = self._pinned_result(dom).data_ptr()
+            for (lo, hi, _, (idx, src_off, dst_off, nbytes)), fin in zip(plan, done):
+                fin.synchronize()
+                n = len(idx)
+                if n:
+                    dsts = np.ascontiguousarray(dst[idx] + dst_off)
+                    nat.check(nat.lib().fedagg_host_unpack(src, dsts.ctypes.data, src_off.ctypes.data,
+                                                           nbytes.ctypes.data, n, _PACK_THREADS), "host_unpack")
+            for dt in minor:
+                gg = self.groups[dt]
+                h = self._pinned_result(dt)
+                h[:gg.length].copy_(outs[dt][:gg.length])  # synchronous; small
+                self._unpack_group(gg, h, per_key)
+        if pooled:
+            self._refill_result_pool()
+        res = OrderedDict()
+        for key, _, _ in self.entries:
+            res[key] = per_key[key]
+        return res
+
+    def _round_outputs(self) -> Dict[torch.dtype, torch.Tensor]:
+        """Device outputs reused across reduce_to_host calls (results leave as
+        host tensors, so nothing holds them)."""
+        if self._round_outs is None:
+            self._round_outs = self.new_outputs()
+        return self._round_outs
+
+    def _pinned_result(self, dt: torch.dtype) -> torch.Tensor:
+        h = self._result_host.get(dt)
+        if h is None:
+            g = self.groups[dt]
+            h = self._result_host[dt] = torch.empty(max(g.length, 1), dtype=g.out_dtype).pin_memory()
+        return h
+
+    def _chunk_plan(self, dt: torch.dtype, chunks: int):
+        """[(lo, hi, pointer table at column lo, host scatter plan)] for the
+        group's columns in ``chunks`` ranges (bounds at multiples of 64K
+        elements, so every range start stays 16-byte aligned).  Cached."""
+        key = (dt, chunks)
+        plan = self._plans.get(key)
+        if plan is not None:
+            return plan
+        g = self.groups[dt]
+        L = g.length
+        step = max(1, -(-L // max(1, chunks)))
+        step = (step + 65535) // 65536 * 65536
+        bounds = [(lo, min(L, lo + step)) for lo in range(0, L, step)] or [(0, 0)]
+        offs = np.array(g.offsets, dtype=np.int64)
+        ends = offs + np.array(g.numels, dtype=np.int64)
+        oesz = torch.empty((), dtype=g.out_dtype).element_size()
+        plan = []
+        for lo, hi in bounds:
+            d_ptrs = g.d_ptrs + lo * g.esize
+            s = np.maximum(offs, lo)
+            e = np.minimum(ends, hi)
+            idx = np.nonzero(e > s)[0]
+            plan.append((lo, hi, d_ptrs, (idx, np.ascontiguousarray(s[idx] * oesz),
+                                          np.ascontiguousarray((s[idx] - offs[idx]) * oesz),
+                                          np.ascontiguousarray((e[idx] - s[idx]) * oesz))))
+        self._plans[key] = plan
+        return plan
+
+    def _host_results(self, into: Optional[Dict[str, torch.Tensor]]) -> Dict[str, torch.Tensor]:
+        per_key = {}
+        for g in self.groups.values():
+            for key, shape in zip(g.keys, g.shapes):
+                t = into.get(key) if into is not None else None
+                if t is None or t.dtype != g.out_dtype or not t.is_contiguous() or t.is_cuda \
+                        or tuple(t.shape) != tuple(shape):
+                    t = torch.empty(shape, dtype=g.out_dtype)
+                per_key[key] = t
+        return per_key
+
+    def _unpack_group(self, g, h: torch.Tensor, per_key: Dict[str, torch.Tensor]) -> None:
+        esz = h.element_size()
+        ts, offs, nbytes = [], [], []
+        for key, off, n in zip(g.keys, g.offsets, g.numels):
+            if n:
+                ts.append(per_key[key].data_ptr())
+                offs.append(off * esz)
+                nbytes.append(n * esz)
+        n = len(ts)
+        if n:
+            nat.check(nat.lib().fedagg_host_unpack(h.data_ptr(), (ctypes.c_void_p * n)(*ts),
+                                                   (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*nbytes),
+                                                   n, _PACK_THREADS), "host_unpack")
+
+    def _take_result_pool(self) -> Optional[Dict[str, torch.Tensor]]:
+        th = self._pool_thread
+        if th is None:
+            return None
+        th.join()
+        self._pool_thread = None
+        pool, self._pool = self._pool, None
+        return pool
+
+    def _refill_result_pool(self) -> None:
+        """Allocate and touch the next call's per-key host tensors on a
+        background thread (torch releases the GIL inside the fills)."""
+        import threading
+
+        shapes = [(k, s, g.out_dtype) for g in self.groups.values() for k, s in zip(g.keys, g.shapes)]
+
+        def work():
+            pool = {}
+            for k, s, dt in shapes:
+                pool[k] = torch.zeros(s, dtype=dt)
+            self._pool = pool
+
+        self._pool_thread = threading.Thread(target=work, name="fedagg-result-pool", daemon=True)
+        _POOL_THREADS.add(self._pool_thread)
+        self._pool_thread.start()
+
+
+# pool threads still filling at interpreter exit are joined first (a daemon
+# thread inside a torch op during finalisation can crash the exit)
+_POOL_THREADS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _join_pool_threads() -> None:
+    for th in list(_POOL_THREADS):
+        th.join()
 

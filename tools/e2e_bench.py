@@ -162,6 +162,34 @@ def main():
     assert all(host2[k] is host[k] for k in host)
     res["round_end_breakdown"] = bd
 
+    # the pipelined round end (reduce_to_host: chunked reduce, D2H on a copy
+    # stream, host scatter into pooled pre-touched tensors, all overlapped),
+    # timed like round_end above: after every put, through the last byte on the host
+    w = bucket.weights([n for n, _ in raw])
+    pl = []
+    for rep in range(4):  # rep 0 builds the chunk plan and the first pool
+        for i, (n, d) in enumerate(raw):
+            bucket.put(i, d, n)
+        t1 = time.perf_counter()
+        piped = bucket.reduce_to_host(w)
+        pl.append((time.perf_counter() - t1) * 1e3)
+        time.sleep(0.2)  # the next round's ingest time, in which the pool refills
+    res["round_end_pipelined_ms"] = sorted(pl[1:])[len(pl[1:]) // 2]
+    res["round_end_pipelined_ms_all"] = pl
+    sweep = {}
+    for ch in (4, 8, 16, 32):
+        ts = []
+        for rep in range(4):
+            for i, (n, d) in enumerate(raw):
+                bucket.put(i, d, n)
+            t1 = time.perf_counter()
+            bucket.reduce_to_host(w, chunks=ch)
+            ts.append((time.perf_counter() - t1) * 1e3)
+            time.sleep(0.2)
+        sweep[ch] = sorted(ts[1:])[1]
+    res["round_end_pipelined_chunk_sweep_ms"] = sweep
+    res["pipelined_equals_serial"] = bool(all(torch.equal(piped[k], host[k]) for k in host))
+
     # FAGG wire messages: ingest straight from the receive buffers
     from fedml_amd import wire
 
