@@ -14,7 +14,11 @@ import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "fedagg.hip")
+# every translation unit of libfedagg.so: compiled to objects separately (an
+# unchanged unit is not recompiled), then linked
+SRCS = [SRC, os.path.join(HERE, "csrc", "robust.hip")]
 OUT_DIR = os.path.join(HERE, "lib")
+OBJ_DIR = os.path.join(OUT_DIR, "obj")
 OUT = os.path.join(OUT_DIR, "libfedagg.so")
 WALKER_SRC = os.path.join(HERE, "csrc", "walker.cpp")
 WALKER_OUT = os.path.join(OUT_DIR, "_fedagg_walker" + sysconfig.get_config_var("EXT_SUFFIX"))
@@ -32,7 +36,6 @@ HIPCC_FLAGS = [
     # IEEE division and sqrt (server Adam step); the HIP default, stated here
     "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-fPIC",
-    "-shared",
     "-Wall",
 ]
 
@@ -44,11 +47,21 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def needs_rebuild() -> bool:
-    if not os.path.exists(OUT):
+HEADER = os.path.join(HERE, "..", "include", "fedagg.h")
+
+
+def _obj(src: str) -> str:
+    return os.path.join(OBJ_DIR, os.path.splitext(os.path.basename(src))[0] + ".o")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
         return True
-    deps = [SRC, os.path.join(HERE, "..", "include", "fedagg.h"), __file__]
-    return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps if os.path.exists(d))
+    return any(os.path.getmtime(d) > os.path.getmtime(target) for d in deps if os.path.exists(d))
+
+
+def needs_rebuild() -> bool:
+    return _stale(OUT, SRCS + [HEADER, __file__])
 
 
 def build_walker(force: bool = False, verbose: bool = False) -> str:
@@ -79,9 +92,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
     build_walker(force=force, verbose=verbose)
     if not force and not needs_rebuild():
         return OUT
-    os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    objs = []
+    for src in SRCS:
+        obj = _obj(src)
+        if force or _stale(obj, [src, HEADER, __file__]):
+            tmp = obj + ".tmp.o"
+            cmd = [hipcc(), *HIPCC_FLAGS, "-c", "-o", tmp, src]
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+            os.replace(tmp, obj)
+        objs.append(obj)
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-o", tmp, SRC]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

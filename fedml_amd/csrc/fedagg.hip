@@ -2443,6 +2443,12 @@ int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes, const 
 
 const char* fedagg_last_error(void) { return g_last_error.c_str(); }
 
+// error reporting for the other translation unit (csrc/robust.hip); not in
+// the header, not exported from the library
+__attribute__((visibility("hidden"))) int fedagg_set_error_internal(int code, const char* msg) {
+  return set_error(code, msg);
+}
+
 int32_t fedagg_version(void) { return 1; }
 
 int fedagg_wsum_f32_variant(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float* d_out,

@@ -1,0 +1,323 @@
+// robust.hip — gfx950 kernels for FedML's distance-based robust aggregation
+// (the Krum / multi-Krum and norm-difference-clipping defenses), exported
+// through include/fedagg.h and linked into libfedagg.so beside fedagg.hip.
+//
+// What this replaces (python/fedml/core/security/):
+//   defense/krum_defense.py:47-60          K(K-1) torch norms of client differences
+//   defense/norm_diff_clipping_defense.py:20-54   one norm per client + the clipped rebuild
+//   common/utils.py:8-13, 24-27            vectorize_weight / compute_euclidean_distance
+//
+// Rows are K device pointers (client updates laid out as bucket rows); the
+// columns that count ("weight" keys, common/utils.py:16-21) arrive as a chunk
+// table of (start, length) pairs built on the host from the key segments.
+//
+//   fedagg_dist2_f32     out[i] = sum_e (x_i[e] - r[e])^2        (HBM-bound, one pass)
+//   fedagg_pairdist2_f32 out[i][j] = sum_e (x_i[e] - x_j[e])^2   (VALU-bound, packed fp32)
+//   fedagg_clip_diff_f32 y_i[e] = fl(fl(fl(x_i[e] - r[e]) / c_i) + r[e])
+//
+// Every difference is the fp32 difference the reference forms
+// (vec_local - vec_global, v1 - v2).  dist2 squares it exactly in fp64 and sums
+// in fp64: the exact sum up to fp64 rounding.  pairdist2 squares and sums in
+// packed fp32 over a stage of at most 64 columns (relative error ~sqrt(64)
+// ulp typical, 64 ulp at worst) and adds the stage sums in fp64: about the
+// accuracy of the reference's own fp32 torch.norm (~1e-7 relative).
+// Partial sums go to a workspace and are combined in a fixed order: results
+// are deterministic run to run.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/fedagg.h"
+
+extern "C" int fedagg_set_error_internal(int code, const char* msg);
+
+namespace {
+
+int rset(int code, const std::string& msg) { return fedagg_set_error_internal(code, msg.c_str()); }
+
+int rcheck(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return rset(static_cast<int>(e), std::string(what) + ": " + hipGetErrorString(e));
+  return FEDAGG_OK;
+}
+
+template <class T>
+__device__ __forceinline__ const T __attribute__((address_space(1)))* gptr(const T* p) {
+  return (const T __attribute__((address_space(1)))*)(p);
+}
+
+constexpr int kBS = 256;
+constexpr int kDistU = FEDAGG_DIST_CHUNK / kBS;  // columns per thread per chunk
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Per-client squared distance to a reference row.  Block (i, g): client i,
+// chunk group g (chunks g, g + G, ...).  blockIdx.x is the client so that the
+// K blocks reading the same reference chunk run back to back (the reference
+// row is then served from L2 / MALL, not re-read from HBM per client).
+__global__ __launch_bounds__(kBS) void dist2_kernel(const float* const* __restrict__ src, int K,
+                                                    const float* __restrict__ ref, const int64_t* __restrict__ chunks,
+                                                    int64_t n_chunks, int G, double* __restrict__ partial) {
+  const int i = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
+  const auto row = gptr(src[i]);
+  const auto r = ref ? gptr(ref) : nullptr;
+  double acc = 0.0;
+  for (int64_t c = g; c < n_chunks; c += G) {
+    const int64_t start = chunks[2 * c];
+    const int len = int(chunks[2 * c + 1]);
+    float x[kDistU], y[kDistU];
+#pragma unroll
+    for (int u = 0; u < kDistU; ++u) {
+      const int idx = t + u * kBS;
+      x[u] = idx < len ? __builtin_nontemporal_load(row + start + idx) : 0.f;
+      y[u] = (r && idx < len) ? r[start + idx] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kDistU; ++u) {
+      const float d = x[u] - y[u];  // the reference's fp32 difference
+      acc = __builtin_fma(double(d), double(d), acc);  // exact square, fp64 sum
+    }
+  }
+  __shared__ double red[kBS / 64];
+  acc = wave_sum(acc);
+  if ((t & 63) == 0) red[t >> 6] = acc;
+  __syncthreads();
+  if (t == 0) partial[int64_t(i) * G + g] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// out[i] = sum over g of partial[i][g], in g order (deterministic)
+__global__ void sum_rows_kernel(const double* __restrict__ partial, int rows, int G, double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  double s = 0.0;
+  for (int g = 0; g < G; ++g) s += partial[int64_t(i) * G + g];
+  out[i] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Pairwise squared distances.  The K x K pair matrix is cut into 64 x 64
+// client tiles (I <= J); a block owns one tile over the chunk group g.  Per
+// stage of 64 columns each wave stages 16 client rows of tile I (and of J) as
+// coalesced 256-B row segments, four rows at a time packed into one 16-byte
+// LDS write per lane: sX[column][client], the 4-client groups XOR-swizzled by
+// column so both the staging writes and the compute reads are bank-conflict
+// free.  Thread (ti, tj) then owns clients 4ti..4ti+3 of I x 4tj..4tj+3 of J:
+// per column one 16-byte LDS read per side and 16 squared differences, as 8
+// packed fp32 subtracts and 8 packed fp32 FMAs (v_pk_add_f32 / v_pk_fma_f32).
+// fp32 sums over one stage (<= 64 columns) are flushed into fp64
+// accumulators, which go to the workspace per block.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kPT = 64;      // clients per tile side
+constexpr int kStage = 64;   // columns per LDS stage
+
+__device__ __forceinline__ int swz(int c, int grp) { return c * kPT + ((grp ^ (c & 15)) << 2); }
+
+__device__ __forceinline__ void stage_tile(f32x4* __restrict__ s, const float* const* __restrict__ src, int K, int base,
+                                           int64_t col0, int w, int t) {
+  const int lane = t & 63, wave = t >> 6;
+  // wave handles client groups 4 wave .. 4 wave + 3 (16 clients), lane = column
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int grp = wave * 4 + q;
+    f32x4 v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cl = base + grp * 4 + k;
+      v[k] = (cl < K && lane < w) ? __builtin_nontemporal_load(gptr(src[cl]) + col0 + lane) : 0.f;
+    }
+    s[swz(lane, grp) >> 2] = v;
+  }
+}
+
+// one column of the thread's 4 x 4 pair block: acc[2k + h] holds pairs
+// (4ti + k, 4tj + 2h) and (4ti + k, 4tj + 2h + 1)
+__device__ __forceinline__ void pair_column(const f32x4* __restrict__ sA, const f32x4* __restrict__ sJ, int col,
+                                            int ti, int tj, f32x2 (&acc)[8]) {
+  const f32x4 a = sA[swz(col, ti) >> 2];
+  const f32x4 b = sJ[swz(col, tj) >> 2];
+  const f32x2 b01 = {b[0], b[1]}, b23 = {b[2], b[3]};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2 ak = {a[k], a[k]};
+    const f32x2 d0 = ak - b01, d1 = ak - b23;  // v_pk_add_f32 (neg, op_sel broadcast)
+    acc[2 * k] = __builtin_elementwise_fma(d0, d0, acc[2 * k]);  // v_pk_fma_f32
+    acc[2 * k + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * k + 1]);
+  }
+}
+
+// tile pair tp -> (a, b), a <= b, row-major over the upper triangle of T x T
+__device__ __forceinline__ int2 tile_of(int tp, int T) {
+  int a = 0;
+  while (tp >= T - a) {
+    tp -= T - a;
+    ++a;
+  }
+  return int2{a, a + tp};
+}
+
+__global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __restrict__ src, int K,
+                                                       const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
+                                                       double* __restrict__ partial) {
+  __shared__ f32x4 sA[kStage * kPT / 4];
+  __shared__ f32x4 sB[kStage * kPT / 4];
+  const int tp = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
+  const int2 tile = tile_of(tp, (K + kPT - 1) / kPT);
+  const int I = tile.x * kPT, J = tile.y * kPT;
+  const bool diag = tile.x == tile.y;
+  const f32x4* sJ = diag ? sA : sB;
+  const int ti = t >> 4, tj = t & 15;
+  double acc64[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc64[k] = 0.0;
+  for (int64_t c = g; c < n_chunks; c += G) {
+    const int64_t start = chunks[2 * c];
+    const int len = int(chunks[2 * c + 1]);
+    for (int s0 = 0; s0 < len; s0 += kStage) {
+      f32x2 acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
+      const int w = len - s0 < kStage ? len - s0 : kStage;
+      __syncthreads();  // the previous stage's reads are done
+      stage_tile(sA, src, K, I, start + s0, w, t);
+      if (!diag) stage_tile(sB, src, K, J, start + s0, w, t);
+      __syncthreads();
+      if (w == kStage) {  // full stage: unrolled so the LDS reads of 8 columns are in flight together
+#pragma unroll 8
+        for (int col = 0; col < kStage; ++col) pair_column(sA, sJ, col, ti, tj, acc);
+      } else {
+        for (int col = 0; col < w; ++col) pair_column(sA, sJ, col, ti, tj, acc);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc64[2 * k] += double(acc[k][0]);
+        acc64[2 * k + 1] += double(acc[k][1]);
+      }
+    }
+  }
+  // pair (4ti + k, 4tj + m) of the tile at acc64[4k + m]
+  double* out = partial + (int64_t(tp) * G + g) * (kPT * kPT);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) out[(4 * ti + k) * kPT + 4 * tj + m] = acc64[4 * k + m];
+}
+
+// D[a][b] and D[b][a] from the tiles' partials, summed over g in order
+__global__ void pair_finish_kernel(const double* __restrict__ partial, int G, int K, double* __restrict__ D) {
+  const int tp = blockIdx.y;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // pair index in the tile
+  if (e >= kPT * kPT) return;
+  const int2 tile = tile_of(tp, (K + kPT - 1) / kPT);
+  const int a = tile.x * kPT + e / kPT, b = tile.y * kPT + e % kPT;
+  if (a >= K || b >= K) return;
+  double s = 0.0;
+  for (int g = 0; g < G; ++g) s += partial[(int64_t(tp) * G + g) * (kPT * kPT) + e];
+  if (a == b) s = 0.0;
+  D[int64_t(a) * K + b] = s;
+  if (tile.x != tile.y) D[int64_t(b) * K + a] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Clipped rebuild (norm_diff_clipping_defense.py:38-54): y = (x - r) / c + r
+// in fp32 with the reference's three roundings (c = fl32 of the clip divisor;
+// torch divides an fp32 tensor by a Python scalar in fp32).
+__global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __restrict__ src,
+                                                        const float* __restrict__ ref, const float* __restrict__ div,
+                                                        int64_t N, float* const* __restrict__ dst) {
+  const int i = blockIdx.y;
+  const auto x = gptr(src[i]);
+  float* y = dst[i];
+  const float c = div[i];
+  const int64_t stride = int64_t(gridDim.x) * kBS;
+  for (int64_t e = int64_t(blockIdx.x) * kBS + threadIdx.x; e < N; e += stride) {
+    const float r = ref[e];
+    y[e] = (__builtin_nontemporal_load(x + e) - r) / c + r;
+  }
+}
+
+int grid_groups(int per_group_blocks, int64_t n_chunks, int64_t work_len, int64_t per_group_work) {
+  int64_t G = (4096 + per_group_blocks - 1) / per_group_blocks;
+  if (G > n_chunks) G = n_chunks;
+  if (per_group_work > 0 && G > work_len / per_group_work) G = work_len / per_group_work;
+  if (G > 65535) G = 65535;
+  return int(G < 1 ? 1 : G);
+}
+
+int pair_tiles(int K) { const int T = (K + kPT - 1) / kPT; return T * (T + 1) / 2; }
+
+}  // namespace
+
+extern "C" {
+
+int64_t fedagg_robust_work_len(int32_t kind, int32_t K, int64_t n_chunks) {
+  if (K < 1 || n_chunks < 0) return -1;
+  if (n_chunks == 0) return 0;
+  if (kind == FEDAGG_WORK_DIST2) return int64_t(K) * grid_groups(K, n_chunks, 0, 0);
+  if (kind == FEDAGG_WORK_PAIRDIST2) {
+    const int NT = pair_tiles(K);
+    return int64_t(NT) * grid_groups(NT, n_chunks, 0, 0) * (kPT * kPT);
+  }
+  return -1;
+}
+
+int fedagg_dist2_f32(const float* const* d_src, int32_t K, const float* d_ref, const int64_t* d_chunks,
+                     int64_t n_chunks, double* d_out, double* d_work, int64_t work_len, fedagg_stream_t stream) {
+  if (K < 1 || n_chunks < 0) return rset(FEDAGG_EINVAL, "fedagg_dist2_f32: K must be >= 1 and n_chunks >= 0");
+  if (!d_src || !d_out || (n_chunks > 0 && (!d_chunks || !d_work)))
+    return rset(FEDAGG_EINVAL, "fedagg_dist2_f32: null pointer");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_chunks == 0) {
+    if (hipMemsetAsync(d_out, 0, sizeof(double) * K, st) != hipSuccess) return rcheck("fedagg_dist2_f32");
+    return FEDAGG_OK;
+  }
+  if (work_len < K) return rset(FEDAGG_EINVAL, "fedagg_dist2_f32: workspace smaller than K doubles");
+  const int G = grid_groups(K, n_chunks, work_len, K);
+  hipLaunchKernelGGL(dist2_kernel, dim3(unsigned(K), unsigned(G)), dim3(kBS), 0, st, d_src, K, d_ref, d_chunks,
+                     n_chunks, G, d_work);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(unsigned((K + 255) / 256)), dim3(256), 0, st, d_work, K, G, d_out);
+  return rcheck("fedagg_dist2_f32");
+}
+
+int fedagg_pairdist2_f32(const float* const* d_src, int32_t K, const int64_t* d_chunks, int64_t n_chunks,
+                         double* d_out, double* d_work, int64_t work_len, fedagg_stream_t stream) {
+  if (K < 1 || n_chunks < 0) return rset(FEDAGG_EINVAL, "fedagg_pairdist2_f32: K must be >= 1 and n_chunks >= 0");
+  if (!d_src || !d_out || (n_chunks > 0 && (!d_chunks || !d_work)))
+    return rset(FEDAGG_EINVAL, "fedagg_pairdist2_f32: null pointer");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_chunks == 0) {
+    if (hipMemsetAsync(d_out, 0, sizeof(double) * K * K, st) != hipSuccess) return rcheck("fedagg_pairdist2_f32");
+    return FEDAGG_OK;
+  }
+  const int NT = pair_tiles(K);
+  if (work_len < int64_t(NT) * kPT * kPT)
+    return rset(FEDAGG_EINVAL, "fedagg_pairdist2_f32: workspace too small (fedagg_robust_work_len)");
+  const int G = grid_groups(NT, n_chunks, work_len, int64_t(NT) * kPT * kPT);
+  hipLaunchKernelGGL(pairdist_kernel, dim3(unsigned(NT), unsigned(G)), dim3(kBS), 0, st, d_src, K, d_chunks, n_chunks,
+                     G, d_work);
+  hipLaunchKernelGGL(pair_finish_kernel, dim3(unsigned(kPT * kPT / 256), unsigned(NT)), dim3(256), 0, st, d_work, G,
+                     K, d_out);
+  return rcheck("fedagg_pairdist2_f32");
+}
+
+int fedagg_clip_diff_f32(const float* const* d_src, int32_t K, const float* d_ref, const float* d_div, int64_t N,
+                         float* const* d_dst, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return rset(FEDAGG_EINVAL, "fedagg_clip_diff_f32: K must be >= 1 and N >= 0");
+  if (!d_src || !d_ref || !d_div || !d_dst) return rset(FEDAGG_EINVAL, "fedagg_clip_diff_f32: null pointer");
+  if (N == 0) return FEDAGG_OK;
+  int64_t gx = (N + kBS - 1) / kBS;
+  const int64_t cap = (8192 + K - 1) / K;
+  if (gx > cap) gx = cap < 1 ? 1 : cap;
+  hipLaunchKernelGGL(clip_diff_kernel, dim3(unsigned(gx), unsigned(K)), dim3(kBS), 0, static_cast<hipStream_t>(stream),
+                     d_src, d_ref, d_div, N, d_dst);
+  return rcheck("fedagg_clip_diff_f32");
+}
+
+}  // extern "C"

@@ -21,12 +21,38 @@ that are pure reductions over the client axis.
                 common/utils.py:213-228 trimmed_mean): clients sorted by their
                 sample count (compute_a_score), int(beta * K) dropped at each
                 end, then ordinary FedAvg (our kernel) on the survivors.
+
+"krum", "multikrum"
+                KrumDefense.defend_before_aggregation (krum_defense.py:28-60):
+                the K x K squared distances of the clients' weight vectors are
+                one fedagg_pairdist2_f32 launch; the scores (sum of the
+                K - f - 2 smallest), their fp32 argsort and the returned
+                sub-list of the ORIGINAL (sample_num, dict) tuples follow the
+                reference on the host (K numbers).
+
+"norm_diff_clipping"
+                NormDiffClippingDefense.defend_before_aggregation
+                (norm_diff_clipping_defense.py:20-54): every client's distance
+                to the global model is one fedagg_dist2_f32 launch, the clipped
+                weights (x - g) / max(1, norm / bound) + g one
+                fedagg_clip_diff_f32 launch; non-weight keys stay the client's
+                own tensors, as in the reference.
+
+Distances: the reference forms fp32 differences and takes an fp32 torch.norm
+(.item(), then ** 2 for Krum).  The kernels sum the exact squares of the same
+fp32 differences in fp64; the host rounds the root to fp32 as the reference's
+norm does.  torch's own fp32 reduction may land one ulp away from that, so a
+Krum selection matches the reference's except between clients whose fp32
+scores are within an ulp (exact ties, e.g. mirror-image clients, can go either
+way in the reference too: its reduction order depends on the thread count),
+and a clipped client's divisor can differ in its last bit.
 """
 from __future__ import annotations
 
 from collections import OrderedDict
 from typing import List, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from . import _native as nat
@@ -35,7 +61,11 @@ from .bucket import ClientBucket
 
 DEFENSE_WISE_MEDIAN = "wise_median"
 DEFENSE_TRIMMED_MEAN = "trimmed_mean"
-SUPPORTED = (DEFENSE_WISE_MEDIAN, DEFENSE_TRIMMED_MEAN)
+DEFENSE_KRUM = "krum"
+DEFENSE_MULTIKRUM = "multikrum"
+DEFENSE_NORM_DIFF_CLIPPING = "norm_diff_clipping"
+SUPPORTED = (DEFENSE_WISE_MEDIAN, DEFENSE_TRIMMED_MEAN, DEFENSE_KRUM, DEFENSE_MULTIKRUM, DEFENSE_NORM_DIFF_CLIPPING)
+BEFORE_AGGREGATION = (DEFENSE_TRIMMED_MEAN, DEFENSE_KRUM, DEFENSE_MULTIKRUM, DEFENSE_NORM_DIFF_CLIPPING)
 
 
 def is_weight_param(k: str) -> bool:
@@ -130,3 +160,164 @@ def trimmed_mean_before_aggregation(raw_client_grad_list: Sequence, beta: float)
     if beta > 1 / 2 or beta < 0:
         raise ValueError("the bound of beta is [0, 1/2)")
     return trimmed_mean(raw_client_grad_list, int(beta * len(raw_client_grad_list)))
+
+
+# ---- distance-based defenses (csrc/robust.hip) ---------------------------------
+
+def weight_chunks(group, chunk: int, device) -> Tuple[torch.Tensor, int]:
+    """Device (start, length) table of a row group's weight-key columns, runs
+    of adjacent keys merged, split into pieces of at most `chunk` columns."""
+    segs = []
+    for key, off, n in zip(group.keys, group.offsets, group.numels):
+        if n == 0 or not is_weight_param(key):
+            continue
+        if segs and segs[-1][0] + segs[-1][1] == off:
+            segs[-1][1] += n
+        else:
+            segs.append([off, n])
+    starts, lens = [], []
+    for off, n in segs:
+        st = np.arange(off, off + n, chunk, dtype=np.int64)
+        starts.append(st)
+        lens.append(np.minimum(chunk, off + n - st))
+    if not starts:
+        return torch.zeros(2, dtype=torch.int64, device=device), 0
+    tab = np.stack([np.concatenate(starts), np.concatenate(lens)], axis=1).ravel()
+    return kn.upload_i64(tab.tolist(), device), len(tab) // 2
+
+
+def _work(kind: int, K: int, n_chunks: int, device) -> torch.Tensor:
+    n = int(nat.lib().fedagg_robust_work_len(kind, K, n_chunks))
+    if n < 0:
+        raise nat.FedAggNativeError("fedagg_robust_work_len: bad sizes")
+    return torch.empty(max(n, 1), dtype=torch.float64, device=device)
+
+
+def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks: int, device) -> torch.Tensor:
+    """K x K fp64 squared distances of K fp32 device rows over the chunked
+    columns (fedagg_pairdist2_f32)."""
+    out = torch.empty((K, K), dtype=torch.float64, device=device)
+    work = _work(nat.WORK_PAIRDIST2, K, n_chunks, device)
+    nat.check(nat.lib().fedagg_pairdist2_f32(d_ptrs.data_ptr(), K, chunks.data_ptr(), n_chunks, out.data_ptr(),
+                                             work.data_ptr(), work.numel(), nat.stream_handle()), "pairdist2")
+    return out
+
+
+def dist2_rows(d_ptrs: torch.Tensor, K: int, ref: "torch.Tensor | None", chunks: torch.Tensor, n_chunks: int,
+               device) -> torch.Tensor:
+    """K fp64 squared distances of K fp32 device rows to `ref` (None: norms)
+    over the chunked columns (fedagg_dist2_f32)."""
+    out = torch.empty(K, dtype=torch.float64, device=device)
+    work = _work(nat.WORK_DIST2, K, n_chunks, device)
+    nat.check(nat.lib().fedagg_dist2_f32(d_ptrs.data_ptr(), K, ref.data_ptr() if ref is not None else None,
+                                         chunks.data_ptr(), n_chunks, out.data_ptr(), work.data_ptr(),
+                                         work.numel(), nat.stream_handle()), "dist2")
+    return out
+
+
+def fp32_norm(sq: float) -> float:
+    """The reference's `torch.norm(fp32 vector).item()`: an fp32 root."""
+    return float(np.float32(np.sqrt(sq)))
+
+
+def _weight_bucket(dicts: Sequence, what: str, device=None):
+    """ClientBucket of the clients' weight keys (vectorize_weight's keys, in
+    client 0's order) and its fp32 row group."""
+    wkeys = [k for k in dicts[0].keys() if is_weight_param(k)]
+    if not wkeys:
+        raise RuntimeError("torch.cat(): expected a non-empty list of Tensors")  # vectorize_weight on no keys
+    for d in dicts[1:]:
+        for k in wkeys:
+            d[k]  # KeyError for a missing key, as the reference's walk would fail
+    dts = {dicts[0][k].dtype for k in wkeys}
+    if dts != {torch.float32}:
+        raise NotImplementedError(f"{what} on the GPU takes fp32 weight keys (got {sorted(map(str, dts))})")
+    t0 = dicts[0][wkeys[0]]
+    dev = t0.device if t0.is_cuda else (torch.device(device) if device is not None else
+                                        torch.device("cuda", torch.cuda.current_device()))
+    layout = [(k, tuple(dicts[0][k].shape), torch.float32) for k in wkeys]
+    with torch.cuda.device(dev):
+        bucket = ClientBucket(layout, len(dicts), dev)
+        for i, d in enumerate(dicts):
+            bucket.put(i, {k: d[k] for k in wkeys}, 1)
+        bucket.sync_ingest()
+    return bucket, bucket.groups[torch.float32], wkeys, dev
+
+
+def krum_scores(D: np.ndarray, byzantine_client_num: int) -> list:
+    """KrumDefense._compute_krum_score (krum_defense.py:47-60) over the K x K
+    squared distances: each distance enters as the reference's
+    `norm.item() ** 2`, the K - f - 2 smallest are summed in ascending order."""
+    K = D.shape[0]
+    scores = []
+    for i in range(K):
+        dists = [fp32_norm(D[i, j]) ** 2 for j in range(K) if j != i]
+        dists.sort()
+        scores.append(sum(dists[0:K - byzantine_client_num - 2]))
+    return scores
+
+
+def krum_before_aggregation(raw_client_grad_list: Sequence, byzantine_client_num: int, krum_param_m: int = 1,
+                            device=None) -> list:
+    """KrumDefense.defend_before_aggregation (krum_defense.py:28-45): the
+    krum_param_m lowest-scoring clients' original tuples, in score order."""
+    num_client = len(raw_client_grad_list)
+    if not 2 * byzantine_client_num + 2 <= num_client - krum_param_m:
+        raise ValueError("byzantine_client_num conflicts with requirements in Krum: "
+                         "2 * byzantine_client_num + 2 < client number - krum_param_m")
+    bucket, g, _, dev = _weight_bucket([item[1] for item in raw_client_grad_list], "krum", device)
+    with torch.cuda.device(dev):
+        chunks, n_chunks = weight_chunks(g, nat.PAIR_CHUNK, dev)
+        D = pairdist2_rows(g.d_ptrs, num_client, chunks, n_chunks, dev).cpu().numpy()
+    scores = krum_scores(D, byzantine_client_num)
+    score_index = torch.argsort(torch.Tensor(scores)).tolist()[0:krum_param_m]
+    return [raw_client_grad_list[i] for i in score_index]
+
+
+def krum_param_m(args) -> int:
+    """KrumDefense.__init__ (krum_defense.py:19-25)."""
+    m = getattr(args, "krum_param_m", None)
+    return m if isinstance(m, int) else 1
+
+
+def norm_diff_clipping_before_aggregation(raw_client_grad_list: Sequence, global_model, norm_bound: float,
+                                          device=None) -> list:
+    """NormDiffClippingDefense.defend_before_aggregation
+    (norm_diff_clipping_defense.py:20-54): every client's weights pulled to
+    within norm_bound of the global model; new dicts, the client's own
+    tensors for non-weight keys."""
+    K = len(raw_client_grad_list)
+    if K == 0:
+        return []
+    dicts = [item[1] for item in raw_client_grad_list]
+    bucket, g, wkeys, dev = _weight_bucket(dicts, "norm_diff_clipping", device)
+    with torch.cuda.device(dev):
+        gb = ClientBucket([(k, tuple(dicts[0][k].shape), torch.float32) for k in wkeys], 1, dev)
+        gb.put(0, {k: global_model[k] for k in wkeys}, 1)
+        gb.sync_ingest()
+        ref = gb.groups[torch.float32].rows[0]
+        chunks, n_chunks = weight_chunks(g, nat.DIST_CHUNK, dev)
+        sq = dist2_rows(g.d_ptrs, K, ref, chunks, n_chunks, dev).cpu().numpy()
+        divs = [max(1, fp32_norm(s) / norm_bound) for s in sq]  # _get_clipped_norm_diff
+        d_div = kn.upload_f32(divs, dev)
+        out = torch.empty_like(g.rows)
+        d_dst = kn.upload_i64([out[i].data_ptr() for i in range(K)], dev)
+        nat.check(nat.lib().fedagg_clip_diff_f32(g.d_ptrs.data_ptr(), K, ref.data_ptr(), d_div.data_ptr(),
+                                                 g.rows.shape[1], d_dst.data_ptr(), nat.stream_handle()),
+                  "clip_diff")
+        if not dicts[0][wkeys[0]].is_cuda:
+            out = out.cpu()  # host clients get host tensors back, as the reference returns
+        else:
+            torch.cuda.current_stream().synchronize()  # the staging buckets go out of scope
+    pos = {k: j for j, k in enumerate(g.keys)}
+    new_list = []
+    for i, (sample_num, local_w) in enumerate(raw_client_grad_list):
+        clipped = OrderedDict()
+        for k, v in local_w.items():  # _get_clipped_weights (:44-54)
+            if is_weight_param(k):
+                j = pos[k]
+                clipped[k] = out[i, g.offsets[j]:g.offsets[j] + g.numels[j]].view(v.size())
+            else:
+                clipped[k] = v
+        new_list.append((sample_num, clipped))
+    return new_list

@@ -6,11 +6,12 @@ aggregate -> on_after_aggregation) and the default subclass of
 python/fedml/ml/aggregator/default_aggregator.py:12-23.
 
 ``aggregate`` routes to fedml_amd.agg_operator.FedMLAggOperator.agg, the GPU
-implementation of the reference's operator.  Two of FedML's defenses are
+implementation of the reference's operator.  Several of FedML's defenses are
 reductions over the client axis and run on the GPU too (fedml_amd.defense):
 ``defense_type`` "wise_median" (on aggregation) and "trimmed_mean" (before
 aggregation), dispatched exactly as FedMLDefender does
-(core/security/fedml_defender.py:131-171).  The other optional hooks (FHE,
+(core/security/fedml_defender.py:131-171); so do the distance-based
+"krum" / "multikrum" and "norm_diff_clipping" (before aggregation).  The other optional hooks (FHE,
 differential privacy, attacks, other defenses, contribution assessment) are
 outside this build's scope: disabled (FedML's default) they are the identity,
 as in the reference; enabling one raises NotImplementedError instead of
@@ -80,12 +81,22 @@ class ServerAggregator(ABC):
         pass
 
     def on_before_aggregation(self, raw_client_model_or_grad_list: List[Tuple[float, OrderedDict]]):
-        """server_aggregator.py:44-73 (FHE/DP/attacks disabled); the trimmed-mean
-        defense filters the list here (fedml_defender.py:134-161)."""
+        """server_aggregator.py:44-73 (FHE/DP/attacks disabled); the
+        before-aggregation defenses (trimmed mean, Krum / multi-Krum, norm-diff
+        clipping) rewrite the list here (fedml_defender.py:134-161)."""
         client_idxs = [i for i in range(len(raw_client_model_or_grad_list))]
-        if _defense(self.args) == dfn.DEFENSE_TRIMMED_MEAN:
+        dt = _defense(self.args)
+        dev = getattr(self.args, "fedagg_device", None)
+        if dt == dfn.DEFENSE_TRIMMED_MEAN:
             raw_client_model_or_grad_list = dfn.trimmed_mean_before_aggregation(
                 raw_client_model_or_grad_list, self.args.beta)
+        elif dt in (dfn.DEFENSE_KRUM, dfn.DEFENSE_MULTIKRUM):
+            raw_client_model_or_grad_list = dfn.krum_before_aggregation(
+                raw_client_model_or_grad_list, self.args.byzantine_client_num, dfn.krum_param_m(self.args), dev)
+        elif dt == dfn.DEFENSE_NORM_DIFF_CLIPPING:
+            # extra_auxiliary_info = the server's current model (server_aggregator.py:66-70)
+            raw_client_model_or_grad_list = dfn.norm_diff_clipping_before_aggregation(
+                raw_client_model_or_grad_list, self.get_model_params(), self.args.norm_bound, dev)
         return raw_client_model_or_grad_list, client_idxs  # no client is flagged malicious
 
     def aggregate(self, raw_client_model_or_grad_list: List[Tuple[float, OrderedDict]]):

@@ -251,6 +251,50 @@ int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K,
                   int64_t N, void* d_out, uint32_t flags,
                   fedagg_stream_t stream);
 
+/* Distance-based defenses (csrc/robust.hip).  Rows are K fp32 device
+ * pointers; the columns that count (FedML's vectorize_weight: every key but
+ * BatchNorm running stats and counters, core/security/common/utils.py:8-21)
+ * arrive as d_chunks, n_chunks (start, length) int64 pairs of row columns,
+ * each length <= the kernel's chunk size (FEDAGG_DIST_CHUNK for dist2,
+ * FEDAGG_PAIR_CHUNK for pairdist2).  Differences are the reference's fp32
+ * differences.  dist2 squares and sums them in fp64; pairdist2 squares and
+ * sums them in fp32 over stages of <= 64 columns and adds the stage sums in
+ * fp64 (relative error ~1e-7, the reference's own fp32 norm's order).
+ * Per-block partials sit in d_work and are combined in a fixed order: the
+ * results are deterministic.  d_work holds at least
+ * fedagg_robust_work_len(kind, K, n_chunks) doubles.
+ *
+ * fedagg_dist2_f32 replaces the per-client torch.norm(vec_local - vec_global)
+ * of NormDiffClippingDefense._get_clipped_norm_diff
+ * (defense/norm_diff_clipping_defense.py:38-42) and CClip's
+ * compute_euclidean_distance (cclip_defense.py:72-80):
+ *   d_out[i] = sum_e (src_i[e] - ref[e])^2   (fp64; ref NULL: plain norms).
+ *
+ * fedagg_pairdist2_f32 replaces KrumDefense._compute_krum_score's K(K-1)
+ * compute_euclidean_distance(v_i, v_j) (defense/krum_defense.py:47-60):
+ *   d_out[i*K + j] = sum_e (src_i[e] - src_j[e])^2   (fp64, symmetric, 0 on
+ *   the diagonal). */
+#define FEDAGG_DIST_CHUNK 2048
+#define FEDAGG_PAIR_CHUNK 256
+#define FEDAGG_WORK_DIST2 0
+#define FEDAGG_WORK_PAIRDIST2 1
+int64_t fedagg_robust_work_len(int32_t kind, int32_t K, int64_t n_chunks);
+int fedagg_dist2_f32(const float* const* d_src, int32_t K, const float* d_ref,
+                     const int64_t* d_chunks, int64_t n_chunks, double* d_out,
+                     double* d_work, int64_t work_len, fedagg_stream_t stream);
+int fedagg_pairdist2_f32(const float* const* d_src, int32_t K,
+                         const int64_t* d_chunks, int64_t n_chunks, double* d_out,
+                         double* d_work, int64_t work_len, fedagg_stream_t stream);
+
+/* The clipped rebuild of NormDiffClippingDefense (:38-54): over the first N
+ * columns of every row,
+ *   d_dst_i[e] = fl32( fl32( fl32(src_i[e] - ref[e]) / d_div[i] ) + ref[e] )
+ * with d_div[i] = fl32(max(1, norm_i / norm_bound)), the Python divisor torch
+ * applies to the fp32 difference vector (K device floats). */
+int fedagg_clip_diff_f32(const float* const* d_src, int32_t K, const float* d_ref,
+                         const float* d_div, int64_t N, float* const* d_dst,
+                         fedagg_stream_t stream);
+
 /* Secure aggregation in a finite field (LightSecAgg), numpy int64 semantics:
  * wrapping adds, floor modulo.  p > 0.
  *

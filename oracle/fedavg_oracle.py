@@ -546,8 +546,74 @@ def trimmed_mean(model_list, trimmed_num):
     return [(t[0], t[1]) for t in temp]
 
 
-def defended_agg(args, raw_grad_list):
-    """FedMLDefender flow for the two reduction defenses (fedml_defender.py:131-171)."""
+def weight_vector(params) -> np.ndarray:
+    """vectorize_weight (core/security/common/utils.py:8-13) of an fp32 model."""
+    return np.concatenate([to_np(v).astype(np.float32).ravel() for k, v in params.items() if _is_weight_param(k)])
+
+
+def dist2(a: np.ndarray, b: np.ndarray) -> float:
+    """Sum of the squares of the fp32 differences a - b (as the reference forms
+    them), exactly squared and summed in fp64."""
+    d = (a - b).astype(np.float32).astype(np.float64)
+    return float(np.dot(d, d))
+
+
+def fp32_norm(sq: float) -> float:
+    """torch.norm(fp32 vector).item(): the root rounded to fp32."""
+    return float(np.float32(np.sqrt(sq)))
+
+
+def krum_select(raw_grad_list, byzantine_client_num: int, krum_param_m: int = 1):
+    """KrumDefense.defend_before_aggregation (krum_defense.py:28-60): scores =
+    sum of the K - f - 2 smallest `norm(v_i - v_j).item() ** 2`, fp32 argsort,
+    the m best ORIGINAL tuples in score order.  Returns (list, scores)."""
+    K = len(raw_grad_list)
+    if not 2 * byzantine_client_num + 2 <= K - krum_param_m:
+        raise ValueError("byzantine_client_num conflicts with requirements in Krum: "
+                         "2 * byzantine_client_num + 2 < client number - krum_param_m")
+    vecs = [weight_vector(p) for _, p in raw_grad_list]
+    scores = []
+    for i in range(K):
+        ds = sorted(fp32_norm(dist2(vecs[i], vecs[j])) ** 2 for j in range(K) if j != i)
+        scores.append(sum(ds[0:K - byzantine_client_num - 2]))
+    order = torch.argsort(torch.Tensor(scores)).tolist()[0:krum_param_m]
+    return [raw_grad_list[i] for i in order], scores
+
+
+def norm_diff_clip(raw_grad_list, global_model, norm_bound: float):
+    """NormDiffClippingDefense.defend_before_aggregation
+    (norm_diff_clipping_defense.py:20-54): per client, d = fp32(local - global)
+    over the weight keys, divisor c = max(1, norm(d) / bound) taken as fp32,
+    weights = fp32(fp32(d / c) + global); other keys are the client's own."""
+    g = weight_vector(global_model)
+    out = []
+    for n, local in raw_grad_list:
+        v = weight_vector(local)
+        d = (v - g).astype(np.float32)
+        c = np.float32(max(1, fp32_norm(float(np.dot(d.astype(np.float64), d.astype(np.float64)))) / norm_bound))
+        clipped = (d / c).astype(np.float32)
+        new, idx = OrderedDict(), 0
+        for k, t in local.items():
+            if _is_weight_param(k):
+                m = t.numel()
+                gk = to_np(global_model[k]).astype(np.float32).ravel()
+                new[k] = torch.from_numpy((clipped[idx:idx + m] + gk).astype(np.float32)).view(t.size())
+                idx += m
+            else:
+                new[k] = t
+        out.append((n, new))
+    return out
+
+
+def defended_agg(args, raw_grad_list, global_model=None):
+    """FedMLDefender flow for the reduction and distance defenses
+    (fedml_defender.py:131-171), followed by the base FedAvg operator."""
+    if args.defense_type in ("krum", "multikrum"):
+        m = getattr(args, "krum_param_m", None)
+        sel, _ = krum_select(raw_grad_list, args.byzantine_client_num, m if isinstance(m, int) else 1)
+        return agg(args, sel)
+    if args.defense_type == "norm_diff_clipping":
+        return agg(args, norm_diff_clip(raw_grad_list, global_model, args.norm_bound))
     if args.defense_type == "wise_median":
         return coordinate_wise_median(raw_grad_list)
     if args.defense_type == "trimmed_mean":

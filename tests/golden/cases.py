@@ -259,8 +259,58 @@ class DefenseArgs(Args):
         super().__init__(spec)
         self.enable_defense = True
         self.defense_type = spec["defense"]
-        if "beta" in spec:
-            self.beta = spec["beta"]
+        for a in ("beta", "byzantine_client_num", "krum_param_m", "norm_bound"):
+            if a in spec:
+                setattr(self, a, spec[a])
+
+
+# Distance-based defenses (krum_defense.py, norm_diff_clipping_defense.py):
+# the reference's own classes, then the base FedAvg operator.  Inputs are the
+# usual base + 0.01 eps clients; "outliers" scales the listed clients' float
+# keys by 1 + factor (Byzantine-looking updates Krum should drop).
+DIST_KEYS = [["conv.weight", [64, 3, 7, 7], F32], ["bn.weight", [64], F32], ["bn.bias", [64], F32],
+             ["bn.running_mean", [64], F32], ["bn.running_var", [64], F32], ["bn.num_batches_tracked", [], I64],
+             ["fc.weight", [10, 640], F32], ["fc.bias", [10], F32]]
+DIST_CASES: List[Dict[str, Any]] = []
+
+
+def _dist(name, defense, K, keys, seed, **kw):
+    DIST_CASES.append(dict(name=name, defense=defense, optimizer="FedAvg", K=K, keys=keys, seed=seed, **kw))
+
+
+# python/tests/security/defense/test_krum.py: create_fake_model_list(20), f = 1, m = 1 / 2
+# (clients i * A: mirror-image clients tie exactly)
+_dist("krum_fake_k20", "krum", 20, None, 0, fake_model_list=True, byzantine_client_num=1)
+_dist("multikrum_fake_k20_m2", "multikrum", 20, None, 0, fake_model_list=True, byzantine_client_num=1,
+      krum_param_m=2)
+_dist("krum_resnet_mini_k10", "krum", 10, RESNET_MINI, 300, byzantine_client_num=2, outliers={3: 4.0, 7: -2.5})
+_dist("multikrum_resnet_mini_k12_m4", "multikrum", 12, RESNET_MINI, 301, byzantine_client_num=2, krum_param_m=4,
+      outliers={0: 3.0, 5: 2.0})
+_dist("multikrum_dist_k70_m5", "multikrum", 70, DIST_KEYS, 302, byzantine_client_num=6, krum_param_m=5,
+      outliers={1: 1.5, 20: 2.0, 64: -1.0, 69: 3.0})
+_dist("multikrum_dist_k130_m9", "multikrum", 130, DIST_KEYS[:3], 303, byzantine_client_num=10, krum_param_m=9,
+      outliers={2: 1.0, 66: 2.0, 128: -3.0})
+_dist("krum_bad_f", "krum", 6, RAGGED_F32[:4], 304, byzantine_client_num=2, expect_error=True)
+_dist("clip_resnet_mini_k8", "norm_diff_clipping", 8, RESNET_MINI, 310, norm_bound=2.94, outliers={2: 3.0})
+_dist("clip_dist_k16", "norm_diff_clipping", 16, DIST_KEYS, 311, norm_bound=9.083, outliers={0: 2.0, 9: -1.5})
+_dist("clip_dist_k16_all", "norm_diff_clipping", 16, DIST_KEYS, 313, norm_bound=0.5)
+_dist("clip_ragged_k5_none", "norm_diff_clipping", 5, [k for k in RAGGED_F32 if k[0] not in ("e", "big")], 312,
+      norm_bound=100.0)
+
+
+def dist_inputs(spec):
+    """(raw_grad_list, global_model) of a distance-defense case."""
+    if spec.get("fake_model_list"):
+        raw = fake_model_list(spec["K"])
+        return raw, copy.deepcopy(raw[0][1])
+    entries = _entries(spec["keys"])
+    raw = host_clients(entries, spec["K"], spec["seed"])
+    for i, f in spec.get("outliers", {}).items():
+        for k, t in raw[int(i)][1].items():
+            if t.is_floating_point():
+                t.mul_(1.0 + f)
+    glob = host_clients(entries, 1, spec["seed"] + 7)[0][1]
+    return raw, glob
 
 
 # LightSecAgg field arithmetic (core/mpc/lightsecagg.py, cross_silo/lightsecagg)

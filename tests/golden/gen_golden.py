@@ -64,6 +64,51 @@ def import_defenses():
     return CoordinateWiseMedianDefense, CoordinateWiseTrimmedMeanDefense
 
 
+def run_dist_case(FedMLAggOperator, spec):
+    """Krum / multi-Krum / norm-diff clipping through the reference's own
+    classes (krum_defense.py, norm_diff_clipping_defense.py), then the base
+    FedAvg operator.  Records the returned list (which input tuples Krum kept,
+    in order; every clipped dict), the reference's own Krum scores and
+    clipping norms, and the aggregated model."""
+    from fedml.core.security.common import utils as sec_utils
+    from fedml.core.security.defense.krum_defense import KrumDefense
+    from fedml.core.security.defense.norm_diff_clipping_defense import NormDiffClippingDefense
+
+    raw, glob = cases.dist_inputs(spec)
+    args = cases.DefenseArgs(spec)
+    meta = {"spec": spec, "in_sha256": fingerprint(raw), "error": None, "tuple": False}
+    arrays = {}
+    ids = [id(item) for item in raw]
+    try:
+        if spec["defense"] in ("krum", "multikrum"):
+            d = KrumDefense(args)
+            vecs = [sec_utils.vectorize_weight(p) for _, p in raw]
+            meta["ref_scores"] = [float(x) for x in d._compute_krum_score(vecs)]
+            out_list = d.defend_before_aggregation(raw, None)
+            meta["selected"] = [ids.index(id(item)) for item in out_list]
+        else:
+            d = NormDiffClippingDefense(args)
+            vg = sec_utils.vectorize_weight(glob)
+            meta["ref_norms"] = [float(torch.norm(sec_utils.vectorize_weight(p) - vg).item()) for _, p in raw]
+            out_list = d.defend_before_aggregation(raw, glob)
+            for i, (_, dct) in enumerate(out_list):
+                for k, t in dct.items():
+                    arrays[f"c{i}:{k}"] = tensor_bytes(t)
+            for k, t in glob.items():
+                arrays[f"g:{k}"] = tensor_bytes(t)
+        res = FedMLAggOperator.agg(args, out_list)
+    except Exception as e:
+        meta["error"] = type(e).__name__
+        save(spec["name"], meta, arrays)
+        return
+    meta["outputs"] = []
+    for k, t in res.items():
+        arrays[f"o0:{k}"] = tensor_bytes(t)
+        meta["outputs"].append({"group": 0, "key": k, "dtype": str(t.dtype).replace("torch.", ""),
+                                "shape": list(t.shape), "is_client0_tensor": False})
+    save(spec["name"], meta, arrays)
+
+
 def tensor_bytes(t: torch.Tensor) -> np.ndarray:
     t = t.detach().cpu().contiguous()
     if t.dtype == torch.bfloat16:
@@ -312,6 +357,9 @@ def main(only=()):
             def agg(raw, args=args):
                 return FedMLAggOperator.agg(args, Trimmed(args).defend_before_aggregation(raw, None))
         run_agg_case(FedMLAggOperator, spec, aggregate=agg)
+        print("wrote", spec["name"])
+    for spec in filter(want, cases.DIST_CASES):
+        run_dist_case(FedMLAggOperator, spec)
         print("wrote", spec["name"])
     for spec in filter(want, cases.SECAGG_CASES):
         run_secagg_case(spec)

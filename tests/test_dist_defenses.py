@@ -1,0 +1,149 @@
+"""Distance-based defenses (Krum / multi-Krum, norm-diff clipping), CPU side:
+the oracle against the reference's own outputs (tests/golden, made by running
+KrumDefense / NormDiffClippingDefense + FedMLAggOperator.agg), the chunk-table
+builder, and the C ABI's argument checks (no GPU needed).
+
+Tolerances, stated once: the reference takes an fp32 torch.norm of the fp32
+difference vector; the oracle (and the kernels) sum the exact squares of the
+same fp32 differences in fp64 and round the root to fp32.  Krum scores agree
+to 1e-6 relative; the selection is the reference's exactly unless two fp32
+scores tie within that (mirror-image clients of the fake model list); a
+clipping divisor can differ in its last bit, so clipped weights agree to
+2^-21 (|w| + |g|) per element (the divisor moves the quotient by an ulp
+before the add), unclipped ones bit for bit.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import cases
+import golden_util as gu
+from fedml_amd import _native as nat
+from fedml_amd import defense as dfn
+from fedml_amd.layout import RowLayout
+from fedml_amd.synth import fingerprint
+from oracle import fedavg_oracle as orc
+
+DIST = [c["name"] for c in cases.DIST_CASES]
+KRUM = [c["name"] for c in cases.DIST_CASES if c["defense"] in ("krum", "multikrum")]
+CLIP = [c["name"] for c in cases.DIST_CASES if c["defense"] == "norm_diff_clipping"]
+
+
+def _m(spec):
+    m = spec.get("krum_param_m")
+    return m if isinstance(m, int) else 1
+
+
+def assert_selection(sel, meta, what=""):
+    """Same clients as the reference's, or tied ones (by the reference's own scores)."""
+    ref_sel = meta["selected"]
+    if list(sel) == list(ref_sel):
+        return True
+    rs = np.asarray(meta["ref_scores"])
+    np.testing.assert_allclose(np.sort(rs[list(sel)]), np.sort(rs[list(ref_sel)]), rtol=1e-6, err_msg=what)
+    return False
+
+
+@pytest.mark.parametrize("name", DIST)
+def test_inputs_reproducible(name):
+    meta, _ = gu.load(name)
+    raw, _ = cases.dist_inputs(meta["spec"])
+    assert fingerprint(raw) == meta["in_sha256"]
+
+
+@pytest.mark.parametrize("name", KRUM)
+def test_oracle_krum_matches_reference(name):
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, _ = cases.dist_inputs(spec)
+    if meta["error"]:
+        with pytest.raises(Exception) as ei:
+            orc.krum_select(raw, spec["byzantine_client_num"], _m(spec))
+        assert type(ei.value).__name__ == meta["error"]
+        return
+    sel, scores = orc.krum_select(raw, spec["byzantine_client_num"], _m(spec))
+    np.testing.assert_allclose(scores, meta["ref_scores"], rtol=1e-6)
+    idx = [next(i for i, item in enumerate(raw) if item is s) for s in sel]
+    if assert_selection(idx, meta, name):
+        gu.assert_groups(orc.agg(cases.DefenseArgs(spec), sel), meta, arrays, name)
+
+
+def test_krum_fake_list_tie_is_real():
+    """The reference test's model list (clients i * A) has mirror-image
+    clients whose scores tie: the tolerance above is about them."""
+    meta, _ = gu.load("krum_fake_k20")
+    s = np.asarray(meta["ref_scores"])
+    i, j = 8, 9  # clients 9 and 10 of 20
+    assert abs(s[i] - s[j]) <= 1e-6 * s[i]
+
+
+@pytest.mark.parametrize("name", CLIP)
+def test_oracle_clip_matches_reference(name):
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, glob = cases.dist_inputs(spec)
+    out = orc.norm_diff_clip(raw, glob, spec["norm_bound"])
+    for i, (n, d) in enumerate(out):
+        clipped = meta["ref_norms"][i] / spec["norm_bound"] > 1
+        for k, t in d.items():
+            ref = arrays[f"c{i}:{k}"].reshape(-1)
+            got = t.numpy().reshape(-1)
+            if not clipped or not orc._is_weight_param(k):
+                np.testing.assert_array_equal(got.view(np.uint8), ref.view(np.uint8), err_msg=f"{name} c{i}:{k}")
+            else:
+                # divisors one ulp apart: |d/c| moves by <= 1.5 ulp, then + g rounds
+                gk = glob[k].numpy().reshape(-1)
+                tol = 2.0 ** -21 * (np.abs(ref) + np.abs(gk))
+                assert (np.abs(got - ref) <= tol).all(), f"{name} c{i}:{k}"
+    res = orc.agg(cases.DefenseArgs(spec), out)
+    for k, t in res.items():
+        np.testing.assert_allclose(t.numpy(), arrays[f"o0:{k}"], rtol=1e-5, atol=1e-7, err_msg=f"{name} {k}")
+    if not any(v / spec["norm_bound"] > 1 for v in meta["ref_norms"]):
+        gu.assert_groups(res, meta, arrays, name)  # nothing clipped: bit for bit
+
+
+def test_ref_norms_match_oracle_fp32_root():
+    for name in CLIP:
+        meta, _ = gu.load(name)
+        raw, glob = cases.dist_inputs(meta["spec"])
+        g = orc.weight_vector(glob)
+        ours = [orc.fp32_norm(orc.dist2(orc.weight_vector(p), g)) for _, p in raw]
+        np.testing.assert_allclose(ours, meta["ref_norms"], rtol=4e-7)  # torch's fp32 sum: within 2 ulp
+
+
+def test_weight_chunks_skip_buffers_and_split():
+    layout = RowLayout([("conv.weight", (3, 5000), torch.float32), ("bn.weight", (7,), torch.float32),
+                        ("bn.running_mean", (7,), torch.float32), ("bn.num_batches_tracked", (), torch.int64),
+                        ("fc.weight", (4097,), torch.float32)], True)
+    g = layout.groups[torch.float32]
+    tab, n = dfn.weight_chunks(g, 2048, torch.device("cpu"))
+    t = tab.view(-1, 2).numpy()
+    assert n == len(t)
+    cols = np.concatenate([np.arange(s, s + l) for s, l in t])
+    want = np.concatenate([np.arange(o, o + m) for k, o, m in zip(g.keys, g.offsets, g.numels)
+                           if dfn.is_weight_param(k)])
+    np.testing.assert_array_equal(cols, want)
+    assert (t[:, 1] <= 2048).all() and (t[:, 1] > 0).all()
+
+
+def test_abi_argument_checks():
+    fbuild = pytest.importorskip("fedml_amd.build")
+    fbuild.build()
+    lib = nat.lib()
+    assert lib.fedagg_robust_work_len(nat.WORK_DIST2, 0, 5) == -1
+    assert lib.fedagg_robust_work_len(nat.WORK_PAIRDIST2, 130, 0) == 0
+    assert lib.fedagg_robust_work_len(nat.WORK_PAIRDIST2, 130, 10) >= 6 * 64 * 64
+    assert lib.fedagg_robust_work_len(7, 4, 4) == -1
+    assert lib.fedagg_dist2_f32(None, 0, None, None, 0, None, None, 0, None) == -1
+    assert b"K must be" in lib.fedagg_last_error()
+    assert lib.fedagg_pairdist2_f32(1, 4, None, 3, 1, None, 0, None) == -1
+    assert b"null pointer" in lib.fedagg_last_error()
+    assert lib.fedagg_clip_diff_f32(1, 2, 1, 1, -1, 1, None) == -1
+
+
+def test_krum_argument_error_before_any_device_work():
+    raw, _ = cases.dist_inputs(next(c for c in cases.DIST_CASES if c["name"] == "krum_bad_f"))
+    with pytest.raises(ValueError):
+        dfn.krum_before_aggregation(raw, 2, 1)

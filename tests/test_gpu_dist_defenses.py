@@ -1,0 +1,221 @@
+"""GPU parity of the distance-based defenses (csrc/robust.hip) against the
+reference's own KrumDefense / NormDiffClippingDefense outputs (tests/golden)
+and against the numpy oracle; tolerances as stated in test_dist_defenses.py:
+Krum's selection equals the reference's (tied fp32 scores excepted), the
+aggregate after it is bit-exact; clipped weights within 2^-21 (|w| + |g|),
+unclipped ones bit for bit.  Kernel level: dist2 (fp64 sums of exact squares)
+within 1e-12 relative of numpy's fp64 sum, pairdist2 (fp32 stage sums) within
+1e-5 relative, and the two kernels agree with each other at full size."""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+import cases
+import golden_util as gu
+from fedml_amd import _native as nat
+from fedml_amd import defense as dfn
+from fedml_amd import kernels as kn
+from fedml_amd.server_aggregator import MI355XServerAggregator
+from oracle import fedavg_oracle as orc
+from test_dist_defenses import _m, assert_selection
+
+pytestmark = pytest.mark.gpu
+
+KRUM = [c["name"] for c in cases.DIST_CASES if c["defense"] in ("krum", "multikrum")]
+CLIP = [c["name"] for c in cases.DIST_CASES if c["defense"] == "norm_diff_clipping"]
+
+
+class _Agg(MI355XServerAggregator):
+    def __init__(self, args, global_model=None):
+        super().__init__(torch.nn.Linear(1, 1), args)
+        self._g = global_model
+
+    def get_model_params(self):
+        return self._g
+
+
+def _to(raw, dev):
+    return [(n, OrderedDict((k, t.to(dev)) for k, t in d.items())) for n, d in raw]
+
+
+@pytest.mark.parametrize("device_inputs", [False, True])
+@pytest.mark.parametrize("name", KRUM)
+def test_krum_matches_reference(name, device_inputs, cuda_device):
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, _ = cases.dist_inputs(spec)
+    if device_inputs:
+        raw = _to(raw, cuda_device)
+    agg = _Agg(cases.DefenseArgs(spec))
+    if meta["error"]:
+        with pytest.raises(Exception) as ei:
+            agg.on_before_aggregation(raw)
+        assert type(ei.value).__name__ == meta["error"]
+        return
+    lst, idxs = agg.on_before_aggregation(raw)
+    assert idxs == list(range(len(raw)))
+    assert len(lst) == _m(spec)
+    sel = [next(i for i, item in enumerate(raw) if item is s) for s in lst]  # the original tuples
+    if assert_selection(sel, meta, name):
+        res = agg.on_after_aggregation(agg.aggregate(lst))
+        for t in res.values():
+            assert t.is_cuda == device_inputs
+        gu.assert_groups(OrderedDict((k, t.cpu()) for k, t in res.items()), meta, arrays, name)
+
+
+@pytest.mark.parametrize("device_inputs", [False, True])
+@pytest.mark.parametrize("name", CLIP)
+def test_clip_matches_reference(name, device_inputs, cuda_device):
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, glob = cases.dist_inputs(spec)
+    if device_inputs:
+        raw, glob = _to(raw, cuda_device), OrderedDict((k, t.to(cuda_device)) for k, t in glob.items())
+    agg = _Agg(cases.DefenseArgs(spec), glob)
+    lst, _ = agg.on_before_aggregation(raw)
+    assert len(lst) == len(raw)
+    for i, (n, d) in enumerate(lst):
+        assert n == raw[i][0]
+        clipped = meta["ref_norms"][i] / spec["norm_bound"] > 1
+        for k, t in d.items():
+            if not dfn.is_weight_param(k):
+                assert t is raw[i][1][k]  # the client's own tensor, as the reference keeps it
+            assert t.is_cuda == device_inputs
+            ref = arrays[f"c{i}:{k}"].reshape(-1)
+            got = t.cpu().numpy().reshape(-1)
+            if not clipped or not dfn.is_weight_param(k):
+                np.testing.assert_array_equal(got.view(np.uint8), ref.view(np.uint8), err_msg=f"{name} c{i}:{k}")
+            else:
+                gk = glob[k].cpu().numpy().reshape(-1)
+                assert (np.abs(got - ref) <= 2.0 ** -21 * (np.abs(ref) + np.abs(gk))).all(), f"{name} c{i}:{k}"
+    res = agg.aggregate(lst)
+    for k, t in res.items():
+        np.testing.assert_allclose(t.cpu().numpy(), arrays[f"o0:{k}"], rtol=1e-5, atol=1e-7, err_msg=k)
+    if not any(v / spec["norm_bound"] > 1 for v in meta["ref_norms"]):
+        gu.assert_groups(OrderedDict((k, t.cpu()) for k, t in res.items()), meta, arrays, name)
+
+
+def _rows(K, L, dev, seed, outliers=()):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    base = torch.randn(L, generator=g, device=dev) * 0.05
+    rows = base + 0.01 * torch.randn((K, L), generator=g, device=dev)
+    for i in outliers:
+        rows[i] *= 3.0
+    return rows
+
+
+def _chunks(segs, chunk, dev):
+    tab = []
+    for off, n in segs:
+        for s in range(off, off + n, chunk):
+            tab += [s, min(chunk, off + n - s)]
+    return kn.upload_i64(tab, dev), len(tab) // 2
+
+
+def _np_pair(rows_np, segs):
+    cols = np.concatenate([np.arange(o, o + n) for o, n in segs])
+    X = rows_np[:, cols]
+    K = X.shape[0]
+    D = np.zeros((K, K))
+    for i in range(K):
+        d = (X[i][None, :] - X).astype(np.float32).astype(np.float64)
+        D[i] = (d * d).sum(axis=1)
+    return D
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 17, 63, 64, 65, 100, 128, 129, 200])
+def test_pairdist2_vs_numpy(K, cuda_device):
+    L = 5000
+    rows = _rows(K, L, cuda_device, K, outliers=[0] if K > 2 else [])
+    segs = [(0, 1), (3, 700), (704, 1), (960, 2500), (4000, 999)]  # ragged, partial stages
+    chunks, n = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    D = dfn.pairdist2_rows(ptrs, K, chunks, n, cuda_device).cpu().numpy()
+    want = _np_pair(rows.cpu().numpy(), segs)
+    np.testing.assert_allclose(D, want, rtol=1e-5)
+    assert (np.diag(D) == 0).all()
+    np.testing.assert_array_equal(D, D.T)
+
+
+@pytest.mark.parametrize("with_ref", [False, True])
+@pytest.mark.parametrize("K", [1, 5, 128, 300])
+def test_dist2_vs_numpy(K, with_ref, cuda_device):
+    L = 9000
+    rows = _rows(K, L, cuda_device, 7 + K)
+    ref = torch.randn(L, device=cuda_device) * 0.05 if with_ref else None
+    segs = [(5, 2048), (2053, 1), (3000, 5999)]
+    chunks, n = _chunks(segs, nat.DIST_CHUNK, cuda_device)
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    got = dfn.dist2_rows(ptrs, K, ref, chunks, n, cuda_device).cpu().numpy()
+    cols = np.concatenate([np.arange(o, o + m) for o, m in segs])
+    X = rows.cpu().numpy()[:, cols]
+    r = ref.cpu().numpy()[cols] if with_ref else np.zeros(len(cols), np.float32)
+    d = (X - r[None, :]).astype(np.float32).astype(np.float64)
+    np.testing.assert_allclose(got, (d * d).sum(axis=1), rtol=1e-12)
+
+
+def test_empty_chunk_table(cuda_device):
+    rows = _rows(3, 64, cuda_device, 1)
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(3)], cuda_device)
+    empty = torch.zeros(2, dtype=torch.int64, device=cuda_device)
+    assert (dfn.pairdist2_rows(ptrs, 3, empty, 0, cuda_device) == 0).all()
+    assert (dfn.dist2_rows(ptrs, 3, None, empty, 0, cuda_device) == 0).all()
+
+
+def test_full_size_pairdist_agrees_with_dist2(cuda_device):
+    """128 clients x 25.6M columns (config 3's row): sampled pairs of the
+    packed-fp32 pair kernel against the fp64 single-reference kernel."""
+    K, L = 128, 25_610_240
+    rows = _rows(K, L, cuda_device, 3, outliers=[5, 77])
+    segs = [(0, 25_610_152)]
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    ch_p, n_p = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
+    D = dfn.pairdist2_rows(ptrs, K, ch_p, n_p, cuda_device).cpu().numpy()
+    ch_d, n_d = _chunks(segs, nat.DIST_CHUNK, cuda_device)
+    for j in (0, 5, 64, 127):
+        col = dfn.dist2_rows(ptrs, K, rows[j], ch_d, n_d, cuda_device).cpu().numpy()
+        np.testing.assert_allclose(D[:, j], col, rtol=2e-6)
+    # Krum at this size picks neither outlier
+    scores = dfn.krum_scores(D, 10)
+    best = torch.argsort(torch.Tensor(scores)).tolist()[:5]
+    assert 5 not in best and 77 not in best
+
+
+def test_clip_kernel_vs_oracle_large(cuda_device):
+    K, L = 16, 1_000_064
+    rows = _rows(K, L, cuda_device, 11, outliers=[3])
+    g = torch.randn(L, device=cuda_device) * 0.05
+    divs = [1.0, 1.5, 3.0000002, 1.0] * 4
+    d_div = kn.upload_f32(divs, cuda_device)
+    out = torch.empty_like(rows)
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    dst = kn.upload_i64([out[i].data_ptr() for i in range(K)], cuda_device)
+    nat.check(nat.lib().fedagg_clip_diff_f32(ptrs.data_ptr(), K, g.data_ptr(), d_div.data_ptr(), L, dst.data_ptr(),
+                                             nat.stream_handle()), "clip")
+    x, gn = rows.cpu().numpy(), g.cpu().numpy()
+    for i in range(K):
+        want = (((x[i] - gn).astype(np.float32) / np.float32(divs[i])).astype(np.float32) + gn).astype(np.float32)
+        np.testing.assert_array_equal(out[i].cpu().numpy().view(np.int32), want.view(np.int32))
+
+
+def test_krum_on_bucket_views_cross_silo_style(cuda_device):
+    """Device dicts that are views into one bucket (the cross-silo server's
+    model_dict) with BatchNorm buffers among the keys: the chunk table skips
+    the buffers, the result equals the oracle's selection."""
+    spec = next(c for c in cases.DIST_CASES if c["name"] == "multikrum_dist_k70_m5")
+    raw, _ = cases.dist_inputs(spec)
+    from fedml_amd.bucket import ClientBucket
+
+    b = ClientBucket(raw[0][1], len(raw), cuda_device, promote_ints=False)
+    for i, (n, d) in enumerate(raw):
+        b.put(i, d, n)
+    b.sync_ingest()
+    views = [(n, b.view(i)) for i, (n, _) in enumerate(raw)]
+    got = dfn.krum_before_aggregation(views, spec["byzantine_client_num"], spec["krum_param_m"])
+    want, _ = orc.krum_select(raw, spec["byzantine_client_num"], spec["krum_param_m"])
+    pos = lambda lst, x: next(i for i, v in enumerate(lst) if v is x)  # noqa: E731
+    assert [pos(views, x) for x in got] == [pos(raw, x) for x in want]
