@@ -38,6 +38,9 @@ from fedml_amd.sharded import ClientAxisAggregator, ParamAxisAggregator  # noqa:
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# packed fp32 vector peak (v_pk_fma_f32: 256 CUs x 64 lanes x 2 x 2 flops x 2.4 GHz), the ceiling of
+# the Krum pair kernel, whose packed subtract + packed FMA are 3 flops per client pair and element
+VALU_PEAK_TFLOPS = 157.3
 LSA_PRIME, LSA_QBITS = 2 ** 15 - 19, 10  # the reference's example LightSecAgg config (fedml_config.yaml:58-59)
 
 CONFIGS = {
@@ -65,7 +68,7 @@ def parse():
                     choices=["sgd", "adam", "adamw", "adagrad", "rmsprop"],
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
                          "or Adam / Adagrad lr=1.0 with torch defaults)")
-    ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa"],
+    ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa", "krum", "dist2", "clip"],
                     help="1 GPU: the reduction measured (median = the wise_median defense kernel; secagg = "
                          "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -255,6 +258,53 @@ def main():
 
         n_launch = 1
         dom_bytes = (K + 1) * gd.length * gd.rows.element_size()
+    elif a.op in ("krum", "dist2", "clip"):
+        # the distance defenses' kernels over the fp32 row's weight keys
+        # (csrc/robust.hip): krum = the K x K pair kernel, dist2 = every
+        # client's distance to a global row, clip = the clipped rebuild
+        from fedml_amd import _native as nat
+        from fedml_amd import defense as dfn
+        from fedml_amd import kernels as kn
+
+        if world > 1:
+            raise SystemExit("--op krum / dist2 / clip is a 1-GPU measurement")
+        gd = bucket.groups[torch.float32]
+        ref_row = gd.rows[K - 1].clone()  # a "global model" row
+        if a.op == "krum":
+            chunks, n_chunks = dfn.weight_chunks(gd, nat.PAIR_CHUNK, dev)
+            pd_out = torch.empty((K, K), dtype=torch.float64, device=dev)
+            work = dfn._work(nat.WORK_PAIRDIST2, K, n_chunks, dev)
+            call = lambda: nat.lib().fedagg_pairdist2_f32(  # noqa: E731
+                gd.d_ptrs.data_ptr(), K, chunks.data_ptr(), n_chunks, pd_out.data_ptr(), work.data_ptr(),
+                work.numel(), nat.stream_handle())
+        elif a.op == "dist2":
+            chunks, n_chunks = dfn.weight_chunks(gd, nat.DIST_CHUNK, dev)
+            d_out = torch.empty(K, dtype=torch.float64, device=dev)
+            work = dfn._work(nat.WORK_DIST2, K, n_chunks, dev)
+            call = lambda: nat.lib().fedagg_dist2_f32(  # noqa: E731
+                gd.d_ptrs.data_ptr(), K, ref_row.data_ptr(), chunks.data_ptr(), n_chunks, d_out.data_ptr(),
+                work.data_ptr(), work.numel(), nat.stream_handle())
+        else:
+            clip_out = torch.empty_like(gd.rows)
+            d_dst = kn.upload_i64([clip_out[i].data_ptr() for i in range(K)], dev)
+            d_div = kn.upload_f32([1.0 + 0.01 * i for i in range(K)], dev)
+            call = lambda: nat.lib().fedagg_clip_diff_f32(  # noqa: E731
+                gd.d_ptrs.data_ptr(), K, ref_row.data_ptr(), d_div.data_ptr(), gd.length, d_dst.data_ptr(),
+                nat.stream_handle())
+        n_weight = sum(n for k, n in zip(gd.keys, gd.numels) if dfn.is_weight_param(k))
+        # krum: 3 flops (sub, mul, add) per client pair and weight element;
+        # dist2: K rows + the reference row read once; clip: K rows in + K out + the reference row
+        dom_bytes = {"krum": 3 * K * (K - 1) // 2 * n_weight, "dist2": (K + 1) * n_weight * 4,
+                     "clip": (2 * K + 1) * gd.length * 4}[a.op]
+
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record()
+            nat.check(call(), a.op)
+            if ev is not None:
+                ev[1].record()
+
+        n_launch = 1
     elif a.op in ("secagg", "lsa"):
         from fedml_amd import _native as nat
 
@@ -344,7 +394,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = sum(e0.elapsed_time(e1) for ev in evs for e0, e1 in ev) / a.steps  # per step
-    achieved = dom_bytes / (kern_ms / 1e3) / 1e9
+    achieved = dom_bytes / (kern_ms / 1e3) / 1e9  # GB/s (GFLOP/s for --op krum)
     if world > 1:
         t = torch.tensor([achieved], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)  # slowest rank's kernel
@@ -385,14 +435,16 @@ def main():
                             "param": f"parameter-axis x{world}, no collective"}[mode],
         },
         "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "bound": "valu" if a.op == "krum" else "hbm",
+            "achieved": round(achieved / 1e3, 2) if a.op == "krum" else round(achieved, 1),
+            "peak": VALU_PEAK_TFLOPS if a.op == "krum" else HBM_PEAK_GBPS,
+            "unit": "TFLOP/s" if a.op == "krum" else "GB/s",
+            "frac": round(achieved / 1e3 / VALU_PEAK_TFLOPS if a.op == "krum" else achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>"}[a.op]
-                       if a.op in ("secagg", "lsa") else
+            "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>",
+                        "krum": "pairdist_kernel (packed fp32)", "dist2": "dist2_kernel",
+                        "clip": "clip_diff_kernel"}[a.op]
+                       if a.op in ("secagg", "lsa", "krum", "dist2", "clip") else
                        f"median_kernel<128, {dom_dt}>" if a.op == "median" else
                        ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
                          "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>"}

@@ -24,7 +24,7 @@ FEDAGG_ACC_REFERENCE = 0
 FEDAGG_ACC_FP32 = 1
 
 DT_F32, DT_BF16, DT_F16, DT_F64, DT_I64, DT_I32 = 0, 1, 2, 3, 4, 5
-DIST_CHUNK, PAIR_CHUNK = 2048, 256  # FEDAGG_DIST_CHUNK / FEDAGG_PAIR_CHUNK
+DIST_CHUNK, PAIR_CHUNK = 1024, 256  # FEDAGG_DIST_CHUNK / FEDAGG_PAIR_CHUNK
 WORK_DIST2, WORK_PAIRDIST2 = 0, 1
 
 # Every symbol include/fedagg.h declares, with its ctypes signature.

@@ -48,8 +48,12 @@ __device__ __forceinline__ const T __attribute__((address_space(1)))* gptr(const
   return (const T __attribute__((address_space(1)))*)(p);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBS = 256;
-constexpr int kDistU = FEDAGG_DIST_CHUNK / kBS;  // columns per thread per chunk
+constexpr int kWaves = kBS / 64;
+constexpr int kLaneCols = FEDAGG_DIST_CHUNK / 64;  // columns per lane per chunk (kLaneCols / 4 f32x4)
+constexpr int kBatch = 16;                         // clients per wave per pass (kWaves * kBatch per block)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -57,39 +61,81 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Columns lane*4 + 256*u (u < kLaneCols/4) of a chunk of `len` columns at
+// `p`: 16-byte loads where a whole f32x4 lies in the chunk and p is 16-byte
+// aligned (bucket rows and key offsets are), 4-byte loads otherwise; columns
+// past len read 0.
+__device__ __forceinline__ void load_chunk(const float* p, int len, int lane, f32x4 (&v)[kLaneCols / 4]) {
+  const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+#pragma unroll
+  for (int u = 0; u < kLaneCols / 4; ++u) {
+    const int c = lane * 4 + 256 * u;
+    if (al && c + 4 <= len) {
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 __attribute__((address_space(1)))*>(gptr(p) + c));
+    } else {
+      v[u].x = c < len ? gptr(p)[c] : 0.f;
+      v[u].y = c + 1 < len ? gptr(p)[c + 1] : 0.f;
+      v[u].z = c + 2 < len ? gptr(p)[c + 2] : 0.f;
+      v[u].w = c + 3 < len ? gptr(p)[c + 3] : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ double sq_diff(float x, float r, double acc) {
+  const float d = x - r;  // the reference's fp32 difference
+  return __builtin_fma(double(d), double(d), acc);  // exact square, fp64 sum
+}
+
 // ---------------------------------------------------------------------------
-// Per-client squared distance to a reference row.  Block (i, g): client i,
-// chunk group g (chunks g, g + G, ...).  blockIdx.x is the client so that the
-// K blocks reading the same reference chunk run back to back (the reference
-// row is then served from L2 / MALL, not re-read from HBM per client).
+// Per-client squared distance to a reference row.  A block owns the chunks
+// g, g + G, ... (a column range) for every client: per chunk each lane holds
+// its reference columns in registers, and wave w streams clients
+// w, w + 4, ... (kBatch of them per pass, one fp64 accumulator each) against
+// them.  The reference row is read from HBM once per pass, not once per
+// client (a client-major grid re-read it ~57x: 1.43x the algorithmic bytes).
 __global__ __launch_bounds__(kBS) void dist2_kernel(const float* const* __restrict__ src, int K,
                                                     const float* __restrict__ ref, const int64_t* __restrict__ chunks,
                                                     int64_t n_chunks, int G, double* __restrict__ partial) {
-  const int i = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
-  const auto row = gptr(src[i]);
-  const auto r = ref ? gptr(ref) : nullptr;
-  double acc = 0.0;
-  for (int64_t c = g; c < n_chunks; c += G) {
-    const int64_t start = chunks[2 * c];
-    const int len = int(chunks[2 * c + 1]);
-    float x[kDistU], y[kDistU];
+  const int g = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int cb = 0; cb < K; cb += kWaves * kBatch) {
+    double acc[kBatch];
 #pragma unroll
-    for (int u = 0; u < kDistU; ++u) {
-      const int idx = t + u * kBS;
-      x[u] = idx < len ? __builtin_nontemporal_load(row + start + idx) : 0.f;
-      y[u] = (r && idx < len) ? r[start + idx] : 0.f;
+    for (int j = 0; j < kBatch; ++j) acc[j] = 0.0;
+    for (int64_t c = g; c < n_chunks; c += G) {
+      const int64_t start = chunks[2 * c];
+      const int len = int(chunks[2 * c + 1]);
+      f32x4 r[kLaneCols / 4];
+      if (ref) {
+        load_chunk(ref + start, len, lane, r);
+      } else {
+#pragma unroll
+        for (int u = 0; u < kLaneCols / 4; ++u) r[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int i = cb + w + kWaves * j;
+        if (i < K) {  // wave-uniform
+          f32x4 x[kLaneCols / 4];
+          load_chunk(src[i] + start, len, lane, x);
+#pragma unroll
+          for (int u = 0; u < kLaneCols / 4; ++u) {
+            acc[j] = sq_diff(x[u].x, r[u].x, acc[j]);
+            acc[j] = sq_diff(x[u].y, r[u].y, acc[j]);
+            acc[j] = sq_diff(x[u].z, r[u].z, acc[j]);
+            acc[j] = sq_diff(x[u].w, r[u].w, acc[j]);
+          }
+        }
+      }
     }
 #pragma unroll
-    for (int u = 0; u < kDistU; ++u) {
-      const float d = x[u] - y[u];  // the reference's fp32 difference
-      acc = __builtin_fma(double(d), double(d), acc);  // exact square, fp64 sum
+    for (int j = 0; j < kBatch; ++j) {
+      const int i = cb + w + kWaves * j;
+      if (i < K) {
+        const double t = wave_sum(acc[j]);
+        if (lane == 0) partial[int64_t(i) * G + g] = t;
+      }
     }
   }
-  __shared__ double red[kBS / 64];
-  acc = wave_sum(acc);
-  if ((t & 63) == 0) red[t >> 6] = acc;
-  __syncthreads();
-  if (t == 0) partial[int64_t(i) * G + g] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // out[i] = sum over g of partial[i][g], in g order (deterministic)
@@ -104,37 +150,41 @@ __global__ void sum_rows_kernel(const double* __restrict__ partial, int rows, in
 // ---------------------------------------------------------------------------
 // Pairwise squared distances.  The K x K pair matrix is cut into 64 x 64
 // client tiles (I <= J); a block owns one tile over the chunk group g.  Per
-// stage of 64 columns each wave stages 16 client rows of tile I (and of J) as
-// coalesced 256-B row segments, four rows at a time packed into one 16-byte
-// LDS write per lane: sX[column][client], the 4-client groups XOR-swizzled by
+// stage of 64 columns each wave loads 16 client rows of tile I (and of J) as
+// coalesced 256-B row segments into registers one stage ahead, then writes
+// them four rows at a time as one 16-byte LDS write per lane: sX[column][client], the 4-client groups XOR-swizzled by
 // column so both the staging writes and the compute reads are bank-conflict
 // free.  Thread (ti, tj) then owns clients 4ti..4ti+3 of I x 4tj..4tj+3 of J:
 // per column one 16-byte LDS read per side and 16 squared differences, as 8
 // packed fp32 subtracts and 8 packed fp32 FMAs (v_pk_add_f32 / v_pk_fma_f32).
 // fp32 sums over one stage (<= 64 columns) are flushed into fp64
 // accumulators, which go to the workspace per block.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kPT = 64;      // clients per tile side
 constexpr int kStage = 64;   // columns per LDS stage
 
 __device__ __forceinline__ int swz(int c, int grp) { return c * kPT + ((grp ^ (c & 15)) << 2); }
 
-__device__ __forceinline__ void stage_tile(f32x4* __restrict__ s, const float* const* __restrict__ src, int K, int base,
+// A stage's global loads for one 64-client side, into registers: wave w
+// holds client groups 4w .. 4w + 3 (16 clients), lane = column.  Issued one
+// stage ahead, so they are in flight while the current stage is computed.
+__device__ __forceinline__ void stage_load(f32x4 (&v)[4], const float* const* __restrict__ src, int K, int base,
                                            int64_t col0, int w, int t) {
   const int lane = t & 63, wave = t >> 6;
-  // wave handles client groups 4 wave .. 4 wave + 3 (16 clients), lane = column
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int grp = wave * 4 + q;
-    f32x4 v;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int cl = base + grp * 4 + k;
-      v[k] = (cl < K && lane < w) ? __builtin_nontemporal_load(gptr(src[cl]) + col0 + lane) : 0.f;
+      v[q][k] = (cl < K && lane < w) ? __builtin_nontemporal_load(gptr(src[cl]) + col0 + lane) : 0.f;
     }
-    s[swz(lane, grp) >> 2] = v;
   }
+}
+
+__device__ __forceinline__ void stage_store(f32x4* __restrict__ s, const f32x4 (&v)[4], int t) {
+  const int lane = t & 63, wave = t >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s[swz(lane, wave * 4 + q) >> 2] = v[q];
 }
 
 // one column of the thread's 4 x 4 pair block: acc[2k + h] holds pairs
@@ -177,29 +227,47 @@ __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __res
   double acc64[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc64[k] = 0.0;
-  for (int64_t c = g; c < n_chunks; c += G) {
-    const int64_t start = chunks[2 * c];
+  // the stages of chunks g, g + G, ... in order; (c, s0) is the next stage
+  int64_t c = g;
+  int s0 = 0;
+  f32x4 va[4], vb[4];
+  int64_t col_next = 0;
+  int w_next = 0;
+  auto fetch = [&]() {  // issue the next stage's loads; false past the last stage
+    if (c >= n_chunks) return false;
     const int len = int(chunks[2 * c + 1]);
-    for (int s0 = 0; s0 < len; s0 += kStage) {
-      f32x2 acc[8];
+    col_next = chunks[2 * c] + s0;
+    w_next = len - s0 < kStage ? len - s0 : kStage;
+    stage_load(va, src, K, I, col_next, w_next, t);
+    if (!diag) stage_load(vb, src, K, J, col_next, w_next, t);
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
+  bool have = fetch();
+  while (have) {
+    const int w = w_next;
+    __syncthreads();  // the previous stage's LDS reads are done
+    stage_store(sA, va, t);
+    if (!diag) stage_store(sB, vb, t);
+    have = fetch();  // next stage's loads in flight during this stage's compute
+    __syncthreads();
+    f32x2 acc[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
-      const int w = len - s0 < kStage ? len - s0 : kStage;
-      __syncthreads();  // the previous stage's reads are done
-      stage_tile(sA, src, K, I, start + s0, w, t);
-      if (!diag) stage_tile(sB, src, K, J, start + s0, w, t);
-      __syncthreads();
-      if (w == kStage) {  // full stage: unrolled so the LDS reads of 8 columns are in flight together
+    for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
+    if (w == kStage) {  // full stage: unrolled so the LDS reads of 8 columns are in flight together
 #pragma unroll 8
-        for (int col = 0; col < kStage; ++col) pair_column(sA, sJ, col, ti, tj, acc);
-      } else {
-        for (int col = 0; col < w; ++col) pair_column(sA, sJ, col, ti, tj, acc);
-      }
+      for (int col = 0; col < kStage; ++col) pair_column(sA, sJ, col, ti, tj, acc);
+    } else {
+      for (int col = 0; col < w; ++col) pair_column(sA, sJ, col, ti, tj, acc);
+    }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        acc64[2 * k] += double(acc[k][0]);
-        acc64[2 * k + 1] += double(acc[k][1]);
-      }
+    for (int k = 0; k < 8; ++k) {
+      acc64[2 * k] += double(acc[k][0]);
+      acc64[2 * k + 1] += double(acc[k][1]);
     }
   }
   // pair (4ti + k, 4tj + m) of the tile at acc64[4k + m]
@@ -228,18 +296,47 @@ __global__ void pair_finish_kernel(const double* __restrict__ partial, int G, in
 // ---------------------------------------------------------------------------
 // Clipped rebuild (norm_diff_clipping_defense.py:38-54): y = (x - r) / c + r
 // in fp32 with the reference's three roundings (c = fl32 of the clip divisor;
-// torch divides an fp32 tensor by a Python scalar in fp32).
-__global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __restrict__ src,
+// torch divides an fp32 tensor by a Python scalar in fp32).  Same shape as
+// dist2: a block owns column tiles g, g + G, ... of FEDAGG_DIST_CHUNK columns,
+// the reference tile sits in registers, wave w rebuilds clients w, w + 4, ...
+// An unclipped client (c == 1) skips the division: x / 1 == x exactly.
+__device__ __forceinline__ f32x4 clip4(f32x4 x, f32x4 r, float c, bool one) {
+  f32x4 d = f32x4{x.x - r.x, x.y - r.y, x.z - r.z, x.w - r.w};
+  if (!one) d = f32x4{d.x / c, d.y / c, d.z / c, d.w / c};
+  return f32x4{d.x + r.x, d.y + r.y, d.z + r.z, d.w + r.w};
+}
+
+__global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __restrict__ src, int K,
                                                         const float* __restrict__ ref, const float* __restrict__ div,
-                                                        int64_t N, float* const* __restrict__ dst) {
-  const int i = blockIdx.y;
-  const auto x = gptr(src[i]);
-  float* y = dst[i];
-  const float c = div[i];
-  const int64_t stride = int64_t(gridDim.x) * kBS;
-  for (int64_t e = int64_t(blockIdx.x) * kBS + threadIdx.x; e < N; e += stride) {
-    const float r = ref[e];
-    y[e] = (__builtin_nontemporal_load(x + e) - r) / c + r;
+                                                        int64_t N, float* const* __restrict__ dst, int G) {
+  const int g = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t tiles = (N + FEDAGG_DIST_CHUNK - 1) / FEDAGG_DIST_CHUNK;
+  for (int64_t t = g; t < tiles; t += G) {
+    const int64_t start = t * FEDAGG_DIST_CHUNK;
+    const int len = int(N - start < FEDAGG_DIST_CHUNK ? N - start : FEDAGG_DIST_CHUNK);
+    f32x4 r[kLaneCols / 4];
+    load_chunk(ref + start, len, lane, r);
+    for (int i = w; i < K; i += kWaves) {
+      const float c = div[i];
+      const bool one = c == 1.0f;
+      f32x4 x[kLaneCols / 4];
+      load_chunk(src[i] + start, len, lane, x);
+      float* y = dst[i] + start;
+      const bool al = (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+#pragma unroll
+      for (int u = 0; u < kLaneCols / 4; ++u) {
+        const int col = lane * 4 + 256 * u;
+        const f32x4 v = clip4(x[u], r[u], c, one);
+        if (al && col + 4 <= len) {
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(y + col));
+        } else {
+          if (col < len) y[col] = v.x;
+          if (col + 1 < len) y[col + 1] = v.y;
+          if (col + 2 < len) y[col + 2] = v.z;
+          if (col + 3 < len) y[col + 3] = v.w;
+        }
+      }
+    }
   }
 }
 
@@ -260,7 +357,7 @@ extern "C" {
 int64_t fedagg_robust_work_len(int32_t kind, int32_t K, int64_t n_chunks) {
   if (K < 1 || n_chunks < 0) return -1;
   if (n_chunks == 0) return 0;
-  if (kind == FEDAGG_WORK_DIST2) return int64_t(K) * grid_groups(K, n_chunks, 0, 0);
+  if (kind == FEDAGG_WORK_DIST2) return int64_t(K) * grid_groups(2, n_chunks, 0, 0);
   if (kind == FEDAGG_WORK_PAIRDIST2) {
     const int NT = pair_tiles(K);
     return int64_t(NT) * grid_groups(NT, n_chunks, 0, 0) * (kPT * kPT);
@@ -279,9 +376,9 @@ int fedagg_dist2_f32(const float* const* d_src, int32_t K, const float* d_ref, c
     return FEDAGG_OK;
   }
   if (work_len < K) return rset(FEDAGG_EINVAL, "fedagg_dist2_f32: workspace smaller than K doubles");
-  const int G = grid_groups(K, n_chunks, work_len, K);
-  hipLaunchKernelGGL(dist2_kernel, dim3(unsigned(K), unsigned(G)), dim3(kBS), 0, st, d_src, K, d_ref, d_chunks,
-                     n_chunks, G, d_work);
+  const int G = grid_groups(2, n_chunks, work_len, K);
+  hipLaunchKernelGGL(dist2_kernel, dim3(unsigned(G)), dim3(kBS), 0, st, d_src, K, d_ref, d_chunks, n_chunks, G,
+                     d_work);
   hipLaunchKernelGGL(sum_rows_kernel, dim3(unsigned((K + 255) / 256)), dim3(256), 0, st, d_work, K, G, d_out);
   return rcheck("fedagg_dist2_f32");
 }
@@ -312,11 +409,9 @@ int fedagg_clip_diff_f32(const float* const* d_src, int32_t K, const float* d_re
   if (K < 1 || N < 0) return rset(FEDAGG_EINVAL, "fedagg_clip_diff_f32: K must be >= 1 and N >= 0");
   if (!d_src || !d_ref || !d_div || !d_dst) return rset(FEDAGG_EINVAL, "fedagg_clip_diff_f32: null pointer");
   if (N == 0) return FEDAGG_OK;
-  int64_t gx = (N + kBS - 1) / kBS;
-  const int64_t cap = (8192 + K - 1) / K;
-  if (gx > cap) gx = cap < 1 ? 1 : cap;
-  hipLaunchKernelGGL(clip_diff_kernel, dim3(unsigned(gx), unsigned(K)), dim3(kBS), 0, static_cast<hipStream_t>(stream),
-                     d_src, d_ref, d_div, N, d_dst);
+  const int G = grid_groups(2, (N + FEDAGG_DIST_CHUNK - 1) / FEDAGG_DIST_CHUNK, 0, 0);
+  hipLaunchKernelGGL(clip_diff_kernel, dim3(unsigned(G)), dim3(kBS), 0, static_cast<hipStream_t>(stream), d_src, K,
+                     d_ref, d_div, N, d_dst, G);
   return rcheck("fedagg_clip_diff_f32");
 }
 

@@ -274,7 +274,7 @@ int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K,
  * compute_euclidean_distance(v_i, v_j) (defense/krum_defense.py:47-60):
  *   d_out[i*K + j] = sum_e (src_i[e] - src_j[e])^2   (fp64, symmetric, 0 on
  *   the diagonal). */
-#define FEDAGG_DIST_CHUNK 2048
+#define FEDAGG_DIST_CHUNK 1024
 #define FEDAGG_PAIR_CHUNK 256
 #define FEDAGG_WORK_DIST2 0
 #define FEDAGG_WORK_PAIRDIST2 1
