@@ -22,8 +22,8 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 SO = os.path.join(HERE, "_build", "libmedian_lanes_probe.so")
 sys.path.insert(0, os.path.dirname(HERE))
-NV = 5
-SHAPE = {0: 256, 1: 512, 2: 512, 3: 1024, 4: 256}
+NV = 8
+SHAPE = {0: 256, 1: 512, 2: 512, 3: 1024, 4: 256, 5: 512, 6: 512, 7: 1024}
 
 
 def build():
@@ -50,7 +50,7 @@ def main():
     N = 4_000_037
     L = (N + 63) // 64 * 64
     res = {"N": N, "shapes": {}}
-    for K in (256, 384, 512, 768, 1024):
+    for K in [int(k) for k in os.environ.get("PROBE_KS", "256,384,512,768,1024").split(",")]:
         rows = torch.empty((K, L), device=dev)
         g = torch.Generator(device=dev).manual_seed(K)
         base = torch.randn(L, generator=g, device=dev) * 0.05
