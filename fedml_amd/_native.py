@@ -65,6 +65,7 @@ SIGNATURES = {
     "fedagg_dist2_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "fedagg_pairdist2_f32": (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P, _I64, _P]),
     "fedagg_clip_diff_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
+    "fedagg_scale_diff_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "fedagg_last_error": (ctypes.c_char_p, []),
     "fedagg_version": (_I32, []),
     "fedagg_wsum_f32_variant": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _I32, _P]),

@@ -5,6 +5,7 @@
 // What this replaces (python/fedml/core/security/):
 //   defense/krum_defense.py:47-60          K(K-1) torch norms of client differences
 //   defense/norm_diff_clipping_defense.py:20-54   one norm per client + the clipped rebuild
+//   defense/cclip_defense.py:30-80         bucket distances to the guess + the scaled differences
 //   common/utils.py:8-13, 24-27            vectorize_weight / compute_euclidean_distance
 //
 // Rows are K device pointers (client updates laid out as bucket rows); the
@@ -14,6 +15,7 @@
 //   fedagg_dist2_f32     out[i] = sum_e (x_i[e] - r[e])^2        (HBM-bound, one pass)
 //   fedagg_pairdist2_f32 out[i][j] = sum_e (x_i[e] - x_j[e])^2   (VALU-bound, packed fp32)
 //   fedagg_clip_diff_f32 y_i[e] = fl(fl(fl(x_i[e] - r[e]) / c_i) + r[e])
+//   fedagg_scale_diff_f32 y_i[e] = fl(fl(x_i[e] - r[e]) * s_i)   (CClip)
 //
 // Every difference is the fp32 difference the reference forms
 // (vec_local - vec_global, v1 - v2).  dist2 squares it exactly in fp64 and sums
@@ -300,12 +302,17 @@ __global__ void pair_finish_kernel(const double* __restrict__ partial, int G, in
 // dist2: a block owns column tiles g, g + G, ... of FEDAGG_DIST_CHUNK columns,
 // the reference tile sits in registers, wave w rebuilds clients w, w + 4, ...
 // An unclipped client (c == 1) skips the division: x / 1 == x exactly.
+// CClip's scaled difference (cclip_defense.py:47-52), MUL = true:
+// y = fl32(fl32(x - r) * s), s = fl32 of the Python score.
+template <bool MUL>
 __device__ __forceinline__ f32x4 clip4(f32x4 x, f32x4 r, float c, bool one) {
   f32x4 d = f32x4{x.x - r.x, x.y - r.y, x.z - r.z, x.w - r.w};
+  if constexpr (MUL) return f32x4{d.x * c, d.y * c, d.z * c, d.w * c};
   if (!one) d = f32x4{d.x / c, d.y / c, d.z / c, d.w / c};
   return f32x4{d.x + r.x, d.y + r.y, d.z + r.z, d.w + r.w};
 }
 
+template <bool MUL>
 __global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __restrict__ src, int K,
                                                         const float* __restrict__ ref, const float* __restrict__ div,
                                                         int64_t N, float* const* __restrict__ dst, int G) {
@@ -326,7 +333,7 @@ __global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __re
 #pragma unroll
       for (int u = 0; u < kLaneCols / 4; ++u) {
         const int col = lane * 4 + 256 * u;
-        const f32x4 v = clip4(x[u], r[u], c, one);
+        const f32x4 v = clip4<MUL>(x[u], r[u], c, one);
         if (al && col + 4 <= len) {
           __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(y + col));
         } else {
@@ -349,6 +356,18 @@ int grid_groups(int per_group_blocks, int64_t n_chunks, int64_t work_len, int64_
 }
 
 int pair_tiles(int K) { const int T = (K + kPT - 1) / kPT; return T * (T + 1) / 2; }
+
+template <bool MUL>
+int launch_diff(const char* what, const float* const* d_src, int32_t K, const float* d_ref, const float* d_c, int64_t N,
+                float* const* d_dst, fedagg_stream_t stream) {
+  if (K < 1 || N < 0) return rset(FEDAGG_EINVAL, std::string(what) + ": K must be >= 1 and N >= 0");
+  if (!d_src || !d_ref || !d_c || !d_dst) return rset(FEDAGG_EINVAL, std::string(what) + ": null pointer");
+  if (N == 0) return FEDAGG_OK;
+  const int G = grid_groups(2, (N + FEDAGG_DIST_CHUNK - 1) / FEDAGG_DIST_CHUNK, 0, 0);
+  hipLaunchKernelGGL(clip_diff_kernel<MUL>, dim3(unsigned(G)), dim3(kBS), 0, static_cast<hipStream_t>(stream), d_src,
+                     K, d_ref, d_c, N, d_dst, G);
+  return rcheck(what);
+}
 
 }  // namespace
 
@@ -406,13 +425,12 @@ int fedagg_pairdist2_f32(const float* const* d_src, int32_t K, const int64_t* d_
 
 int fedagg_clip_diff_f32(const float* const* d_src, int32_t K, const float* d_ref, const float* d_div, int64_t N,
                          float* const* d_dst, fedagg_stream_t stream) {
-  if (K < 1 || N < 0) return rset(FEDAGG_EINVAL, "fedagg_clip_diff_f32: K must be >= 1 and N >= 0");
-  if (!d_src || !d_ref || !d_div || !d_dst) return rset(FEDAGG_EINVAL, "fedagg_clip_diff_f32: null pointer");
-  if (N == 0) return FEDAGG_OK;
-  const int G = grid_groups(2, (N + FEDAGG_DIST_CHUNK - 1) / FEDAGG_DIST_CHUNK, 0, 0);
-  hipLaunchKernelGGL(clip_diff_kernel, dim3(unsigned(G)), dim3(kBS), 0, static_cast<hipStream_t>(stream), d_src, K,
-                     d_ref, d_div, N, d_dst, G);
-  return rcheck("fedagg_clip_diff_f32");
+  return launch_diff<false>("fedagg_clip_diff_f32", d_src, K, d_ref, d_div, N, d_dst, stream);
+}
+
+int fedagg_scale_diff_f32(const float* const* d_src, int32_t K, const float* d_ref, const float* d_scale, int64_t N,
+                          float* const* d_dst, fedagg_stream_t stream) {
+  return launch_diff<true>("fedagg_scale_diff_f32", d_src, K, d_ref, d_scale, N, d_dst, stream);
 }
 
 }  // extern "C"

@@ -30,6 +30,20 @@ that are pure reductions over the client axis.
                 sub-list of the ORIGINAL (sample_num, dict) tuples follow the
                 reference on the host (K numbers).
 
+"slsgd"         SLSGDDefense (slsgd_defense.py:28-67): option 2 trims by
+                sample count before aggregation (the trimmed-mean helper);
+                on aggregation FedAvg, then (1 - alpha) g + alpha avg per key,
+                a two-row weighted sum on the GPU (our FedAvg kernel: the
+                same two roundings per element as torch).
+
+"cclip"         CClipDefense (cclip_defense.py:21-80): bucketization =
+                FedAvg over consecutive groups of bucket_size clients (our
+                kernel, one launch per group), one bucket mean drawn by
+                np.random.randint as the guess, each mean's distance to it
+                (fedagg_dist2_f32), the scaled differences (mean - guess) *
+                min(1, tau / dist) over every key (fedagg_scale_diff_f32);
+                after aggregation guess + aggregate (a two-row sum).
+
 "norm_diff_clipping"
                 NormDiffClippingDefense.defend_before_aggregation
                 (norm_diff_clipping_defense.py:20-54): every client's distance
@@ -49,6 +63,7 @@ and a clipped client's divisor can differ in its last bit.
 """
 from __future__ import annotations
 
+import math
 from collections import OrderedDict
 from typing import List, Sequence, Tuple
 
@@ -64,8 +79,10 @@ DEFENSE_TRIMMED_MEAN = "trimmed_mean"
 DEFENSE_KRUM = "krum"
 DEFENSE_MULTIKRUM = "multikrum"
 DEFENSE_NORM_DIFF_CLIPPING = "norm_diff_clipping"
-SUPPORTED = (DEFENSE_WISE_MEDIAN, DEFENSE_TRIMMED_MEAN, DEFENSE_KRUM, DEFENSE_MULTIKRUM, DEFENSE_NORM_DIFF_CLIPPING)
-BEFORE_AGGREGATION = (DEFENSE_TRIMMED_MEAN, DEFENSE_KRUM, DEFENSE_MULTIKRUM, DEFENSE_NORM_DIFF_CLIPPING)
+DEFENSE_SLSGD = "slsgd"
+DEFENSE_CCLIP = "cclip"
+SUPPORTED = (DEFENSE_WISE_MEDIAN, DEFENSE_TRIMMED_MEAN, DEFENSE_KRUM, DEFENSE_MULTIKRUM, DEFENSE_NORM_DIFF_CLIPPING,
+             DEFENSE_SLSGD, DEFENSE_CCLIP)
 
 
 def is_weight_param(k: str) -> bool:
@@ -321,3 +338,140 @@ def norm_diff_clipping_before_aggregation(raw_client_grad_list: Sequence, global
                 clipped[k] = v
         new_list.append((sample_num, clipped))
     return new_list
+
+
+# ---- SLSGD / CClip (two-row and grouped weighted sums, scaled differences) ------
+
+def _like_input(out: "OrderedDict[str, torch.Tensor]", on_device: bool) -> "OrderedDict[str, torch.Tensor]":
+    if on_device:
+        return out
+    return OrderedDict((k, t.cpu()) for k, t in out.items())
+
+
+def _float_bucket(template, capacity: int, what: str, device=None):
+    """A ClientBucket for fp32 models (integer buffers allowed: they sit in
+    the fp32 row as fl32(v), the dtype torch's int64 * float yields), laid out
+    by `template`'s keys, on its device (or `device` for host tensors)."""
+    keys = list(template.keys())
+    layout = [(k, tuple(template[k].shape), template[k].dtype) for k in keys]
+    dts = {dt for _, _, dt in layout}
+    if not dts <= {torch.float32, torch.int64, torch.int32} or torch.float32 not in dts:
+        raise NotImplementedError(f"{what} on the GPU takes fp32 models (integer buffers allowed), got "
+                                  f"{sorted(map(str, dts))}")
+    t0 = template[keys[0]]
+    dev = t0.device if t0.is_cuda else (torch.device(device) if device is not None else
+                                        torch.device("cuda", torch.cuda.current_device()))
+    with torch.cuda.device(dev):
+        bucket = ClientBucket(layout, capacity, dev)
+    return bucket, dev
+
+
+def _put_float(bucket, slot: int, d, keys) -> None:
+    """put() of the layout's keys; an integer tensor under a float key is
+    converted by put (fl32(v), torch's rounding of int64 -> float32)."""
+    bucket.put(slot, OrderedDict((k, d[k]) for k in keys), 1)
+
+
+def mix_two(first, second, w_first: float, w_second: float, device=None) -> "OrderedDict[str, torch.Tensor]":
+    """fl(w_first * first[k]) + fl(w_second * second[k]) for every key of
+    `second`, as torch computes `(1 - alpha) * g[k] + alpha * avg[k]` (two
+    rows of our weighted-sum kernel; integer keys enter as fl32(v))."""
+    keys = list(second.keys())
+    on_dev = second[keys[0]].is_cuda
+    bucket, dev = _float_bucket(second, 2, "slsgd / cclip", device)
+    with torch.cuda.device(dev):
+        _put_float(bucket, 0, first, keys)
+        _put_float(bucket, 1, second, keys)
+        bucket.sync_ingest()
+        outs = bucket.new_outputs()
+        bucket.reduce_into(outs, [w_first, w_second], 2)
+        res = OrderedDict((k, t.clone()) for k, t in bucket.unflatten(outs).items())
+    return _like_input(res, on_dev)
+
+
+def slsgd_alpha_check(alpha: float) -> None:
+    """SLSGDDefense.__init__ (slsgd_defense.py:29-33)."""
+    if alpha > 1 or alpha < 0:
+        raise ValueError("the bound of alpha is [0, 1]")
+
+
+def slsgd_before_aggregation(raw_client_grad_list: Sequence, b: int, option_type: int) -> list:
+    """SLSGDDefense.defend_before_aggregation (slsgd_defense.py:36-52)."""
+    if b > math.ceil(len(raw_client_grad_list) / 2) - 1 or b < 0:
+        raise ValueError("the bound of b is [0, {}])".format(math.ceil(len(raw_client_grad_list) / 2) - 1))
+    if option_type != 1 and option_type != 2:
+        raise Exception("Such option type does not exist!")
+    if option_type == 2:
+        raw_client_grad_list = trimmed_mean(raw_client_grad_list, b)
+    return list(raw_client_grad_list)
+
+
+def slsgd_on_aggregation(avg_params, global_model, alpha: float, device=None):
+    """SLSGDDefense.defend_on_aggregation (slsgd_defense.py:54-67) after the
+    base FedAvg: (1 - alpha) * global + alpha * avg for every key."""
+    return mix_two(global_model, avg_params, 1 - alpha, alpha, device)
+
+
+def cclip_tau(args) -> float:
+    """CClipDefense.__init__ (cclip_defense.py:22-26)."""
+    tau = getattr(args, "tau", None)
+    return tau if type(tau) in [int, float] and tau > 0 else 10
+
+
+def cclip_before_aggregation(raw_client_grad_list: Sequence, tau: float, bucket_size: int, device=None):
+    """CClipDefense.defend_before_aggregation (cclip_defense.py:30-56).
+    Returns (new list, initial guess dict) -- the guess is kept for
+    defend_after_aggregation, as the reference's defender object does."""
+    K = len(raw_client_grad_list)
+    dicts = [item[1] for item in raw_client_grad_list]
+    on_dev = next(iter(dicts[0].values())).is_cuda
+    bucket, dev = _float_bucket(dicts[0], K, "cclip", device)
+    keys = list(dicts[0].keys())
+    with torch.cuda.device(dev):
+        for i, d in enumerate(dicts):
+            bucket.put(i, {k: d[k] for k in keys}, 1)
+        bucket.sync_ingest()
+    g = bucket.groups[torch.float32]
+    B = math.ceil(K / bucket_size)
+    with torch.cuda.device(dev):
+        means = torch.empty((B, g.rows.shape[1]), dtype=torch.float32, device=dev)
+        nums = []
+        for b in range(B):  # Bucket.bucketization (common/bucket.py:6-28)
+            lo = b * bucket_size
+            cn = min(bucket_size, K - lo)
+            sample_num = 0
+            for i in range(cn):
+                sample_num += raw_client_grad_list[lo + i][0]
+            w = [raw_client_grad_list[lo + i][0] / sample_num for i in range(cn)]
+            kn.wsum_ptrs(torch.float32, g.d_ptrs[lo:lo + cn], kn.weights_for(w, torch.float32, dev), cn, g.length,
+                         means[b], True)
+            nums.append(sample_num)
+        guess_idx = np.random.randint(0, B)  # _compute_an_initial_guess (:61-62), the global numpy RNG
+        guess = means[guess_idx]
+        m_ptrs = kn.upload_i64([means[b].data_ptr() for b in range(B)], dev)
+        chunks, n_chunks = weight_chunks(g, nat.DIST_CHUNK, dev)
+        sq = dist2_rows(m_ptrs, B, guess, chunks, n_chunks, dev).cpu().numpy()
+        scores = [min(1, tau / (fp32_norm(v) + 1e-8)) for v in sq]  # _compute_cclip_score (:64-71)
+        d_sc = kn.upload_f32([float(x) for x in scores], dev)
+        out = torch.empty_like(means)
+        d_dst = kn.upload_i64([out[b].data_ptr() for b in range(B)], dev)
+        nat.check(nat.lib().fedagg_scale_diff_f32(m_ptrs.data_ptr(), B, guess.data_ptr(), d_sc.data_ptr(),
+                                                  g.rows.shape[1], d_dst.data_ptr(), nat.stream_handle()),
+                  "scale_diff")
+        views = [bucket_view(g, out[b]) for b in range(B)]
+        guess_dict = bucket_view(g, guess)
+    new_list = [(nums[b], _like_input(views[b], on_dev)) for b in range(B)]
+    return new_list, _like_input(guess_dict, on_dev)
+
+
+def bucket_view(group, row: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
+    """Per-key views of one fp32 row of a group (keys in layout order)."""
+    return OrderedDict((k, row[o:o + n].view(shp))
+                       for k, o, n, shp in zip(group.keys, group.offsets, group.numels, group.shapes))
+
+
+def cclip_after_aggregation(global_model, initial_guess, device=None):
+    """CClipDefense.defend_after_aggregation (cclip_defense.py:57-60):
+    guess[k] + global[k] for every key (a two-row sum, weights 1 and 1:
+    fl(1 * x) = x, so one rounding, as torch's add)."""
+    return mix_two(initial_guess, global_model, 1.0, 1.0, device)

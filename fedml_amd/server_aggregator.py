@@ -11,7 +11,7 @@ reductions over the client axis and run on the GPU too (fedml_amd.defense):
 ``defense_type`` "wise_median" (on aggregation) and "trimmed_mean" (before
 aggregation), dispatched exactly as FedMLDefender does
 (core/security/fedml_defender.py:131-171); so do the distance-based
-"krum" / "multikrum" and "norm_diff_clipping" (before aggregation).  The other optional hooks (FHE,
+"krum" / "multikrum", "norm_diff_clipping", "slsgd" and "cclip".  The other optional hooks (FHE,
 differential privacy, attacks, other defenses, contribution assessment) are
 outside this build's scope: disabled (FedML's default) they are the identity,
 as in the reference; enabling one raises NotImplementedError instead of
@@ -47,6 +47,8 @@ def _check_flags(args) -> None:
         dt = str(getattr(args, "defense_type", "")).strip()
         if dt not in dfn.SUPPORTED:
             raise NotImplementedError(f"defense_type {dt!r}: fedml_amd runs {dfn.SUPPORTED} on the GPU")
+        if dt == dfn.DEFENSE_SLSGD:
+            dfn.slsgd_alpha_check(args.alpha)  # SLSGDDefense.__init__ raises at FedMLDefender.init
 
 
 def _defense(args):
@@ -65,6 +67,7 @@ class ServerAggregator(ABC):
         _check_flags(args)
         self.final_contribution_assigment_dict = dict()
         self.eval_data = None
+        self._cclip_guess = None  # CClip's initial guess, kept from before to after aggregation
 
     def is_main_process(self):
         return True
@@ -97,6 +100,12 @@ class ServerAggregator(ABC):
             # extra_auxiliary_info = the server's current model (server_aggregator.py:66-70)
             raw_client_model_or_grad_list = dfn.norm_diff_clipping_before_aggregation(
                 raw_client_model_or_grad_list, self.get_model_params(), self.args.norm_bound, dev)
+        elif dt == dfn.DEFENSE_SLSGD:
+            raw_client_model_or_grad_list = dfn.slsgd_before_aggregation(
+                raw_client_model_or_grad_list, self.args.trim_param_b, self.args.option_type)
+        elif dt == dfn.DEFENSE_CCLIP:
+            raw_client_model_or_grad_list, self._cclip_guess = dfn.cclip_before_aggregation(
+                raw_client_model_or_grad_list, dfn.cclip_tau(self.args), self.args.bucket_size, dev)
         return raw_client_model_or_grad_list, client_idxs  # no client is flagged malicious
 
     def aggregate(self, raw_client_model_or_grad_list: List[Tuple[float, OrderedDict]]):
@@ -104,10 +113,21 @@ class ServerAggregator(ABC):
         (fedml_defender.py:163-174), otherwise FedMLAggOperator.agg."""
         if _defense(self.args) == dfn.DEFENSE_WISE_MEDIAN:
             return dfn.coordinate_wise_median(raw_client_model_or_grad_list, getattr(self.args, "fedagg_device", None))
+        if _defense(self.args) == dfn.DEFENSE_SLSGD:
+            # defend_on_aggregation (slsgd_defense.py:54-67): the base operator, then the
+            # moving average with the global model (extra_auxiliary_info, :81-85)
+            avg = FedMLAggOperator.agg(self.args, raw_client_model_or_grad_list)
+            return dfn.slsgd_on_aggregation(avg, self.get_model_params(), self.args.alpha,
+                                            getattr(self.args, "fedagg_device", None))
         return FedMLAggOperator.agg(self.args, raw_client_model_or_grad_list)
 
     def on_after_aggregation(self, aggregated_model_or_grad: OrderedDict) -> OrderedDict:
-        """server_aggregator.py:90-103 with DP/defense disabled."""
+        """server_aggregator.py:90-103 with DP disabled: CClip adds its
+        initial guess back (fedml_defender.py:149-150, cclip_defense.py:57-60);
+        the other defenses pass the model through."""
+        if _defense(self.args) == dfn.DEFENSE_CCLIP:
+            return dfn.cclip_after_aggregation(aggregated_model_or_grad, self._cclip_guess,
+                                               getattr(self.args, "fedagg_device", None))
         return aggregated_model_or_grad
 
     def assess_contribution(self):

@@ -295,6 +295,14 @@ int fedagg_clip_diff_f32(const float* const* d_src, int32_t K, const float* d_re
                          const float* d_div, int64_t N, float* const* d_dst,
                          fedagg_stream_t stream);
 
+/* CClip's scaled differences (CClipDefense.defend_before_aggregation,
+ * defense/cclip_defense.py:47-52, over every key of the bucket means):
+ *   d_dst_i[e] = fl32( fl32(src_i[e] - ref[e]) * d_scale[i] )
+ * with d_scale[i] = fl32(min(1, tau / (norm_i + 1e-8))) (K device floats). */
+int fedagg_scale_diff_f32(const float* const* d_src, int32_t K, const float* d_ref,
+                          const float* d_scale, int64_t N, float* const* d_dst,
+                          fedagg_stream_t stream);
+
 /* Secure aggregation in a finite field (LightSecAgg), numpy int64 semantics:
  * wrapping adds, floor modulo.  p > 0.
  *

@@ -605,6 +605,79 @@ def norm_diff_clip(raw_grad_list, global_model, norm_bound: float):
     return out
 
 
+def _f32(t: torch.Tensor) -> np.ndarray:
+    """A tensor's values as float32 the way torch promotes int64 * float."""
+    return to_np(t).astype(np.float32)
+
+
+def mix_two(first, second, w_first: float, w_second: float):
+    """`w_first * first[k] + w_second * second[k]` per key of `second`, in
+    torch's fp32 arithmetic (each product rounded, then the sum)."""
+    out = OrderedDict()
+    for k, t in second.items():
+        a = (np.float32(w_first) * _f32(first[k])).astype(np.float32)
+        b = (np.float32(w_second) * _f32(t)).astype(np.float32)
+        out[k] = torch.from_numpy(np.asarray(a + b, dtype=np.float32)).view(t.size())
+    return out
+
+
+def slsgd(args, raw_grad_list, global_model):
+    """SLSGDDefense (slsgd_defense.py:28-67): bounds checks, option-2 trim by
+    sample count, FedAvg, then (1 - alpha) * global + alpha * avg."""
+    import math
+
+    if args.alpha > 1 or args.alpha < 0:
+        raise ValueError("the bound of alpha is [0, 1]")
+    b = args.trim_param_b
+    if b > math.ceil(len(raw_grad_list) / 2) - 1 or b < 0:
+        raise ValueError("the bound of b")
+    if args.option_type not in (1, 2):
+        raise Exception("Such option type does not exist!")
+    lst = trimmed_mean(raw_grad_list, b) if args.option_type == 2 else raw_grad_list
+    return mix_two(global_model, agg(args, lst), 1 - args.alpha, args.alpha), lst
+
+
+def bucketization(raw_grad_list, bucket_size: int):
+    """common/bucket.py:6-28: per group of bucket_size consecutive clients the
+    weighted average with w_i = n_i / sum n (the FedAvg chain, int keys ->
+    float32), keys of client 0; the group's sample count."""
+    import math
+
+    K = len(raw_grad_list)
+    keys = list(raw_grad_list[0][1].keys())
+    out = []
+    for b in range(math.ceil(K / bucket_size)):
+        grp = raw_grad_list[b * bucket_size: min((b + 1) * bucket_size, K)]
+        total = 0
+        for n, _ in grp:
+            total += n
+        ws = [n / total for n, _ in grp]
+        out.append((total, OrderedDict((k, wsum([p[k] for _, p in grp], ws)) for k in keys)))
+    return out
+
+
+def cclip(raw_grad_list, tau: float, bucket_size: int):
+    """CClipDefense.defend_before_aggregation (cclip_defense.py:30-71); the
+    caller seeds numpy's global RNG as the reference run did.  Returns (new
+    list, initial guess dict)."""
+    groups = bucketization(raw_grad_list, bucket_size)
+    guess = groups[np.random.randint(0, len(groups))][1]
+    g = weight_vector(guess)
+    new = []
+    for n, params in groups:
+        score = min(1, tau / (fp32_norm(dist2(weight_vector(params), g)) + 1e-8))
+        new.append((n, OrderedDict(
+            (k, torch.from_numpy(np.asarray((_f32(t) - _f32(guess[k])).astype(np.float32) * np.float32(score),
+                                            dtype=np.float32)).view(t.size())) for k, t in params.items())))
+    return new, guess
+
+
+def cclip_after(global_model, guess):
+    """cclip_defense.py:57-60: guess[k] + global[k]."""
+    return OrderedDict((k, torch.from_numpy(np.asarray(_f32(guess[k]) + _f32(t), dtype=np.float32)).view(t.size()))
+                       for k, t in global_model.items())
+
+
 def defended_agg(args, raw_grad_list, global_model=None):
     """FedMLDefender flow for the reduction and distance defenses
     (fedml_defender.py:131-171), followed by the base FedAvg operator."""

@@ -259,7 +259,8 @@ class DefenseArgs(Args):
         super().__init__(spec)
         self.enable_defense = True
         self.defense_type = spec["defense"]
-        for a in ("beta", "byzantine_client_num", "krum_param_m", "norm_bound"):
+        for a in ("beta", "byzantine_client_num", "krum_param_m", "norm_bound", "trim_param_b", "alpha", "option_type",
+                  "tau", "bucket_size"):
             if a in spec:
                 setattr(self, a, spec[a])
 
@@ -298,13 +299,29 @@ _dist("clip_ragged_k5_none", "norm_diff_clipping", 5, [k for k in RAGGED_F32 if 
       norm_bound=100.0)
 
 
+# SLSGD (slsgd_defense.py) and CClip (cclip_defense.py): "np_seed" seeds numpy's
+# global RNG right before the defense runs (CClip draws its guess from it)
+_dist("slsgd_opt1_k6_a05", "slsgd", 6, RESNET_MINI, 320, trim_param_b=0, alpha=0.5, option_type=1)
+_dist("slsgd_opt2_k7_b1_a03", "slsgd", 7, DIST_KEYS, 321, trim_param_b=1, alpha=0.3, option_type=2,
+      outliers={4: 2.0})
+_dist("slsgd_opt2_k5_b2_a1", "slsgd", 5, RESNET_MINI, 322, trim_param_b=2, alpha=1.0, option_type=2,
+      sample_nums=[30, 10, 50, 20, 40])
+_dist("slsgd_bad_alpha", "slsgd", 4, RAGGED_F32[:3], 323, trim_param_b=0, alpha=1.5, option_type=1, expect_error=True)
+_dist("slsgd_bad_b", "slsgd", 4, RAGGED_F32[:3], 324, trim_param_b=2, alpha=0.5, option_type=2, expect_error=True)
+_dist("slsgd_bad_option", "slsgd", 4, RAGGED_F32[:3], 325, trim_param_b=0, alpha=0.5, option_type=3,
+      expect_error=True)
+_dist("cclip_resnet_mini_k8_s2", "cclip", 8, RESNET_MINI, 330, bucket_size=2, np_seed=7, outliers={5: 3.0})
+_dist("cclip_dist_k10_s3_tau", "cclip", 10, DIST_KEYS, 331, bucket_size=3, tau=0.5, np_seed=11, outliers={0: -2.0})
+_dist("cclip_fake_k9_s4", "cclip", 9, None, 0, fake_model_list=True, bucket_size=4, tau=2, np_seed=3)
+
+
 def dist_inputs(spec):
     """(raw_grad_list, global_model) of a distance-defense case."""
     if spec.get("fake_model_list"):
         raw = fake_model_list(spec["K"])
         return raw, copy.deepcopy(raw[0][1])
     entries = _entries(spec["keys"])
-    raw = host_clients(entries, spec["K"], spec["seed"])
+    raw = host_clients(entries, spec["K"], spec["seed"], sample_nums=spec.get("sample_nums"))
     for i, f in spec.get("outliers", {}).items():
         for k, t in raw[int(i)][1].items():
             if t.is_floating_point():

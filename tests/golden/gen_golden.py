@@ -64,6 +64,14 @@ def import_defenses():
     return CoordinateWiseMedianDefense, CoordinateWiseTrimmedMeanDefense
 
 
+class _Done(Exception):
+    """Carries a finished defense's result out of run_dist_case's try block."""
+
+    def __init__(self, res):
+        super().__init__("done")
+        self.res = res
+
+
 def run_dist_case(FedMLAggOperator, spec):
     """Krum / multi-Krum / norm-diff clipping through the reference's own
     classes (krum_defense.py, norm_diff_clipping_defense.py), then the base
@@ -80,6 +88,32 @@ def run_dist_case(FedMLAggOperator, spec):
     arrays = {}
     ids = [id(item) for item in raw]
     try:
+        if spec["defense"] == "slsgd":
+            from fedml.core.security.defense.slsgd_defense import SLSGDDefense
+
+            d = SLSGDDefense(args)
+            lst = d.defend_before_aggregation(raw, glob)
+            dict_ids = [id(item[1]) for item in raw]  # trimmed_mean builds new tuples around the same dicts
+            meta["selected"] = [dict_ids.index(id(item[1])) for item in lst]
+            for k, t in glob.items():
+                arrays[f"g:{k}"] = tensor_bytes(t)
+            res = d.defend_on_aggregation(lst, FedMLAggOperator.agg, glob)
+            raise _Done(res)
+        if spec["defense"] == "cclip":
+            from fedml.core.security.defense.cclip_defense import CClipDefense
+
+            d = CClipDefense(args)
+            np.random.seed(spec["np_seed"])
+            lst = d.defend_before_aggregation(raw, None)
+            B = len(lst)
+            np.random.seed(spec["np_seed"])
+            meta["guess_index"] = int(np.random.randint(0, B))
+            meta["bucket_nums"] = [float(n) for n, _ in lst]
+            for b, (_, dct) in enumerate(lst):
+                for k, t in dct.items():
+                    arrays[f"c{b}:{k}"] = tensor_bytes(t)
+            res = d.defend_after_aggregation(FedMLAggOperator.agg(args, lst))
+            raise _Done(res)
         if spec["defense"] in ("krum", "multikrum"):
             d = KrumDefense(args)
             vecs = [sec_utils.vectorize_weight(p) for _, p in raw]
@@ -97,6 +131,8 @@ def run_dist_case(FedMLAggOperator, spec):
             for k, t in glob.items():
                 arrays[f"g:{k}"] = tensor_bytes(t)
         res = FedMLAggOperator.agg(args, out_list)
+    except _Done as dn:
+        res = dn.res
     except Exception as e:
         meta["error"] = type(e).__name__
         save(spec["name"], meta, arrays)

@@ -1,4 +1,5 @@
-"""Distance-based defenses (Krum / multi-Krum, norm-diff clipping), CPU side:
+"""Distance-based defenses (Krum / multi-Krum, norm-diff clipping, CClip) and
+SLSGD, CPU side:
 the oracle against the reference's own outputs (tests/golden, made by running
 KrumDefense / NormDiffClippingDefense + FedMLAggOperator.agg), the chunk-table
 builder, and the C ABI's argument checks (no GPU needed).
@@ -27,6 +28,8 @@ from fedml_amd.synth import fingerprint
 from oracle import fedavg_oracle as orc
 
 DIST = [c["name"] for c in cases.DIST_CASES]
+SLSGD = [c["name"] for c in cases.DIST_CASES if c["defense"] == "slsgd"]
+CCLIP = [c["name"] for c in cases.DIST_CASES if c["defense"] == "cclip"]
 KRUM = [c["name"] for c in cases.DIST_CASES if c["defense"] in ("krum", "multikrum")]
 CLIP = [c["name"] for c in cases.DIST_CASES if c["defense"] == "norm_diff_clipping"]
 
@@ -147,3 +150,49 @@ def test_krum_argument_error_before_any_device_work():
     raw, _ = cases.dist_inputs(next(c for c in cases.DIST_CASES if c["name"] == "krum_bad_f"))
     with pytest.raises(ValueError):
         dfn.krum_before_aggregation(raw, 2, 1)
+
+
+@pytest.mark.parametrize("name", SLSGD)
+def test_oracle_slsgd_matches_reference(name):
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, glob = cases.dist_inputs(spec)
+    if meta["error"]:
+        with pytest.raises(Exception) as ei:
+            orc.slsgd(cases.DefenseArgs(spec), raw, glob)
+        assert type(ei.value).__name__ == meta["error"]
+        return
+    res, lst = orc.slsgd(cases.DefenseArgs(spec), raw, glob)
+    assert [next(i for i, it in enumerate(raw) if it[1] is x[1]) for x in lst] == meta["selected"]
+    gu.assert_groups(res, meta, arrays, name)  # bit for bit
+
+
+@pytest.mark.parametrize("name", CCLIP)
+def test_oracle_cclip_matches_reference(name):
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, _ = cases.dist_inputs(spec)
+    np.random.seed(spec["np_seed"])
+    new, guess = orc.cclip(raw, cases.DefenseArgs(spec).__dict__.get("tau", 10), spec["bucket_size"])
+    assert [n for n, _ in new] == meta["bucket_nums"]
+    assert_cclip_list(new, meta, arrays, name)
+    res = orc.cclip_after(orc.agg(cases.DefenseArgs(spec), new), guess)
+    assert_close_groups(res, meta, arrays, name)
+
+
+def assert_cclip_list(new, meta, arrays, name):
+    """CClip's scaled differences: bit for bit where the score is 1 (the guess's
+    own bucket, and buckets within tau); a score below 1 comes from the fp32
+    norm (within 2 ulp of torch's), so those agree to 2^-21 relative."""
+    for b, (_, d) in enumerate(new):
+        for k, t in d.items():
+            got = t.cpu().numpy().reshape(-1)
+            ref = arrays[f"c{b}:{k}"].reshape(-1)
+            if not np.array_equal(got.view(np.uint32), ref.view(np.uint32)):
+                assert (np.abs(got - ref) <= 2.0 ** -21 * np.abs(ref)).all(), f"{name} c{b}:{k}"
+
+
+def assert_close_groups(res, meta, arrays, name):
+    for k, t in res.items():
+        np.testing.assert_allclose(t.cpu().numpy().reshape(-1), arrays[f"o0:{k}"].reshape(-1), rtol=1e-5, atol=1e-6,
+                                   err_msg=f"{name} {k}")

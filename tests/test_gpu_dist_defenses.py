@@ -219,3 +219,59 @@ def test_krum_on_bucket_views_cross_silo_style(cuda_device):
     want, _ = orc.krum_select(raw, spec["byzantine_client_num"], spec["krum_param_m"])
     pos = lambda lst, x: next(i for i, v in enumerate(lst) if v is x)  # noqa: E731
     assert [pos(views, x) for x in got] == [pos(raw, x) for x in want]
+
+
+SLSGD = [c["name"] for c in cases.DIST_CASES if c["defense"] == "slsgd"]
+CCLIP = [c["name"] for c in cases.DIST_CASES if c["defense"] == "cclip"]
+
+
+@pytest.mark.parametrize("device_inputs", [False, True])
+@pytest.mark.parametrize("name", SLSGD)
+def test_slsgd_matches_reference(name, device_inputs, cuda_device):
+    """SLSGD: trim by sample count, FedAvg, (1 - alpha) g + alpha avg on the GPU: bit for bit."""
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, glob = cases.dist_inputs(spec)
+    if device_inputs:
+        raw, glob = _to(raw, cuda_device), OrderedDict((k, t.to(cuda_device)) for k, t in glob.items())
+
+    def run():
+        agg = _Agg(cases.DefenseArgs(spec), glob)
+        lst, _ = agg.on_before_aggregation(raw)
+        return lst, agg.on_after_aggregation(agg.aggregate(lst))
+
+    if meta["error"]:
+        with pytest.raises(Exception) as ei:
+            run()
+        assert type(ei.value).__name__ == meta["error"]
+        return
+    lst, res = run()
+    assert [next(i for i, it in enumerate(raw) if it[1] is x[1]) for x in lst] == meta["selected"]
+    for t in res.values():
+        assert t.is_cuda == device_inputs
+    gu.assert_groups(OrderedDict((k, t.cpu()) for k, t in res.items()), meta, arrays, name)
+
+
+@pytest.mark.parametrize("device_inputs", [False, True])
+@pytest.mark.parametrize("name", CCLIP)
+def test_cclip_matches_reference(name, device_inputs, cuda_device):
+    """CClip: bucket means (our FedAvg kernel per group), the seeded guess,
+    scaled differences, FedAvg, guess added back after aggregation."""
+    from test_dist_defenses import assert_cclip_list, assert_close_groups
+
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, _ = cases.dist_inputs(spec)
+    if device_inputs:
+        raw = _to(raw, cuda_device)
+    agg = _Agg(cases.DefenseArgs(spec))
+    np.random.seed(spec["np_seed"])
+    lst, idxs = agg.on_before_aggregation(raw)
+    assert idxs == list(range(len(raw)))
+    assert [n for n, _ in lst] == meta["bucket_nums"]
+    for _, d in lst:
+        for t in d.values():
+            assert t.is_cuda == device_inputs
+    assert_cclip_list(lst, meta, arrays, name)
+    res = agg.on_after_aggregation(agg.aggregate(lst))
+    assert_close_groups(res, meta, arrays, name)
