@@ -40,6 +40,7 @@ _ROW_ALIGN = 64
 # H2D rate, tools/ingest_probe.py; 16 threads contend with the DMA reads)
 _PACK_THREADS = int(os.environ.get("FEDAGG_PACK_THREADS", min(8, os.cpu_count() or 1)))
 _STAGES = 3
+_PIECE = 1 << 22  # columns per evented H2D piece of a put() (16 MiB of fp32)
 
 
 def _pad(n: int) -> int:
@@ -88,6 +89,13 @@ class ClientBucket:
         self._staging: Dict[torch.dtype, dict] = {}
         self._result_host: Dict[torch.dtype, torch.Tensor] = {}
         self._pending = False
+        # put()'s H2D pieces: per dtype, piece index (column // _PIECE) ->
+        # (sequence number, event after the latest copy into it); the copy
+        # stream is in order, so that event also covers every earlier copy.
+        # _pending_other: an H2D path without pieces is pending
+        self._piece_events: Dict[torch.dtype, Dict[int, tuple]] = {}
+        self._piece_seq = 0
+        self._pending_other = False
         self._d2h: Optional[torch.cuda.Stream] = None
         self._round_outs: Optional[Dict[torch.dtype, torch.Tensor]] = None
         self._plans: Dict[tuple, list] = {}
@@ -165,6 +173,7 @@ class ClientBucket:
                 if host is not None:
                     self.groups[dt].rows[slot, :host.numel()].copy_(host, non_blocking=True)
         self._pending = True
+        self._pending_other = True
         self.sample_nums[slot] = sample_num
 
     def put_batch(self, tables: Dict[int, bytes], state_dicts: Sequence, sample_nums: Sequence[float]) -> None:
@@ -224,6 +233,7 @@ class ClientBucket:
                 ev.record(self._copy)
             st[1] = ev
             self._pending = True
+            self._pending_other = True
         for i, n in enumerate(sample_nums):
             self.sample_nums[i] = n
 
@@ -267,6 +277,7 @@ class ClientBucket:
                 ev.record(self._copy)
             b[1] = ev
             self._pending = True
+            self._pending_other = True
         self.sample_nums[slot] = sample_num
 
     def _table_plans(self):
@@ -335,8 +346,20 @@ class ClientBucket:
         del keep
         self._order_after_readers()
         with torch.cuda.stream(self._copy):
-            for a, e in runs.values():
-                g.rows[slot, a:e].copy_(stage[a:e], non_blocking=True)
+            # in pieces of _PIECE columns, each with an event: the pipelined
+            # round end (reduce_to_host) starts reducing a column range as soon
+            # as the last client's bytes for it have landed
+            last = self._piece_events.setdefault(dt, {})
+            for a, e in sorted(runs.values()):
+                while a < e:
+                    p = a // _PIECE
+                    z = min(e, (p + 1) * _PIECE)
+                    g.rows[slot, a:z].copy_(stage[a:z], non_blocking=True)
+                    pev = torch.cuda.Event()
+                    pev.record(self._copy)
+                    self._piece_seq += 1
+                    last[p] = (self._piece_seq, pev)
+                    a = z
             ev = torch.cuda.Event()
             ev.record(self._copy)
         b[1] = ev
@@ -359,7 +382,12 @@ class ClientBucket:
         """Make the current stream wait for every H2D issued by put()."""
         if self._pending and self._copy is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._copy)
-            self._pending = False
+        self._ingest_consumed()
+
+    def _ingest_consumed(self) -> None:
+        self._pending = False
+        self._pending_other = False
+        self._piece_events = {}
 
     # ---- reduction ------------------------------------------------------------
 
@@ -529,8 +557,13 @@ class ClientBucket:
         g = self.groups[dom]
         t = {} if timings is None else timings
         with torch.cuda.device(self.device):
-            self.sync_ingest()
             cur = torch.cuda.current_stream(self.device)
+            # only put()'s pieces pending: each range waits for the pieces it
+            # covers (the last client's H2D overlaps the first ranges' reduction)
+            fine = self._pending and not self._pending_other and self._copy is not None
+            if not fine:
+                self.sync_ingest()
+            pieces = self._piece_events.get(dom, {}) if fine else {}
             if self._d2h is None:
                 self._d2h = torch.cuda.Stream(self.device)
             w32 = kn.weights_for(weights, torch.float32, self.device)
@@ -539,6 +572,10 @@ class ClientBucket:
             plan = self._chunk_plan(dom, chunks)
             done = []
             for lo, hi, d_ptrs, _ in plan:
+                if fine:
+                    cover = [pieces[p] for p in range(lo // _PIECE, (hi - 1) // _PIECE + 1) if p in pieces]
+                    if cover:  # the copy stream is in order: the latest of them covers the others
+                        cur.wait_event(max(cover, key=lambda se: se[0])[1])
                 kn.wsum_ptrs(dom, d_ptrs, w64 if dom == torch.float64 else w32, K, hi - lo, outs[dom][lo:hi], True,
                              self.acc_mode)
                 ev = torch.cuda.Event()
@@ -550,6 +587,9 @@ class ClientBucket:
                     fin = torch.cuda.Event()
                     fin.record(self._d2h)
                 done.append(fin)
+            if fine:  # everything after this (the small groups, later readers) sees every H2D
+                cur.wait_stream(self._copy)
+                self._ingest_consumed()
             # the small groups behind the dominant one (e.g. ResNet's counters
             # are promoted into it; bf16 models' fp32 keys are not)
             minor = [dt for dt, gg in self.groups.items() if dt != dom and gg.length]

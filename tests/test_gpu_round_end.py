@@ -109,3 +109,43 @@ def test_reduce_to_host_bf16_model_with_fp32_keys(cuda_device):
     for k in exp:
         assert res[k].dtype == exp[k].dtype, k
         gu.assert_same(res[k], exp[k], k)
+
+
+@pytest.mark.parametrize("chunks", [3, 8])
+def test_reduce_to_host_waits_per_piece(chunks, cuda_device):
+    """Rows of ~13.4M columns: each put() lands as 4 evented H2D pieces and
+    every range of the reduction waits only for the pieces it covers.  The
+    last client has a device key in the middle of the row (its host runs
+    skip that piece), and the round is reduced while its H2D is in flight."""
+    layout = _layout(13_400_003)
+    K = 4
+    raw = _clients(layout, K, seed=77 + chunks)
+    raw[-1][1]["fc.weight"] = raw[-1][1]["fc.weight"].to(cuda_device)  # mixed residency, last client
+    exp, w = _expected([(n, OrderedDict((k, t.cpu()) for k, t in d.items())) for n, d in raw])
+    bucket = ClientBucket(layout, K, cuda_device)
+    for rnd in range(2):  # the second round reuses the staging and the pieces' bookkeeping
+        for i, (n, d) in enumerate(raw):
+            bucket.put(i, d, n)
+        got = bucket.reduce_to_host(w, chunks=chunks)
+        for k, t in got.items():
+            gu.assert_same(t, exp[k], f"round {rnd} {k}")
+        assert not bucket._pending and not bucket._piece_events
+
+
+def test_reduce_to_host_after_unpieced_ingest(cuda_device):
+    """A client ingested by put_encoded (one H2D without pieces) sends the
+    round end back to the full wait; results unchanged."""
+    from fedml_amd import wire
+
+    layout = _layout(5_000_001)
+    K = 3
+    raw = _clients(layout, K, seed=5)
+    exp, w = _expected(raw)
+    bucket = ClientBucket(layout, K, cuda_device)
+    bucket.put(0, raw[0][1], raw[0][0])
+    bucket.put_encoded(1, wire.encode(raw[1][1], raw[1][0]))
+    bucket.put(2, raw[2][1], raw[2][0])
+    assert bucket._pending_other
+    got = bucket.reduce_to_host(w)
+    for k, t in got.items():
+        gu.assert_same(t, exp[k], k)

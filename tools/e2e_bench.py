@@ -189,6 +189,22 @@ def main():
         sweep[ch] = sorted(ts[1:])[1]
     res["round_end_pipelined_chunk_sweep_ms"] = sweep
     res["pipelined_equals_serial"] = bool(all(torch.equal(piped[k], host[k]) for k in host))
+    # A/B of the per-piece wait: the same pipelined round end with the range
+    # reductions waiting for their own H2D pieces of the last clients ("piece")
+    # or for every pending H2D first ("full", as before), interleaved
+    ab = {"piece": [], "full": []}
+    for rep in range(8):
+        arm = "piece" if rep % 2 else "full"
+        for i, (n, d) in enumerate(raw):
+            bucket.put(i, d, n)
+        if arm == "full":
+            bucket._pending_other = True  # forces the whole-ingest wait
+        t1 = time.perf_counter()
+        bucket.reduce_to_host(w)
+        ab[arm].append((time.perf_counter() - t1) * 1e3)
+        time.sleep(0.2)
+    res["round_end_piece_wait_ab_ms"] = {k: sorted(v)[len(v) // 2] for k, v in ab.items()}
+    res["round_end_piece_wait_ab_all"] = ab
 
     # FAGG wire messages: ingest straight from the receive buffers
     from fedml_amd import wire
