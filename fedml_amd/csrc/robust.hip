@@ -69,6 +69,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 // past len read 0.
 __device__ __forceinline__ void load_chunk(const float* p, int len, int lane, f32x4 (&v)[kLaneCols / 4]) {
   const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  if (al && len == FEDAGG_DIST_CHUNK) {  // wave-uniform: a full aligned chunk, no per-lane conditions
+#pragma unroll
+    for (int u = 0; u < kLaneCols / 4; ++u)
+      v[u] = __builtin_nontemporal_load(
+          reinterpret_cast<const f32x4 __attribute__((address_space(1)))*>(gptr(p) + lane * 4 + 256 * u));
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < kLaneCols / 4; ++u) {
     const int c = lane * 4 + 256 * u;
@@ -166,21 +173,43 @@ constexpr int kStage = 64;   // columns per LDS stage
 
 __device__ __forceinline__ int swz(int c, int grp) { return c * kPT + ((grp ^ (c & 15)) << 2); }
 
-// A stage's global loads for one 64-client side, into registers: wave w
-// holds client groups 4w .. 4w + 3 (16 clients), lane = column.  Issued one
-// stage ahead, so they are in flight while the current stage is computed.
-__device__ __forceinline__ void stage_load(f32x4 (&v)[4], const float* const* __restrict__ src, int K, int base,
-                                           int64_t col0, int w, int t) {
-  const int lane = t & 63, wave = t >> 6;
+// The 16 client rows (4 groups of 4) a wave stages for one 64-client side:
+// wave-uniform pointers, read once per block (kept in SGPRs); a row past K
+// points at row 0 and is zeroed by `live`.
+struct SideRows {
+  const float* p[4][4];
+  bool live[4][4];
+};
+
+__device__ __forceinline__ SideRows side_rows(const float* const* __restrict__ src, int K, int base, int wave) {
+  SideRows r;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int grp = wave * 4 + q;
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int cl = base + grp * 4 + k;
-      v[q][k] = (cl < K && lane < w) ? __builtin_nontemporal_load(gptr(src[cl]) + col0 + lane) : 0.f;
+      const int cl = base + (wave * 4 + q) * 4 + k;
+      r.live[q][k] = cl < K;
+      r.p[q][k] = src[cl < K ? cl : 0];
     }
-  }
+  return r;
+}
+
+// A stage's global loads for one side, into registers (lane = column):
+// unconditional loads at a clamped column, then zeroed past w / past K, so
+// all 16 are in flight together.  Issued one stage ahead, they overlap the
+// current stage's compute.
+__device__ __forceinline__ void stage_load(f32x4 (&v)[4], const SideRows& rows, int64_t col0, int w, int lane) {
+  const int c = lane < w ? lane : 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x = __builtin_nontemporal_load(gptr(rows.p[q][k]) + col0 + c);
+      // a mask, not a select: a select on the uniform `live` became a branch
+      // around each load with a full vmcnt(0) wait at every join
+      const uint32_t m = (rows.live[q][k] && lane < w) ? 0xffffffffu : 0u;
+      v[q][k] = __uint_as_float(__float_as_uint(x) & m);
+    }
 }
 
 __device__ __forceinline__ void stage_store(f32x4* __restrict__ s, const f32x4 (&v)[4], int t) {
@@ -232,6 +261,9 @@ __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __res
   // the stages of chunks g, g + G, ... in order; (c, s0) is the next stage
   int64_t c = g;
   int s0 = 0;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const SideRows rowsA = side_rows(src, K, I, wave);
+  const SideRows rowsB = side_rows(src, K, diag ? I : J, wave);
   f32x4 va[4], vb[4];
   int64_t col_next = 0;
   int w_next = 0;
@@ -240,8 +272,8 @@ __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __res
     const int len = int(chunks[2 * c + 1]);
     col_next = chunks[2 * c] + s0;
     w_next = len - s0 < kStage ? len - s0 : kStage;
-    stage_load(va, src, K, I, col_next, w_next, t);
-    if (!diag) stage_load(vb, src, K, J, col_next, w_next, t);
+    stage_load(va, rowsA, col_next, w_next, lane);
+    if (!diag) stage_load(vb, rowsB, col_next, w_next, lane);
     s0 += kStage;
     if (s0 >= len) {
       s0 = 0;
