@@ -1553,6 +1553,169 @@ int launch_median_lanes(const typename E::S* const* src, int K, int64_t N, typen
   return check_launch("fedagg_median");
 }
 
+// 16-bit rows with more than 128 clients, two columns per register: the lane
+// group layout above on the packed int16 order keys of median_pk16_pair.  One
+// 32-bit load brings columns 2e and 2e+1 of a client; the in-lane sorts and
+// half-cleaners are v_pk_min_i16 / v_pk_max_i16 (one op per comparator side
+// for TWO columns), so the per-column VALU is about half of the widening
+// kernel's, which is what bounds this range.  The cross-lane min-or-max has no
+// packed med3: both sides and one v_cndmask on a lane mask.  Pads are packed
+// ±inf (their keys sit below / above every non-NaN key); a NaN column returns
+// its first NaN in client order, per half.  An odd last column runs as the
+// TAIL instantiation: one block whose every column group recomputes the
+// duplicated lone column, and lane 0 stores it.
+template <int CTRL>
+__device__ __forceinline__ short2_t dpp_mov(short2_t x) {
+  return __builtin_bit_cast(short2_t, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ short2_t pk_pick(short2_t a, short2_t b, bool up) {
+  const short2_t lo = __builtin_elementwise_min(a, b), hi = __builtin_elementwise_max(a, b);
+  return up ? hi : lo;
+}
+template <int M, int R>
+__device__ __forceinline__ void pk_lanes_reverse_pair(short2_t (&v)[R], bool up) {
+#pragma unroll
+  for (int i = 0; i < R / 2; ++i) {
+    const short2_t a = dpp_mov<dpp_xor_ctrl<M>()>(v[R - 1 - i]);
+    const short2_t b = dpp_mov<dpp_xor_ctrl<M>()>(v[i]);
+    v[i] = pk_pick(v[i], a, up);
+    v[R - 1 - i] = pk_pick(v[R - 1 - i], b, up);
+  }
+}
+template <int M, int R>
+__device__ __forceinline__ void pk_lanes_cross_stage(short2_t (&v)[R], int sub) {
+  const bool up = (sub & M) != 0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) v[i] = pk_pick(v[i], dpp_mov<dpp_xor_ctrl<M>()>(v[i]), up);
+}
+template <int R>
+__device__ __forceinline__ void pk_lane_bitonic_merge(short2_t (&v)[R]) {
+#pragma unroll
+  for (int d = R / 2; d > 0; d /= 2) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if ((i & d) == 0) cmpx(v[i], v[i + d]);
+  }
+}
+template <int G, int P, int R>
+__device__ __forceinline__ void pk_lanes_merge_levels(short2_t (&v)[R], int sub) {
+  if constexpr (G < P) {
+    static_assert(G <= 8, "a level of 16 lanes would need an xor-4 stage");
+    pk_lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) != 0);
+    if constexpr (G == 8) pk_lanes_cross_stage<2>(v, sub);
+    if constexpr (G >= 4) pk_lanes_cross_stage<1>(v, sub);
+    pk_lane_bitonic_merge(v);
+    pk_lanes_merge_levels<G * 2, P, R>(v, sub);
+  }
+}
+
+// packed ±inf pair in each 16-bit element type: a padded slot's 32-bit load
+template <class E>
+__device__ uint32_t g_median_pad2[2] = {E::kNegInf * 0x10001u, E::kPosInf * 0x10001u};
+
+template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
+    const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out) {
+  static_assert(P == 2 || P == 4 || P == 8, "2, 4 or 8 lanes per column pair");
+  static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
+  constexpr int KMAX = P * R, PAD = 2;
+  __shared__ const uint16_t* rows[KMAX + PAD * P];
+  __shared__ uint64_t offmask[FULL ? 1 : KMAX + PAD * P];
+  const int t = threadIdx.x, sub = t & (P - 1);
+  if constexpr (FULL) K = KMAX;
+  const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
+  for (int i = t; i < KMAX; i += BS) {
+    const int q = i + PAD * (i / R);
+    if (FULL || i < K) {
+      rows[q] = src[i];
+      if constexpr (!FULL) offmask[q] = ~uint64_t(0);
+    } else {
+      rows[q] = reinterpret_cast<const uint16_t*>(&g_median_pad2<E>[i - K < below ? 0 : 1]);
+      offmask[q] = 0;
+    }
+  }
+  __syncthreads();
+  // TAIL: `pairs` is the index of the pair holding the lone last column.
+  // Otherwise a column group past the end recomputes the last pair and does
+  // not store (every lane stays active through the DPP exchanges).
+  const int64_t e = TAIL ? pairs : (int64_t(blockIdx.x) * BS + t) / P;
+  const uint64_t boff = uint64_t(TAIL || e < pairs ? e : pairs - 1) * 4u;
+  uint32_t raw[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (j % 16 == 0 && j) __builtin_amdgcn_sched_barrier(0);
+    const int q = sub * (R + PAD) + j;
+    const uint64_t off = FULL ? boff : (boff & offmask[q]);
+    const auto row = reinterpret_cast<const char*>(rows[q]);
+    if constexpr (TAIL)
+      raw[j] = uint32_t(*as_global(reinterpret_cast<const uint16_t*>(row + off))) * 0x10001u;
+    else
+      raw[j] = __builtin_nontemporal_load(as_global(reinterpret_cast<const uint32_t*>(row + off)));
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test
+  uint32_t nanacc = 0;  // per half, max of |x| bits
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+    nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
+                                                                     __builtin_bit_cast(ushort2_t, raw[j] & 0x7fff7fffu)));
+  // first NaN per half in client (= slot) order as (slot << 16 | bits), only
+  // in waves holding a NaN column; KMAX << 16: none
+  int first_lo = KMAX << 16, first_hi = KMAX << 16;
+  if (__ballot((nanacc & 0xffffu) > E::kPosInf || (nanacc >> 16) > E::kPosInf)) {
+#pragma unroll
+    for (int j = R - 1; j >= 0; --j) {  // predicated, walked backwards: the lowest slot wins
+      const uint32_t x = raw[j];
+      const int s = (sub * R + j) << 16;
+      if ((x & 0x7fffu) > E::kPosInf) first_lo = s | int(x & 0xffffu);
+      if (((x >> 16) & 0x7fffu) > E::kPosInf) first_hi = s | int(x >> 16);
+    }
+#pragma unroll
+    for (int m = 1; m < P; m <<= 1) {
+      first_lo = min(first_lo, __shfl_xor(first_lo, m, 64));
+      first_hi = min(first_hi, __shfl_xor(first_hi, m, 64));
+    }
+  }
+  short2_t v[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = pk16_key(raw[j]);
+  pairwise_sort<R>(v);
+  pk_lanes_merge_levels<2, P, R>(v, sub);
+  // last level: the lower P/2 lanes keep the KMAX/2 smallest keys per half
+  pk_lanes_reverse_pair<P - 1>(v, (sub & (P / 2)) != 0);
+  short2_t m = v[0];
+#pragma unroll
+  for (int i = 1; i < R; ++i) m = __builtin_elementwise_max(m, v[i]);
+  if constexpr (P >= 4) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
+  if constexpr (P >= 8) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
+  uint32_t bits = pk16_bits(m);
+  if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
+  if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
+  if constexpr (TAIL) {
+    if (t == 0) out[2 * e] = uint16_t(bits);
+  } else if (sub == 0 && e < pairs) {
+    *reinterpret_cast<uint32_t*>(out + 2 * e) = bits;
+  }
+}
+
+template <int P, int R, class E, int BS = 256>
+int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  const int64_t pairs = N / 2;
+  const int64_t grid = (pairs * P + BS - 1) / BS;
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
+  if (pairs > 0) {
+    if (K == P * R)
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st,
+                         src, K, pairs, out);
+    else
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0,
+                         st, src, K, pairs, out);
+  }
+  if (N & 1)
+    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS>), dim3(1), dim3(BS), 0, st, src, K,
+                       pairs, out);
+  return check_launch("fedagg_median");
+}
+
 // Any number of clients (the path above 1024, where the lane-group sort runs
 // out of lanes per column): MSD radix select over 32-bit order keys, the
 // column tile streamed from memory once per 8-bit digit.  A block owns 64
@@ -1951,6 +2114,13 @@ template <class E>
 int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typename E::S* d_out, bool aligned,
                     hipStream_t st) {
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
+    if constexpr (sizeof(typename E::S) == 2) {
+      if (aligned && K <= 1024) {  // two columns per lane on packed int16 keys
+        if (K <= 256) return launch_median_pk16_lanes<4, 64, E>(d_src, K, N, d_out, st);
+        if (K <= 512) return launch_median_pk16_lanes<4, 128, E>(d_src, K, N, d_out, st);
+        return launch_median_pk16_lanes<8, 128, E>(d_src, K, N, d_out, st);
+      }
+    }
     if (K <= 256) return launch_median_lanes<4, 64, E>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
     if (K <= 512) return launch_median_lanes<4, 128, E>(d_src, K, N, d_out, st);
     if (K <= 1024) return launch_median_lanes<8, 128, E>(d_src, K, N, d_out, st);

@@ -163,7 +163,7 @@ def test_median_more_than_2_30_columns(dtype, cuda_device):
 
 @pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K", [1, 9, 33, 64, 127, 128, 129, 256, 257, 700, 1024])
+@pytest.mark.parametrize("K", [1, 9, 33, 64, 127, 128, 129, 200, 256, 257, 384, 511, 512, 513, 700, 1000, 1024])
 def test_median_16bit_rows_vs_oracle(aligned, dtype, K, cuda_device):
     """bf16 / f16 rows (a 16-bit model's stack): every kernel family (aligned
     rows with K <= 128 take the packed two-columns-per-lane kernel, with an odd
@@ -190,3 +190,34 @@ def test_median_16bit_rows_vs_oracle(aligned, dtype, K, cuda_device):
     dfn.median_rows(d_ptrs, K, N, out, aligned=aligned)
     exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
     gu.assert_same(out.cpu(), exp, f"median {dtype} K={K}")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K,N", [(256, 1_000), (512, 999), (700, 65), (1024, 1)])
+def test_median_16bit_lanes_first_nan_payload(dtype, K, N, cuda_device):
+    """The packed lane-group kernel (16-bit rows, 128 < K <= 1024): a NaN
+    column returns ITS FIRST NaN in client order, payload included, per half of
+    a packed pair, when the NaNs sit in different lanes of the column group;
+    an odd N takes the lone-last-column launch (N = 1: that launch alone)."""
+    g = torch.Generator(device=cuda_device).manual_seed(K)
+    rows = torch.empty((K, (N + 127) // 128 * 128), dtype=dtype, device=cuda_device)[:, :N]
+    rows.copy_(torch.randn(K, N, generator=g, device=cuda_device).to(dtype))
+    r16 = rows.view(torch.int16)
+    nan = 0x7f80 if dtype == torch.bfloat16 else 0x7c00
+    late, early = K - 3, K // 3 + 1  # different lanes of the group; the earlier client wins
+    cols = [c for c in (0, 1, 2, 5, N - 1) if c < N]
+    for c in cols:
+        r16[late, c] = nan | 0x11
+        r16[early, c] = ((nan | 0x23) | 0x8000) - 0x10000  # negative NaN, payload 0x23
+    if N > 5:
+        r16[late, 3] = nan | 0x5  # only one NaN: its pair neighbour (column 2) has two
+    out = torch.empty(N, dtype=dtype, device=cuda_device)
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    dfn.median_rows(d_ptrs, K, N, out, aligned=True)
+    o16 = out.view(torch.int16).cpu()
+    for c in cols:
+        assert int(o16[c]) & 0xffff == (nan | 0x23) | 0x8000, f"column {c}: {int(o16[c]) & 0xffff:#06x}"
+    if N > 5:
+        assert int(o16[3]) & 0xffff == nan | 0x5
+    exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
+    gu.assert_same(out.cpu(), exp, f"median {dtype} K={K} N={N}")

@@ -5,6 +5,8 @@
 fp32 K = 100 vs 128 over 25,610,152 columns (config 3's row), bf16 K = 100 vs
 128 over 86,567,656 (config 4's row, packed kernel), fp32 K = 129 / 256 / 512 /
 1024 over 4,000,037 columns, and the radix path at K = 1025 / 2048 over 1M.
+--sixteen: bf16 / f16 rows above 128 clients (the packed lane-group kernel),
+up to config 4's full shape (512 x 86,567,656 bf16, 88.6 GB).
 Each shape: 3 warm-up launches, then 10 timed with HIP events on the launch
 stream; median reported, with the algorithmic bytes ((K + 1) x N x esize)
 over that time.
@@ -67,6 +69,9 @@ def main():
     out = args[0] if args else "gpurun_out/median_bench.json"
     res = []
     shapes = [(dt, K, N, False) for dt, K, N in SHAPES]
+    if "--sixteen" in sys.argv:  # 16-bit rows above 128 clients (packed lane-group kernel), config 4's K = 512
+        shapes = [(torch.bfloat16, K, 4_000_037, False) for K in (129, 256, 384, 512, 700, 1024)]
+        shapes += [(torch.float16, 512, 4_000_037, False), (torch.bfloat16, 512, 86_567_656, False)]
     if "--one-row" in sys.argv:
         shapes += [(torch.float32, 128, 25_610_152, True), (torch.float32, 512, 4_000_037, True),
                    (torch.float32, 256, 4_000_037, True), (torch.float32, 1024, 4_000_037, True)]
