@@ -1373,8 +1373,8 @@ int launch_median_pk16(const uint16_t* const* src, int K, int64_t N, uint16_t* o
 
 // More than 128 clients, in registers: P adjacent lanes share one column,
 // each holding R of its KMAX = P·R (±inf-padded) values, slot s = sub·R + j =
-// client s (shipped: P = 4, R = 64 up to 256 clients, then R = 128 with P = 4
-// or 8).  Every lane sorts its R values with the pairwise network (all outputs
+// client s (shipped: P = 4, R = 64 up to 256 clients, then R = 128 with P = 4,
+// 8 or 16, i.e. up to 2048 clients).  Every lane sorts its R values with the pairwise network (all outputs
 // used, so nothing is pruned); the sorted runs are then merged across lanes as
 // in a bitonic merge sort:
 //   - "reverse pairing" of two sorted runs A, B of length L held by lane
@@ -1616,7 +1616,7 @@ __device__ uint32_t g_median_pad2[2] = {E::kNegInf * 0x10001u, E::kPosInf * 0x10
 template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
     const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out) {
-  static_assert(P == 2 || P == 4 || P == 8, "2, 4 or 8 lanes per column pair");
+  static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2, 4, 8 or 16 lanes per column pair");
   static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
   constexpr int KMAX = P * R, PAD = 2;
   __shared__ const uint16_t* rows[KMAX + PAD * P];
@@ -1687,6 +1687,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   for (int i = 1; i < R; ++i) m = __builtin_elementwise_max(m, v[i]);
   if constexpr (P >= 4) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
   if constexpr (P >= 8) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
+  if constexpr (P >= 16) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima
   uint32_t bits = pk16_bits(m);
   if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
   if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
@@ -2115,15 +2116,17 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
                     hipStream_t st) {
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
     if constexpr (sizeof(typename E::S) == 2) {
-      if (aligned && K <= 1024) {  // two columns per lane on packed int16 keys
+      if (aligned && K <= 2048) {  // two columns per lane on packed int16 keys
         if (K <= 256) return launch_median_pk16_lanes<4, 64, E>(d_src, K, N, d_out, st);
         if (K <= 512) return launch_median_pk16_lanes<4, 128, E>(d_src, K, N, d_out, st);
-        return launch_median_pk16_lanes<8, 128, E>(d_src, K, N, d_out, st);
+        if (K <= 1024) return launch_median_pk16_lanes<8, 128, E>(d_src, K, N, d_out, st);
+        return launch_median_pk16_lanes<16, 128, E>(d_src, K, N, d_out, st);
       }
     }
     if (K <= 256) return launch_median_lanes<4, 64, E>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
     if (K <= 512) return launch_median_lanes<4, 128, E>(d_src, K, N, d_out, st);
     if (K <= 1024) return launch_median_lanes<8, 128, E>(d_src, K, N, d_out, st);
+    if (K <= 2048) return launch_median_lanes<16, 128, E>(d_src, K, N, d_out, st);
     return launch_median_radix_stream<E>(d_src, K, N, d_out, st);  // no bound on K
   }
   if constexpr (sizeof(typename E::S) == 2) {

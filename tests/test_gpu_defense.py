@@ -113,16 +113,23 @@ def test_median_lanes_large_sampled(cuda_device):
     gu.assert_same(out[idx].cpu(), torch.from_numpy(exp), "median K=512 sampled")
 
 
+@pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K", [1025, 1500, 2048, 4097])
-def test_median_more_than_1024_clients(dtype, K, cuda_device):
+@pytest.mark.parametrize("K", [1025, 1500, 2048, 2049, 4097])
+def test_median_more_than_1024_clients(aligned, dtype, K, cuda_device):
     """No client bound, as torch.median has none (coordinate_wise_median_
-    defense.py:24-32): above 1024 clients the radix-select kernel, every
-    dtype, with duplicates, infinities, NaN columns (first NaN in client
-    order) and -0.0, a ragged last tile."""
+    defense.py:24-32): up to 2048 clients the 16-lane group kernels (packed for
+    aligned 16-bit rows), above that the radix-select kernel; every dtype,
+    with duplicates, infinities, NaN columns (first NaN in client order) and
+    -0.0, a ragged last tile and an odd column count."""
     N = 1_037
     g = torch.Generator(device=cuda_device).manual_seed(K)
-    rows = (torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125).to(dtype)
+    vals = (torch.randint(-50, 50, (K, N), generator=g, device=cuda_device).float() * 0.125).to(dtype)
+    if aligned:  # 256-B row stride, as bucket rows have
+        rows = torch.empty((K, 1_088), dtype=dtype, device=cuda_device)[:, :N]
+        rows.copy_(vals)
+    else:
+        rows = vals
     rows[:, 17:29] = torch.randn(K, 12, generator=g, device=cuda_device).to(dtype)
     rows[:, :7] = float("inf")
     rows[:, 7:9] = -float("inf")
@@ -131,7 +138,7 @@ def test_median_more_than_1024_clients(dtype, K, cuda_device):
     rows[:, 200:203] = -0.0
     d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
     out = torch.empty(N, dtype=dtype, device=cuda_device)
-    dfn.median_rows(d_ptrs, K, N, out, aligned=True)
+    dfn.median_rows(d_ptrs, K, N, out, aligned=aligned)
     exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
     gu.assert_same(out.cpu(), exp, f"median {dtype} K={K}")
 
@@ -193,9 +200,9 @@ def test_median_16bit_rows_vs_oracle(aligned, dtype, K, cuda_device):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K,N", [(256, 1_000), (512, 999), (700, 65), (1024, 1)])
+@pytest.mark.parametrize("K,N", [(256, 1_000), (512, 999), (700, 65), (1024, 1), (2048, 77)])
 def test_median_16bit_lanes_first_nan_payload(dtype, K, N, cuda_device):
-    """The packed lane-group kernel (16-bit rows, 128 < K <= 1024): a NaN
+    """The packed lane-group kernel (16-bit rows, 128 < K <= 2048): a NaN
     column returns ITS FIRST NaN in client order, payload included, per half of
     a packed pair, when the NaNs sit in different lanes of the column group;
     an odd N takes the lone-last-column launch (N = 1: that launch alone)."""
