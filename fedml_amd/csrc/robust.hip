@@ -312,19 +312,36 @@ __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __res
     for (int m = 0; m < 4; ++m) out[(4 * ti + k) * kPT + 4 * tj + m] = acc64[4 * k + m];
 }
 
-// D[a][b] and D[b][a] from the tiles' partials, summed over g in order
-__global__ void pair_finish_kernel(const double* __restrict__ partial, int G, int K, double* __restrict__ D) {
-  const int tp = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // pair index in the tile
-  if (e >= kPT * kPT) return;
+// D[a][b] and D[b][a] from the tiles' partials.  A block owns 64 pairs of a
+// tile (one coalesced 512-B row of the partials per chunk group); its four
+// waves sum the chunk groups g = q, q + 4, ... (8 loads in flight per lane),
+// and the four quarter sums are added in a fixed order: deterministic.  (One
+// thread per pair summing all G in sequence kept 16 blocks per tile busy:
+// 0.33 ms at config 3.)
+__global__ __launch_bounds__(256) void pair_finish_kernel(const double* __restrict__ partial, int G, int K,
+                                                          double* __restrict__ D) {
+  __shared__ double quarter[4][64];
+  const int tp = blockIdx.y, lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;  // pair index in the tile
+  const double* p = partial + int64_t(tp) * G * (kPT * kPT) + e;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int g = q;
+  for (; g + 28 < G; g += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += p[int64_t(g + 4 * u) * (kPT * kPT)];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)  // the last < 8 of this quarter's groups
+    if (g + 4 * u < G) s[u] += p[int64_t(g + 4 * u) * (kPT * kPT)];
+  quarter[q][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (q != 0) return;
+  const double t = (quarter[0][lane] + quarter[1][lane]) + (quarter[2][lane] + quarter[3][lane]);
   const int2 tile = tile_of(tp, (K + kPT - 1) / kPT);
   const int a = tile.x * kPT + e / kPT, b = tile.y * kPT + e % kPT;
   if (a >= K || b >= K) return;
-  double s = 0.0;
-  for (int g = 0; g < G; ++g) s += partial[(int64_t(tp) * G + g) * (kPT * kPT) + e];
-  if (a == b) s = 0.0;
-  D[int64_t(a) * K + b] = s;
-  if (tile.x != tile.y) D[int64_t(b) * K + a] = s;
+  D[int64_t(a) * K + b] = a == b ? 0.0 : t;
+  if (tile.x != tile.y) D[int64_t(b) * K + a] = t;
 }
 
 // ---------------------------------------------------------------------------
@@ -450,7 +467,7 @@ int fedagg_pairdist2_f32(const float* const* d_src, int32_t K, const int64_t* d_
   const int G = grid_groups(NT, n_chunks, work_len, int64_t(NT) * kPT * kPT);
   hipLaunchKernelGGL(pairdist_kernel, dim3(unsigned(NT), unsigned(G)), dim3(kBS), 0, st, d_src, K, d_chunks, n_chunks,
                      G, d_work);
-  hipLaunchKernelGGL(pair_finish_kernel, dim3(unsigned(kPT * kPT / 256), unsigned(NT)), dim3(256), 0, st, d_work, G,
+  hipLaunchKernelGGL(pair_finish_kernel, dim3(unsigned(kPT * kPT / 64), unsigned(NT)), dim3(256), 0, st, d_work, G,
                      K, d_out);
   return rcheck("fedagg_pairdist2_f32");
 }
