@@ -345,6 +345,174 @@ __global__ __launch_bounds__(256) void pair_finish_kernel(const double* __restri
 }
 
 // ---------------------------------------------------------------------------
+// Up to 128 clients: the pair triangle in ONE block per chunk group.  The
+// tiled kernel above runs a 64 x 64 diagonal tile as a full square (256 4x4
+// pair blocks for the 136 of its upper triangle): at K = 128 that is 768
+// block-threads for 528 useful blocks, at K = 64 256 for 136.  Here every
+// client sits in LDS per stage (128 clients x 64 columns = 32 KB,
+// [column][client], 4-client groups XOR-swizzled by column) and thread t owns
+// the t-th 4x4 block (bi <= bj, row-major) of the upper triangle: 576 threads
+// (9 waves) at K = 128, 192 at K = 64.  Per column and thread the work is the
+// tiled kernel's (two 16-byte LDS reads, 8 packed subtracts, 8 packed FMAs,
+// fp32 stage sums flushed into fp64).  A diagonal block computes all 16
+// slots; its mirrored halves are the same fp32 values.  Partials are laid out
+// [g][slot][block] so both their stores and the finish kernel's reads are
+// coalesced.
+constexpr int kTriMax = 128;   // clients the triangle kernel holds
+constexpr int kTriBS = 576;    // 9 waves: 528 blocks at K = 128
+constexpr int kTriLoads = 6;   // 4-client groups a wave stages per stage
+
+__device__ __forceinline__ int tri_swz(int c, int grp) { return c * kTriMax + ((grp ^ (c & 31)) << 2); }
+
+__host__ __device__ inline int tri_blocks(int K) {
+  const int nb = (K + 3) / 4;
+  return nb * (nb + 1) / 2;
+}
+// threads of the triangle kernel: every block owned, every 4-client group staged
+inline int tri_threads(int K) {
+  const int nb = (K + 3) / 4, nblk = tri_blocks(K);
+  int w = (nblk + 63) / 64;
+  const int wl = (nb + kTriLoads - 1) / kTriLoads;
+  return 64 * (w > wl ? w : wl);
+}
+
+// block index -> (bi, bj), row-major over the upper triangle of nb x nb
+__device__ __forceinline__ int2 tri_block(int t, int nb) {
+  int bi = 0;
+  while (t >= nb - bi) {
+    t -= nb - bi;
+    ++bi;
+  }
+  return int2{bi, bi + t};
+}
+
+__global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __restrict__ src, int K,
+                                                        const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
+                                                        double* __restrict__ partial) {
+  __shared__ f32x4 sX[kStage * kTriMax / 4];
+  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6), W = blockDim.x >> 6;
+  const int nb = (K + 3) >> 2, nblk = nb * (nb + 1) / 2;
+  const bool active = t < nblk;
+  const int2 blk = tri_block(active ? t : 0, nb);
+  // the groups this wave stages: wave, wave + W, ... (wave-uniform pointers
+  // in SGPRs; a row past K points at row 0 and is zeroed by the mask)
+  const float* rp[kTriLoads][4];
+  bool live[kTriLoads][4];
+#pragma unroll
+  for (int q = 0; q < kTriLoads; ++q)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cl = 4 * (wave + W * q) + k;
+      live[q][k] = cl < K;
+      rp[q][k] = src[cl < K ? cl : 0];
+    }
+  double acc64[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc64[k] = 0.0;
+  int64_t c = g;
+  int s0 = 0;
+  f32x4 v[kTriLoads];
+  int w_next = 0;
+  auto fetch = [&]() {  // the next stage's loads; false past the last stage
+    if (c >= n_chunks) return false;
+    const int len = int(chunks[2 * c + 1]);
+    const int64_t col0 = chunks[2 * c] + s0;
+    w_next = len - s0 < kStage ? len - s0 : kStage;
+    const int cc = lane < w_next ? lane : 0;
+#pragma unroll
+    for (int q = 0; q < kTriLoads; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x = __builtin_nontemporal_load(gptr(rp[q][k]) + col0 + cc);
+        const uint32_t m = (live[q][k] && lane < w_next) ? 0xffffffffu : 0u;  // a mask, not a branch
+        v[q][k] = __uint_as_float(__float_as_uint(x) & m);
+      }
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
+  bool have = fetch();
+  while (have) {
+    const int w = w_next;
+    __syncthreads();  // the previous stage's LDS reads are done
+#pragma unroll
+    for (int q = 0; q < kTriLoads; ++q)
+      if (wave + W * q < nb) sX[tri_swz(lane, wave + W * q) >> 2] = v[q];
+    have = fetch();  // next stage's loads in flight during this stage's compute
+    __syncthreads();
+    if (active) {
+      f32x2 acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
+      auto column = [&](int col) {
+        const f32x4 a = sX[tri_swz(col, blk.x) >> 2];
+        const f32x4 b = sX[tri_swz(col, blk.y) >> 2];
+        const f32x2 b01 = {b[0], b[1]}, b23 = {b[2], b[3]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 ak = {a[k], a[k]};
+          const f32x2 d0 = ak - b01, d1 = ak - b23;
+          acc[2 * k] = __builtin_elementwise_fma(d0, d0, acc[2 * k]);
+          acc[2 * k + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * k + 1]);
+        }
+      };
+      if (w == kStage) {
+#pragma unroll 8
+        for (int col = 0; col < kStage; ++col) column(col);
+      } else {
+        for (int col = 0; col < w; ++col) column(col);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc64[2 * k] += double(acc[k][0]);
+        acc64[2 * k + 1] += double(acc[k][1]);
+      }
+    }
+  }
+  if (active) {
+    double* out = partial + int64_t(g) * 16 * nblk + t;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) out[int64_t(j) * nblk] = acc64[j];  // slot j = 4k + m: pair (4bi + k, 4bj + m)
+  }
+}
+
+// D from the triangle kernel's partials: entry e = slot * nblk + block, the
+// chunk groups summed in four fixed-order quarters as in pair_finish_kernel
+__global__ __launch_bounds__(256) void tri_finish_kernel(const double* __restrict__ partial, int G, int K,
+                                                         double* __restrict__ D) {
+  __shared__ double quarter[4][64];
+  const int nb = (K + 3) >> 2, nblk = nb * (nb + 1) / 2, E = 16 * nblk;
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const int ec = e < E ? e : E - 1;
+  const double* p = partial + ec;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int g = q;
+  for (; g + 28 < G; g += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += p[int64_t(g + 4 * u) * E];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (g + 4 * u < G) s[u] += p[int64_t(g + 4 * u) * E];
+  quarter[q][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (q != 0 || e >= E) return;
+  const double tsum = (quarter[0][lane] + quarter[1][lane]) + (quarter[2][lane] + quarter[3][lane]);
+  const int j = e / nblk;
+  const int2 blk = tri_block(e - j * nblk, nb);
+  const int a = 4 * blk.x + (j >> 2), b = 4 * blk.y + (j & 3);
+  if (a >= K || b >= K) return;
+  // a diagonal block holds (a, b) and (b, a) as equal values: both write both
+  D[int64_t(a) * K + b] = a == b ? 0.0 : tsum;
+  D[int64_t(b) * K + a] = a == b ? 0.0 : tsum;
+}
+
+// ---------------------------------------------------------------------------
 // Clipped rebuild (norm_diff_clipping_defense.py:38-54): y = (x - r) / c + r
 // in fp32 with the reference's three roundings (c = fl32 of the clip divisor;
 // torch divides an fp32 tensor by a Python scalar in fp32).  Same shape as
@@ -427,6 +595,7 @@ int64_t fedagg_robust_work_len(int32_t kind, int32_t K, int64_t n_chunks) {
   if (n_chunks == 0) return 0;
   if (kind == FEDAGG_WORK_DIST2) return int64_t(K) * grid_groups(2, n_chunks, 0, 0);
   if (kind == FEDAGG_WORK_PAIRDIST2) {
+    if (K <= kTriMax) return int64_t(16) * tri_blocks(K) * grid_groups(4, n_chunks, 0, 0);
     const int NT = pair_tiles(K);
     return int64_t(NT) * grid_groups(NT, n_chunks, 0, 0) * (kPT * kPT);
   }
@@ -460,6 +629,15 @@ int fedagg_pairdist2_f32(const float* const* d_src, int32_t K, const int64_t* d_
   if (n_chunks == 0) {
     if (hipMemsetAsync(d_out, 0, sizeof(double) * K * K, st) != hipSuccess) return rcheck("fedagg_pairdist2_f32");
     return FEDAGG_OK;
+  }
+  if (K <= kTriMax) {  // the whole triangle in one block per chunk group
+    const int64_t per = int64_t(16) * tri_blocks(K);
+    if (work_len < per) return rset(FEDAGG_EINVAL, "fedagg_pairdist2_f32: workspace too small (fedagg_robust_work_len)");
+    const int G = grid_groups(4, n_chunks, work_len, per);
+    hipLaunchKernelGGL(pairtri_kernel, dim3(unsigned(G)), dim3(unsigned(tri_threads(K))), 0, st, d_src, K, d_chunks,
+                       n_chunks, G, d_work);
+    hipLaunchKernelGGL(tri_finish_kernel, dim3(unsigned((per + 63) / 64)), dim3(256), 0, st, d_work, G, K, d_out);
+    return rcheck("fedagg_pairdist2_f32");
   }
   const int NT = pair_tiles(K);
   if (work_len < int64_t(NT) * kPT * kPT)
