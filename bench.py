@@ -73,6 +73,9 @@ def parse():
                          "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
+    ap.add_argument("--clients", type=int, default=None,
+                    help="1 GPU: clients per GPU instead of the config's (e.g. config 4's median over all 512 "
+                         "clients: the median does not split along the client axis)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=5, help="cpu_baseline: timed runs after one warm-up")
     return ap.parse_args()
@@ -143,6 +146,20 @@ def cpu_baseline(bucket, ns, reps: int) -> dict:
                      "cgroup_quota_cpus": cpus["cgroup_quota_cpus"]}}
 
 
+def median_kernel_name(K: int, dt) -> str:
+    """The kernel fedagg_median dispatches for K clients of aligned rows
+    (median_dispatch in csrc/fedagg.hip)."""
+    name = str(dt).replace("torch.", "")
+    packed = dt in (torch.bfloat16, torch.float16)
+    if K <= 128:
+        kmax = next(m for m in ((32, 64, 96, 128) if packed else (8, 16, 24, 32, 48, 64, 96, 128)) if K <= m)
+        return f"median_{'pk16_' if packed else ''}kernel<{kmax}> ({name})"
+    if K > 2048:
+        return f"median_radix_stream_kernel ({name})"
+    p, r = (4, 64) if K <= 256 else (4, 128) if K <= 512 else (8, 128) if K <= 1024 else (16, 128)
+    return f"median_{'pk16_' if packed else ''}lanes_kernel<{p}, {r}> ({name})"
+
+
 def load_traffic(config: str, mode: str, world: int, variant: str = ""):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None.
@@ -174,6 +191,10 @@ def main():
     cfg = CONFIGS[a.config]
     entries = shapes.MODELS[cfg["model"]]()
     K = cfg["K"]
+    if a.clients is not None:
+        if world > 1 or a.clients < 1:
+            raise SystemExit("--clients is a 1-GPU override (>= 1)")
+        K = a.clients
     mode = a.mode if world > 1 else "single"
 
     server = None
@@ -402,7 +423,8 @@ def main():
 
     ms_per_step = elapsed / a.steps * 1e3
     value = world * K * n_elems / (elapsed / a.steps)
-    traffic = load_traffic(a.config, mode, world, a.fedopt or ("" if a.op == "fedavg" else a.op))
+    variant = (a.fedopt or ("" if a.op == "fedavg" else a.op)) + (f"@K{K}" if a.clients is not None else "")
+    traffic = load_traffic(a.config, mode, world, variant)
     line = {
         "metric": METRIC,
         "value": value,
@@ -417,7 +439,7 @@ def main():
         "dtype": "int64" if a.op in ("secagg", "lsa") else "bf16" if dom_dt == torch.bfloat16 else "f32",
         "data": "synthetic (base~N(0,0.05^2), client=base+0.01*eps, generated in HBM)",
         "config": {
-            "workload": cfg["desc"],
+            "workload": cfg["desc"] + (f" [--clients {K}]" if a.clients is not None else ""),
             "clients_per_gpu": K,
             "clients_total": K * world,
             "elements_per_client": n_elems,
@@ -445,7 +467,7 @@ def main():
                         "krum": "pairdist_kernel (packed fp32)", "dist2": "dist2_kernel",
                         "clip": "clip_diff_kernel"}[a.op]
                        if a.op in ("secagg", "lsa", "krum", "dist2", "clip") else
-                       f"median_kernel<128, {dom_dt}>" if a.op == "median" else
+                       median_kernel_name(K, dom_dt) if a.op == "median" else
                        ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
                          "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>"}
                         .get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>"))
