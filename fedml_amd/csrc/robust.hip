@@ -161,9 +161,8 @@ __global__ void sum_rows_kernel(const double* __restrict__ partial, int rows, in
 // client tiles (I <= J); a block owns one tile over the chunk group g.  Per
 // stage of 64 columns each wave loads 16 client rows of tile I (and of J) as
 // coalesced 256-B row segments into registers one stage ahead, then writes
-// them four rows at a time as one 16-byte LDS write per lane: sX[column][client], the 4-client groups XOR-swizzled by
-// column so both the staging writes and the compute reads are bank-conflict
-// free.  Thread (ti, tj) then owns clients 4ti..4ti+3 of I x 4tj..4tj+3 of J:
+// them four rows at a time as one 16-byte LDS write per lane: sX[column][client], rows padded by one group so
+// both the staging writes and the compute reads are bank-conflict free.  Thread (ti, tj) then owns clients 4ti..4ti+3 of I x 4tj..4tj+3 of J:
 // per column one 16-byte LDS read per side and 16 squared differences, as 8
 // packed fp32 subtracts and 8 packed fp32 FMAs (v_pk_add_f32 / v_pk_fma_f32).
 // fp32 sums over one stage (<= 64 columns) are flushed into fp64
@@ -171,7 +170,12 @@ __global__ void sum_rows_kernel(const double* __restrict__ partial, int rows, in
 constexpr int kPT = 64;      // clients per tile side
 constexpr int kStage = 64;   // columns per LDS stage
 
-__device__ __forceinline__ int swz(int c, int grp) { return c * kPT + ((grp ^ (c & 15)) << 2); }
+// [column][client] tile rows padded by one 4-client group (272 B): a staging
+// write (lane = column, 16 B) walks the banks 16 B apart, and a compute read's
+// address is the thread's group base plus a constant per unrolled column (an
+// immediate offset; the earlier XOR swizzle cost two VALU ops per column)
+constexpr int kRowF = kPT + 4;
+__device__ __forceinline__ int swz(int c, int grp) { return c * kRowF + (grp << 2); }
 
 // The 16 client rows (4 groups of 4) a wave stages for one 64-client side:
 // wave-uniform pointers, read once per block (kept in SGPRs); a row past K
@@ -247,8 +251,8 @@ __device__ __forceinline__ int2 tile_of(int tp, int T) {
 __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __restrict__ src, int K,
                                                        const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
                                                        double* __restrict__ partial) {
-  __shared__ f32x4 sA[kStage * kPT / 4];
-  __shared__ f32x4 sB[kStage * kPT / 4];
+  __shared__ f32x4 sA[kStage * kRowF / 4];
+  __shared__ f32x4 sB[kStage * kRowF / 4];
   const int tp = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
   const int2 tile = tile_of(tp, (K + kPT - 1) / kPT);
   const int I = tile.x * kPT, J = tile.y * kPT;
@@ -349,8 +353,8 @@ __global__ __launch_bounds__(256) void pair_finish_kernel(const double* __restri
 // tiled kernel above runs a 64 x 64 diagonal tile as a full square (256 4x4
 // pair blocks for the 136 of its upper triangle): at K = 128 that is 768
 // block-threads for 528 useful blocks, at K = 64 256 for 136.  Here every
-// client sits in LDS per stage (128 clients x 64 columns = 32 KB,
-// [column][client], 4-client groups XOR-swizzled by column) and thread t owns
+// client sits in LDS per stage (128 clients x 64 columns = 33 KB,
+// [column][client], rows padded by one 4-client group) and thread t owns
 // the t-th 4x4 block (bi <= bj, row-major) of the upper triangle: 576 threads
 // (9 waves) at K = 128, 192 at K = 64.  Per column and thread the work is the
 // tiled kernel's (two 16-byte LDS reads, 8 packed subtracts, 8 packed FMAs,
@@ -362,7 +366,8 @@ constexpr int kTriMax = 128;   // clients the triangle kernel holds
 constexpr int kTriBS = 576;    // 9 waves: 528 blocks at K = 128
 constexpr int kTriLoads = 6;   // 4-client groups a wave stages per stage
 
-__device__ __forceinline__ int tri_swz(int c, int grp) { return c * kTriMax + ((grp ^ (c & 31)) << 2); }
+constexpr int kTriRowF = kTriMax + 4;  // padded as the tiles' rows
+__device__ __forceinline__ int tri_swz(int c, int grp) { return c * kTriRowF + (grp << 2); }
 
 __host__ __device__ inline int tri_blocks(int K) {
   const int nb = (K + 3) / 4;
@@ -389,7 +394,7 @@ __device__ __forceinline__ int2 tri_block(int t, int nb) {
 __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __restrict__ src, int K,
                                                         const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
                                                         double* __restrict__ partial) {
-  __shared__ f32x4 sX[kStage * kTriMax / 4];
+  __shared__ f32x4 sX[kStage * kTriRowF / 4];
   const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6), W = blockDim.x >> 6;
   const int nb = (K + 3) >> 2, nblk = nb * (nb + 1) / 2;
