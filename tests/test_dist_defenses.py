@@ -138,6 +138,11 @@ def test_abi_argument_checks():
     assert lib.fedagg_robust_work_len(nat.WORK_DIST2, 0, 5) == -1
     assert lib.fedagg_robust_work_len(nat.WORK_PAIRDIST2, 130, 0) == 0
     assert lib.fedagg_robust_work_len(nat.WORK_PAIRDIST2, 130, 10) >= 6 * 64 * 64
+    # up to 128 clients the triangle kernel: 16 slots per 4x4 pair block of the
+    # upper triangle, one set per chunk group (at most one group per chunk)
+    assert lib.fedagg_robust_work_len(nat.WORK_PAIRDIST2, 128, 10) == 16 * 528 * 10
+    assert lib.fedagg_robust_work_len(nat.WORK_PAIRDIST2, 64, 3) == 16 * 136 * 3
+    assert lib.fedagg_robust_work_len(nat.WORK_PAIRDIST2, 5, 1) == 16 * 3
     assert lib.fedagg_robust_work_len(7, 4, 4) == -1
     assert lib.fedagg_dist2_f32(None, 0, None, None, 0, None, None, 0, None) == -1
     assert b"K must be" in lib.fedagg_last_error()
