@@ -68,7 +68,8 @@ def parse():
                     choices=["sgd", "adam", "adamw", "adagrad", "rmsprop"],
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
                          "or Adam / Adagrad lr=1.0 with torch defaults)")
-    ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa", "krum", "dist2", "clip"],
+    ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa", "krum", "dist2", "clip",
+                                                       "rlr"],
                     help="1 GPU: the reduction measured (median = the wise_median defense kernel; secagg = "
                          "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -279,6 +280,24 @@ def main():
 
         n_launch = 1
         dom_bytes = (K + 1) * gd.length * gd.rows.element_size()
+    elif a.op == "rlr":
+        # the robust-learning-rate defense: FedAvg chain + per-coordinate sign
+        # sum + the lr rule, one pass over the fp32 row (threshold K/4)
+        from fedml_amd import kernels as kn
+
+        gd = bucket.groups[torch.float32]
+        rlr_out = torch.empty(gd.padded, dtype=torch.float32, device=dev)
+        rlr_w = kn.weights_for([n / sum(ns_local) for n in ns_local], torch.float32, dev)
+
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record()
+            kn.wsum_rlr_ptrs(gd.d_ptrs, rlr_w, K, gd.length, float(max(1, K // 4)), rlr_out, True)
+            if ev is not None:
+                ev[1].record()
+
+        n_launch = 1
+        dom_bytes = (K + 1) * gd.length * 4
     elif a.op in ("krum", "dist2", "clip"):
         # the distance defenses' kernels over the fp32 row's weight keys
         # (csrc/robust.hip): krum = the K x K pair kernel, dist2 = every
@@ -465,8 +484,8 @@ def main():
             "traffic": traffic,
             "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>",
                         "krum": "pairdist_kernel (packed fp32)", "dist2": "dist2_kernel",
-                        "clip": "clip_diff_kernel"}[a.op]
-                       if a.op in ("secagg", "lsa", "krum", "dist2", "clip") else
+                        "clip": "clip_diff_kernel", "rlr": "reduce_kernel<OpF32Rlr, RlrEpi>"}[a.op]
+                       if a.op in ("secagg", "lsa", "krum", "dist2", "clip", "rlr") else
                        median_kernel_name(K, dom_dt) if a.op == "median" else
                        ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
                          "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>"}

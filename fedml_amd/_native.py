@@ -54,6 +54,7 @@ SIGNATURES = {
     "fedagg_wsum_fedopt_adamw_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _F, _I32, _U32, _P]),
     "fedagg_wsum_fedopt_rmsprop_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _F, ctypes.c_double, _F, _U32,
                                                       _P]),
+    "fedagg_wsum_rlr_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _P, _U32, _P]),
     "fedagg_median_f32": (ctypes.c_int, [_P, _I32, _I64, _P, _U32, _P]),
     "fedagg_median": (ctypes.c_int, [_I32, _P, _I32, _I64, _P, _U32, _P]),
     "fedagg_sum_mod_i64": (ctypes.c_int, [_P, _I32, _I64, _I64, _P, _U32, _P]),

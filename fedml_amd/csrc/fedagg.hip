@@ -547,6 +547,43 @@ struct LsaEpi {
   __device__ __forceinline__ void one(int64_t e, int64_t acc) const { out[e] = one_value(acc, mask[e]); }
 };
 
+// Robust learning rate (RobustLearningRateDefense.run,
+// core/security/defense/robust_learning_rate_defense.py:35-62): the FedAvg
+// chain of the FedAvg branch, and in the same pass the coordinate's sum of the
+// clients' torch.sign values (exact in fp32 below 2^24 clients; a NaN input
+// makes it NaN, as torch.sign does); the epilogue applies
+//   lr = |Σ sign|;  lr[lr < thr] = -1;  lr[lr >= thr] = 1;  out = lr * avg
+// in that order (a NaN lr stays NaN), the multiply by ±1 exact.
+struct RlrAcc {
+  float a, s;
+};
+__device__ __forceinline__ float sign_of(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : x); }  // ±0, NaN: x
+struct OpF32Rlr {
+  using in_t = float; using out_t = float; using acc_t = RlrAcc; using w_t = float;
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return {x * w, sign_of(x)}; }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return {a.a + x * w, a.s + sign_of(x)}; }
+};
+struct RlrEpi {
+  float* out;
+  float thr;  // fl32(robust_threshold): torch compares the fp32 sign sum with the Python number in fp32
+  static constexpr int E = 4;
+  struct Pre {};
+  __device__ __forceinline__ Pre pre(int64_t) const { return {}; }
+  __device__ __forceinline__ float one_value(RlrAcc acc) const {
+    float lr = fabsf(acc.s);
+    lr = lr < thr ? -1.f : lr;
+    lr = lr >= thr ? 1.f : lr;
+    return lr * acc.a;
+  }
+  __device__ __forceinline__ void pack(int64_t off, const RlrAcc (&acc)[E], const Pre&) const {
+    float o[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) o[e] = one_value(acc[e]);
+    store_pack<float, E>(out + off, o);
+  }
+  __device__ __forceinline__ void one(int64_t e, RlrAcc acc) const { out[e] = one_value(acc); }
+};
+
 // Scalar path: one element at a time, identical arithmetic.  Used for the
 // ragged tail of a tensor and for unaligned pointers.
 template <class OP, class EPI, class WS>
@@ -2155,6 +2192,25 @@ int fedagg_wsum_f32(const float* const* d_src, const float* d_w, int32_t K, int6
                     uint32_t flags, fedagg_stream_t stream) {
   return launch<OpF32>(reinterpret_cast<const void* const*>(d_src), d_w, K, N, d_out, flags, stream,
                        "fedagg_wsum_f32");
+}
+
+int fedagg_wsum_rlr_f32(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float threshold,
+                        float* d_out, uint32_t flags, fedagg_stream_t stream) {
+  const char* name = "fedagg_wsum_rlr_f32";
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, std::string(name) + ": K must be >= 1 and N >= 0");
+  if (!d_src || !d_out || !d_w) return set_error(FEDAGG_EINVAL, std::string(name) + ": null pointer");
+  if (N == 0) return FEDAGG_OK;
+  const Seg<OpF32Rlr> s{d_src, N};
+  const RlrEpi epi{d_out, threshold};
+  const bool al = (flags & FEDAGG_ALIGNED16) != 0;
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  if (flags & FEDAGG_HOST_WEIGHTS) {
+    InlW<float> iw;
+    if (!inline_weights<float>(d_w, K, &iw))
+      return set_error(FEDAGG_EINVAL, std::string(name) + ": FEDAGG_HOST_WEIGHTS needs K <= 256");
+    return launch_epi<OpF32Rlr>(s, epi, iw, K, al, st, name);
+  }
+  return launch_epi<OpF32Rlr>(s, epi, PtrW<float>{d_w}, K, al, st, name);
 }
 
 int fedagg_wsum_bf16(const uint16_t* const* d_src, const float* d_w, int32_t K, int64_t N, uint16_t* d_out,

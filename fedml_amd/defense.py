@@ -81,8 +81,14 @@ DEFENSE_MULTIKRUM = "multikrum"
 DEFENSE_NORM_DIFF_CLIPPING = "norm_diff_clipping"
 DEFENSE_SLSGD = "slsgd"
 DEFENSE_CCLIP = "cclip"
+DEFENSE_ROBUST_LEARNING_RATE = "robust_learning_rate"
 SUPPORTED = (DEFENSE_WISE_MEDIAN, DEFENSE_TRIMMED_MEAN, DEFENSE_KRUM, DEFENSE_MULTIKRUM, DEFENSE_NORM_DIFF_CLIPPING,
-             DEFENSE_SLSGD, DEFENSE_CCLIP)
+             DEFENSE_SLSGD, DEFENSE_CCLIP, DEFENSE_ROBUST_LEARNING_RATE)
+# FedMLDefender constructs these but lists them under none of its
+# before / on / after-aggregation hooks (fedml_defender.py:131-154), so the
+# plugin path aggregates as if no defense were set; they act only through
+# FedMLDefender.defend (the MPI FedAvg aggregator)
+PLUGIN_IDENTITY = (DEFENSE_ROBUST_LEARNING_RATE,)
 
 
 def is_weight_param(k: str) -> bool:
@@ -475,3 +481,62 @@ def cclip_after_aggregation(global_model, initial_guess, device=None):
     guess[k] + global[k] for every key (a two-row sum, weights 1 and 1:
     fl(1 * x) = x, so one rounding, as torch's add)."""
     return mix_two(initial_guess, global_model, 1.0, 1.0, device)
+
+
+# ---- Robust learning rate (sign agreement per coordinate) ----------------------
+
+def robust_learning_rate(raw_client_grad_list: Sequence, robust_threshold, base_aggregation_func=None,
+                         device=None) -> "OrderedDict[str, torch.Tensor]":
+    """RobustLearningRateDefense.run (robust_learning_rate_defense.py:35-62) on
+    the GPU: ONE pass over the clients' rows computes the FedAvg chain and the
+    per-coordinate sum of their signs (fedagg_wsum_rlr_f32), and the key
+    becomes lr * avg with lr = +1 where |Σ sign| >= threshold, else -1.
+    As in the reference: threshold 0 hands the list to base_aggregation_func,
+    the weights are n_i / Σn (ZeroDivisionError at Σn = 0), a missing key
+    raises KeyError, and client 0's dict is returned with its keys rebound
+    (integer keys come back fp32: torch's fp32 average times the integer lr)."""
+    if robust_threshold == 0:
+        return base_aggregation_func(raw_client_grad_list)
+    total = 0
+    for n, _ in raw_client_grad_list:
+        total += n
+    K = len(raw_client_grad_list)
+    ws = [n / total for n, _ in raw_client_grad_list]
+    num0, avg_params = raw_client_grad_list[0]
+    keys = list(avg_params.keys())
+    on_dev = avg_params[keys[0]].is_cuda
+    bucket, dev = _float_bucket(avg_params, K, "robust_learning_rate", device)
+    with torch.cuda.device(dev):
+        for i, (_, d) in enumerate(raw_client_grad_list):
+            _put_float(bucket, i, d, keys)
+        bucket.sync_ingest()
+        outs = bucket.new_outputs()
+        g = bucket.groups[torch.float32]
+        kn.wsum_rlr_ptrs(g.d_ptrs, kn.weights_for(ws, torch.float32, dev), K, g.length,
+                         float(np.float32(robust_threshold)), outs[torch.float32], True)
+        res = _like_input(OrderedDict((k, t.clone()) for k, t in bucket.unflatten(outs).items()), on_dev)
+    for k in keys:
+        avg_params[k] = res[k]
+    return avg_params
+
+
+class RobustLearningRateDefense:
+    """Drop-in for FedML's RobustLearningRateDefense (the object
+    FedMLDefender.init builds for defense_type "robust_learning_rate"):
+    FedMLDefender.defend -> run() aggregates on the GPU."""
+
+    def __init__(self, config):
+        self.robust_threshold = config.robust_threshold
+        self.server_learning_rate = 1
+
+    def run(self, raw_client_grad_list, base_aggregation_func=None, extra_auxiliary_info=None):
+        return robust_learning_rate(raw_client_grad_list, self.robust_threshold, base_aggregation_func)
+
+    def defend_before_aggregation(self, raw_client_grad_list, extra_auxiliary_info=None):
+        return None  # BaseDefenseMethod's default (defense_base.py:11-24)
+
+    def defend_on_aggregation(self, raw_client_grad_list, base_aggregation_func=None, extra_auxiliary_info=None):
+        return None
+
+    def get_malicious_client_idxs(self):
+        return []

@@ -83,6 +83,20 @@ def aligned16(ptrs: Sequence[int]) -> bool:
     return (functools.reduce(operator.or_, ptrs, 0) & 15) == 0
 
 
+def wsum_rlr_ptrs(d_ptrs: torch.Tensor, d_w, K: int, N: int, threshold: float, out: torch.Tensor,
+                  aligned: bool) -> None:
+    """fedagg_wsum_rlr_f32: the FedAvg chain and the robust-learning-rate sign
+    rule over K fp32 sources in one pass (RobustLearningRateDefense.run)."""
+    _require_cuda(out, "wsum_rlr")
+    if out.dtype != torch.float32:
+        raise TypeError("robust learning rate: fp32 rows and output")
+    flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0
+    if isinstance(d_w, HostWeights):
+        flags |= nat.FEDAGG_HOST_WEIGHTS
+    nat.check(nat.lib().fedagg_wsum_rlr_f32(d_ptrs.data_ptr(), d_w.data_ptr(), K, N, float(threshold),
+                                            out.data_ptr(), flags, nat.stream_handle()), "wsum_rlr")
+
+
 def wsum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int,
               out: torch.Tensor, aligned: bool, acc_mode: int = ACC_REFERENCE) -> None:
     """Weighted sum over K sources given as a device pointer table."""

@@ -11,7 +11,10 @@ reductions over the client axis and run on the GPU too (fedml_amd.defense):
 ``defense_type`` "wise_median" (on aggregation) and "trimmed_mean" (before
 aggregation), dispatched exactly as FedMLDefender does
 (core/security/fedml_defender.py:131-171); so do the distance-based
-"krum" / "multikrum", "norm_diff_clipping", "slsgd" and "cclip".  The other optional hooks (FHE,
+"krum" / "multikrum", "norm_diff_clipping", "slsgd" and "cclip".  "robust_learning_rate" is accepted and,
+as in FedML, leaves the plugin path a plain FedAvg (FedMLDefender lists it under
+none of the three hooks; its GPU version, fedml_amd.defense.
+RobustLearningRateDefense, runs where FedML calls FedMLDefender.defend).  The other optional hooks (FHE,
 differential privacy, attacks, other defenses, contribution assessment) are
 outside this build's scope: disabled (FedML's default) they are the identity,
 as in the reference; enabling one raises NotImplementedError instead of
@@ -49,6 +52,8 @@ def _check_flags(args) -> None:
             raise NotImplementedError(f"defense_type {dt!r}: fedml_amd runs {dfn.SUPPORTED} on the GPU")
         if dt == dfn.DEFENSE_SLSGD:
             dfn.slsgd_alpha_check(args.alpha)  # SLSGDDefense.__init__ raises at FedMLDefender.init
+        if dt == dfn.DEFENSE_ROBUST_LEARNING_RATE:
+            args.robust_threshold  # RobustLearningRateDefense.__init__ reads it at FedMLDefender.init
 
 
 def _defense(args):

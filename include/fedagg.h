@@ -306,6 +306,19 @@ int fedagg_scale_diff_f32(const float* const* d_src, int32_t K, const float* d_r
                           const float* d_scale, int64_t N, float* const* d_dst,
                           fedagg_stream_t stream);
 
+/* The robust-learning-rate defense (RobustLearningRateDefense.run,
+ * core/security/defense/robust_learning_rate_defense.py:35-62, reached through
+ * FedMLDefender.defend from simulation/mpi/fedavg/FedAVGAggregator.py:83-88):
+ * per element, the FedAvg chain of fedagg_wsum_f32 (avg) and the sum of the
+ * clients' torch.sign values (s), in one pass; then
+ *   lr = |s|; lr = lr < thr ? -1 : lr; lr = lr >= thr ? 1 : lr; out = lr * avg
+ * (a NaN input leaves lr, and so out, NaN).  threshold = fl32 of the config's
+ * robust_threshold (!= 0; 0 means plain aggregation, handled by the caller).
+ * Flags as fedagg_wsum_f32. */
+int fedagg_wsum_rlr_f32(const float* const* d_src, const float* d_w, int32_t K,
+                        int64_t N, float threshold, float* d_out, uint32_t flags,
+                        fedagg_stream_t stream);
+
 /* Secure aggregation in a finite field (LightSecAgg), numpy int64 semantics:
  * wrapping adds, floor modulo.  p > 0.
  *

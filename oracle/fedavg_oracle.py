@@ -732,3 +732,32 @@ def lsa_reconstruct(dicts, mask, p, q_bits):
         t = torch.from_numpy(np.asarray(v, dtype=np.float64).astype(np.float32).reshape(v.shape if v.ndim else (1,)))
         out[k] = t * (1 / K)
     return out
+
+
+def robust_learning_rate(raw_grad_list, robust_threshold, base_aggregation_func=None):
+    """RobustLearningRateDefense.run (core/security/defense/robust_learning_rate_defense.py:35-62):
+    per key, the FedAvg chain (sample-count weights n_i / Σn) and the sum of the
+    clients' torch.sign values; lr = |Σ sign|, set to -1 where below the
+    threshold, then to 1 where at or above it (in that order), and the key
+    becomes lr * avg.  Keys are rebound in client 0's dict, which is returned.
+    robust_threshold == 0 hands the list to base_aggregation_func."""
+    if robust_threshold == 0:
+        return base_aggregation_func(raw_grad_list)
+    total = 0
+    for n, _ in raw_grad_list:
+        total += n
+    num0, avg_params = raw_grad_list[0]
+    ws = [n / total for n, _ in raw_grad_list]
+    thr = np.float32(robust_threshold)
+    for k in list(avg_params.keys()):
+        ts = [d[k] for _, d in raw_grad_list]
+        avg = to_np(wsum(ts, ws)).astype(np.float32)
+        sgn = np.zeros(avg.shape, dtype=np.float32)
+        for t in ts:
+            sgn = np.asarray(sgn + np.sign(_f32(t)), dtype=np.float32)
+        lr = np.abs(sgn)
+        with np.errstate(invalid="ignore"):
+            lr = np.where(lr < thr, np.float32(-1), lr)
+            lr = np.where(lr >= thr, np.float32(1), lr)
+        avg_params[k] = torch.from_numpy(np.asarray(lr * avg, dtype=np.float32)).view(ts[0].size())
+    return avg_params

@@ -260,7 +260,7 @@ class DefenseArgs(Args):
         self.enable_defense = True
         self.defense_type = spec["defense"]
         for a in ("beta", "byzantine_client_num", "krum_param_m", "norm_bound", "trim_param_b", "alpha", "option_type",
-                  "tau", "bucket_size"):
+                  "tau", "bucket_size", "robust_threshold"):
             if a in spec:
                 setattr(self, a, spec[a])
 
@@ -315,6 +315,21 @@ _dist("cclip_dist_k10_s3_tau", "cclip", 10, DIST_KEYS, 331, bucket_size=3, tau=0
 _dist("cclip_fake_k9_s4", "cclip", 9, None, 0, fake_model_list=True, bucket_size=4, tau=2, np_seed=3)
 
 
+# Robust learning rate (robust_learning_rate_defense.py, reached through
+# FedMLDefender.defend in simulation/mpi/fedavg/FedAVGAggregator.py:83-88):
+# RobustLearningRateDefense.run itself.  "flip" negates the listed clients'
+# float keys (sign-disagreeing updates); threshold 0 is the plain-aggregation
+# branch (base function: FedMLAggOperator.agg).
+_dist("rlr_fake_k10_t1", "robust_learning_rate", 10, None, 0, fake_model_list=True, robust_threshold=1)
+_dist("rlr_resnet_mini_k8_t4", "robust_learning_rate", 8, RESNET_MINI, 340, robust_threshold=4, flip=[1, 2, 5])
+_dist("rlr_dist_k16_t10", "robust_learning_rate", 16, DIST_KEYS, 341, robust_threshold=10, flip=[0, 3, 4, 9, 11],
+      outliers={7: 2.0})
+_dist("rlr_ragged_k9_t3_5", "robust_learning_rate", 9, [k for k in RAGGED_F32 if k[0] != "e"], 342,
+      robust_threshold=3.5, flip=[2, 6])
+_dist("rlr_ragged_k5_tneg", "robust_learning_rate", 5, RAGGED_F32[:4], 343, robust_threshold=-2, flip=[0])
+_dist("rlr_resnet_mini_k6_t0", "robust_learning_rate", 6, RESNET_MINI, 344, robust_threshold=0)
+
+
 def dist_inputs(spec):
     """(raw_grad_list, global_model) of a distance-defense case."""
     if spec.get("fake_model_list"):
@@ -326,6 +341,10 @@ def dist_inputs(spec):
         for k, t in raw[int(i)][1].items():
             if t.is_floating_point():
                 t.mul_(1.0 + f)
+    for i in spec.get("flip", []):
+        for k, t in raw[int(i)][1].items():
+            if t.is_floating_point():
+                t.neg_()
     glob = host_clients(entries, 1, spec["seed"] + 7)[0][1]
     return raw, glob
 

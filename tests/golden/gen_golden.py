@@ -88,6 +88,13 @@ def run_dist_case(FedMLAggOperator, spec):
     arrays = {}
     ids = [id(item) for item in raw]
     try:
+        if spec["defense"] == "robust_learning_rate":
+            from fedml.core.security.defense.robust_learning_rate_defense import RobustLearningRateDefense
+
+            d = RobustLearningRateDefense(args)
+            res = d.run(raw, lambda lst: FedMLAggOperator.agg(args, lst))
+            meta["returns_client0_dict"] = res is raw[0][1]
+            raise _Done(res)
         if spec["defense"] == "slsgd":
             from fedml.core.security.defense.slsgd_defense import SLSGDDefense
 

@@ -15,6 +15,8 @@ before the add), unclipped ones bit for bit.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import numpy as np
 import pytest
 import torch
@@ -32,6 +34,7 @@ SLSGD = [c["name"] for c in cases.DIST_CASES if c["defense"] == "slsgd"]
 CCLIP = [c["name"] for c in cases.DIST_CASES if c["defense"] == "cclip"]
 KRUM = [c["name"] for c in cases.DIST_CASES if c["defense"] in ("krum", "multikrum")]
 CLIP = [c["name"] for c in cases.DIST_CASES if c["defense"] == "norm_diff_clipping"]
+RLR = [c["name"] for c in cases.DIST_CASES if c["defense"] == "robust_learning_rate"]
 
 
 def _m(spec):
@@ -201,3 +204,30 @@ def assert_close_groups(res, meta, arrays, name):
     for k, t in res.items():
         np.testing.assert_allclose(t.cpu().numpy().reshape(-1), arrays[f"o0:{k}"].reshape(-1), rtol=1e-5, atol=1e-6,
                                    err_msg=f"{name} {k}")
+
+
+@pytest.mark.parametrize("name", RLR)
+def test_oracle_robust_learning_rate_matches_reference(name):
+    """RobustLearningRateDefense.run restated (oracle) vs the reference's own
+    outputs, bit for bit; client 0's dict is the returned object."""
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, _ = cases.dist_inputs(spec)
+    args = cases.DefenseArgs(spec)
+    res = orc.robust_learning_rate(raw, spec["robust_threshold"], lambda lst: orc.agg(args, lst))
+    assert (res is raw[0][1]) == meta["returns_client0_dict"]
+    gu.assert_groups(res, meta, arrays, name)
+
+
+def test_oracle_robust_learning_rate_signs():
+    """The lr rule on a hand case: 3 clients, threshold 2 -> coordinates whose
+    signs agree keep the average, split or zero ones flip it, NaN stays NaN."""
+    t = [torch.tensor([1.0, 2.0, -1.0, 0.0, float("nan")]), torch.tensor([3.0, -2.0, -1.0, 0.0, 1.0]),
+         torch.tensor([2.0, 1.0, -4.0, 0.0, 1.0])]
+    raw = [(1, OrderedDict(x=t[0].clone())), (1, OrderedDict(x=t[1].clone())), (2, OrderedDict(x=t[2].clone()))]
+    out = orc.robust_learning_rate(raw, 2)["x"].numpy()
+    w = [np.float32(0.25), np.float32(0.25), np.float32(0.5)]
+    avg = (t[0].numpy() * w[0] + t[1].numpy() * w[1]) + t[2].numpy() * w[2]
+    assert out[0] == avg[0] and out[2] == avg[2]  # |3| >= 2
+    assert out[1] == -avg[1]  # |1 - 1 + 1| = 1 < 2
+    assert out[3] == 0.0 and np.isnan(out[4])

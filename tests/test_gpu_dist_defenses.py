@@ -275,3 +275,67 @@ def test_cclip_matches_reference(name, device_inputs, cuda_device):
     assert_cclip_list(lst, meta, arrays, name)
     res = agg.on_after_aggregation(agg.aggregate(lst))
     assert_close_groups(res, meta, arrays, name)
+
+
+RLR = [c["name"] for c in cases.DIST_CASES if c["defense"] == "robust_learning_rate"]
+
+
+@pytest.mark.parametrize("device_inputs", [False, True])
+@pytest.mark.parametrize("name", RLR)
+def test_robust_learning_rate_matches_reference(name, device_inputs, cuda_device):
+    """RobustLearningRateDefense.run through the GPU drop-in (one fused pass:
+    FedAvg chain + sign sum + the lr rule) vs the reference's own outputs, bit
+    for bit; client 0's dict comes back with its keys rebound, on the inputs'
+    device; threshold 0 goes to the base function (here our FedAvg)."""
+    from fedml_amd.agg_operator import FedMLAggOperator
+
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw, _ = cases.dist_inputs(spec)
+    if device_inputs:
+        raw = _to(raw, cuda_device)
+    args = cases.DefenseArgs(spec)
+    d = dfn.RobustLearningRateDefense(args)
+    res = d.run(raw, lambda lst: FedMLAggOperator.agg(args, lst))
+    assert (res is raw[0][1]) == meta["returns_client0_dict"]
+    for t in res.values():
+        assert t.is_cuda == device_inputs
+    gu.assert_groups(OrderedDict((k, t.cpu()) for k, t in res.items()), meta, arrays, name)
+
+
+def test_robust_learning_rate_plugin_path_is_plain_fedavg(cuda_device):
+    """As in FedML, "robust_learning_rate" is not one of FedMLDefender's
+    before / on / after hooks: the plugin path aggregates plain FedAvg."""
+    spec = next(c for c in cases.DIST_CASES if c["name"] == "rlr_resnet_mini_k8_t4")
+    raw, _ = cases.dist_inputs(spec)
+    args = cases.DefenseArgs(spec)
+    agg = _Agg(args)
+    lst, idxs = agg.on_before_aggregation(cases.clone_raw(raw))
+    assert idxs == list(range(len(raw)))
+    res = agg.on_after_aggregation(agg.aggregate(lst))
+    want = orc.agg(args, cases.clone_raw(raw))
+    for k in want:
+        gu.assert_same(res[k].cpu(), want[k], k)
+
+
+@pytest.mark.parametrize("K,N", [(3, 1), (7, 4099), (128, 1_000_003), (300, 65_537)])
+def test_robust_learning_rate_kernel_vs_oracle(K, N, cuda_device):
+    """The fused kernel on bucket-shaped rows vs the oracle: ragged N (edge
+    path), K above the 256 inline weights (device weight array), sign-split,
+    zero and NaN / inf coordinates, thresholds that flip some coordinates."""
+    g = torch.Generator().manual_seed(K + N)
+    base = torch.randn(N, generator=g)
+    rows = [base + 0.5 * torch.randn(N, generator=g) for _ in range(K)]
+    for r in rows[: K // 3]:
+        r.neg_()
+    rows[0][: min(N, 5)] = 0.0
+    if N > 20:
+        rows[K // 2][10] = float("nan")
+        rows[-1][11] = float("inf")
+        rows[1 % K][12] = -float("inf")
+    raw = [(float(10 + i % 7), OrderedDict(x=r.clone())) for i, r in enumerate(rows)]
+    thr = max(1, K // 3)
+    want = orc.robust_learning_rate([(n, OrderedDict(x=d["x"].clone())) for n, d in raw], thr)["x"]
+    dev_raw = _to(raw, cuda_device)
+    got = dfn.robust_learning_rate(dev_raw, thr)["x"]
+    gu.assert_same(got.cpu(), want, f"rlr K={K} N={N}")
