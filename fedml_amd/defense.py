@@ -82,13 +82,14 @@ DEFENSE_NORM_DIFF_CLIPPING = "norm_diff_clipping"
 DEFENSE_SLSGD = "slsgd"
 DEFENSE_CCLIP = "cclip"
 DEFENSE_ROBUST_LEARNING_RATE = "robust_learning_rate"
+DEFENSE_WEAK_DP = "weak_dp"
 SUPPORTED = (DEFENSE_WISE_MEDIAN, DEFENSE_TRIMMED_MEAN, DEFENSE_KRUM, DEFENSE_MULTIKRUM, DEFENSE_NORM_DIFF_CLIPPING,
-             DEFENSE_SLSGD, DEFENSE_CCLIP, DEFENSE_ROBUST_LEARNING_RATE)
+             DEFENSE_SLSGD, DEFENSE_CCLIP, DEFENSE_ROBUST_LEARNING_RATE, DEFENSE_WEAK_DP)
 # FedMLDefender constructs these but lists them under none of its
 # before / on / after-aggregation hooks (fedml_defender.py:131-154), so the
 # plugin path aggregates as if no defense were set; they act only through
 # FedMLDefender.defend (the MPI FedAvg aggregator)
-PLUGIN_IDENTITY = (DEFENSE_ROBUST_LEARNING_RATE,)
+PLUGIN_IDENTITY = (DEFENSE_ROBUST_LEARNING_RATE, DEFENSE_WEAK_DP)
 
 
 def is_weight_param(k: str) -> bool:

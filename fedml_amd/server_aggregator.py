@@ -11,10 +11,11 @@ reductions over the client axis and run on the GPU too (fedml_amd.defense):
 ``defense_type`` "wise_median" (on aggregation) and "trimmed_mean" (before
 aggregation), dispatched exactly as FedMLDefender does
 (core/security/fedml_defender.py:131-171); so do the distance-based
-"krum" / "multikrum", "norm_diff_clipping", "slsgd" and "cclip".  "robust_learning_rate" is accepted and,
-as in FedML, leaves the plugin path a plain FedAvg (FedMLDefender lists it under
-none of the three hooks; its GPU version, fedml_amd.defense.
-RobustLearningRateDefense, runs where FedML calls FedMLDefender.defend).  The other optional hooks (FHE,
+"krum" / "multikrum", "norm_diff_clipping", "slsgd" and "cclip".  "robust_learning_rate" and
+"weak_dp" are accepted and, as in FedML, leave the plugin path a plain FedAvg
+(FedMLDefender lists them under none of the three hooks; the GPU version of the
+first, fedml_amd.defense.RobustLearningRateDefense, runs where FedML calls
+FedMLDefender.defend).  The other optional hooks (FHE,
 differential privacy, attacks, other defenses, contribution assessment) are
 outside this build's scope: disabled (FedML's default) they are the identity,
 as in the reference; enabling one raises NotImplementedError instead of
@@ -54,6 +55,8 @@ def _check_flags(args) -> None:
             dfn.slsgd_alpha_check(args.alpha)  # SLSGDDefense.__init__ raises at FedMLDefender.init
         if dt == dfn.DEFENSE_ROBUST_LEARNING_RATE:
             args.robust_threshold  # RobustLearningRateDefense.__init__ reads it at FedMLDefender.init
+        if dt == dfn.DEFENSE_WEAK_DP:
+            args.stddev  # WeakDPDefense.__init__ (weak_dp_defense.py:12-14)
 
 
 def _defense(args):

@@ -231,3 +231,21 @@ def test_oracle_robust_learning_rate_signs():
     assert out[0] == avg[0] and out[2] == avg[2]  # |3| >= 2
     assert out[1] == -avg[1]  # |1 - 1 + 1| = 1 < 2
     assert out[3] == 0.0 and np.isnan(out[4])
+
+
+def test_plugin_identity_defenses_read_their_config():
+    """robust_learning_rate / weak_dp are accepted on the plugin path (FedML
+    builds them but hooks neither); a missing config value raises at
+    construction, as FedMLDefender.init does through their __init__."""
+    from types import SimpleNamespace
+
+    from fedml_amd.server_aggregator import _check_flags
+
+    _check_flags(SimpleNamespace(enable_defense=True, defense_type="robust_learning_rate", robust_threshold=4))
+    _check_flags(SimpleNamespace(enable_defense=True, defense_type="weak_dp", stddev=0.1))
+    with pytest.raises(AttributeError):
+        _check_flags(SimpleNamespace(enable_defense=True, defense_type="robust_learning_rate"))
+    with pytest.raises(AttributeError):
+        _check_flags(SimpleNamespace(enable_defense=True, defense_type="weak_dp"))
+    with pytest.raises(NotImplementedError):
+        _check_flags(SimpleNamespace(enable_defense=True, defense_type="foolsgold"))
