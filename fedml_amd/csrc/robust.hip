@@ -598,7 +598,10 @@ extern "C" {
 int64_t fedagg_robust_work_len(int32_t kind, int32_t K, int64_t n_chunks) {
   if (K < 1 || n_chunks < 0) return -1;
   if (n_chunks == 0) return 0;
-  if (kind == FEDAGG_WORK_DIST2) return int64_t(K) * grid_groups(2, n_chunks, 0, 0);
+  // dist2: 1,024 blocks, the kernel's residency (4 waves per SIMD): every
+  // block streams its column ranges from start to end with no second round
+  // of blocks (2,048: 2.31 ms at config 3, 1,024: 2.22 ms)
+  if (kind == FEDAGG_WORK_DIST2) return int64_t(K) * grid_groups(4, n_chunks, 0, 0);
   if (kind == FEDAGG_WORK_PAIRDIST2) {
     if (K <= kTriMax) return int64_t(16) * tri_blocks(K) * grid_groups(4, n_chunks, 0, 0);
     const int NT = pair_tiles(K);
@@ -618,7 +621,7 @@ int fedagg_dist2_f32(const float* const* d_src, int32_t K, const float* d_ref, c
     return FEDAGG_OK;
   }
   if (work_len < K) return rset(FEDAGG_EINVAL, "fedagg_dist2_f32: workspace smaller than K doubles");
-  const int G = grid_groups(2, n_chunks, work_len, K);
+  const int G = grid_groups(4, n_chunks, work_len, K);
   hipLaunchKernelGGL(dist2_kernel, dim3(unsigned(G)), dim3(kBS), 0, st, d_src, K, d_ref, d_chunks, n_chunks, G,
                      d_work);
   hipLaunchKernelGGL(sum_rows_kernel, dim3(unsigned((K + 255) / 256)), dim3(256), 0, st, d_work, K, G, d_out);
