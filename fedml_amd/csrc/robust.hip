@@ -223,11 +223,9 @@ __device__ __forceinline__ void stage_store(f32x4* __restrict__ s, const f32x4 (
 }
 
 // one column of the thread's 4 x 4 pair block: acc[2k + h] holds pairs
-// (4ti + k, 4tj + 2h) and (4ti + k, 4tj + 2h + 1)
-__device__ __forceinline__ void pair_column(const f32x4* __restrict__ sA, const f32x4* __restrict__ sJ, int col,
-                                            int ti, int tj, f32x2 (&acc)[8]) {
-  const f32x4 a = sA[swz(col, ti) >> 2];
-  const f32x4 b = sJ[swz(col, tj) >> 2];
+// (4ti + k, 4tj + 2h) and (4ti + k, 4tj + 2h + 1); a = the column's values of
+// clients 4ti.., b = of clients 4tj..
+__device__ __forceinline__ void pair_ab(f32x4 a, f32x4 b, f32x2 (&acc)[8]) {
   const f32x2 b01 = {b[0], b[1]}, b23 = {b[2], b[3]};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -235,6 +233,28 @@ __device__ __forceinline__ void pair_column(const f32x4* __restrict__ sA, const 
     const f32x2 d0 = ak - b01, d1 = ak - b23;  // v_pk_add_f32 (neg, op_sel broadcast)
     acc[2 * k] = __builtin_elementwise_fma(d0, d0, acc[2 * k]);  // v_pk_fma_f32
     acc[2 * k + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * k + 1]);
+  }
+}
+
+// The columns [0, w) of a stage; pa / pb point at column 0 of the thread's
+// two 4-client groups, RS = row stride in f32x4.  A full stage reads column
+// c + 1 before column c computes (the last prefetch reads a pad row past the
+// stage), so a wave does not wait a whole LDS round trip in front of every
+// column: SQ_WAIT_ANY was 52 % of the triangle kernel's wave cycles.
+template <int RS>
+__device__ __forceinline__ void pair_stage(const f32x4* pa, const f32x4* pb, int w, f32x2 (&acc)[8]) {
+  if (w == kStage) {
+    f32x4 an = pa[0], bn = pb[0];
+#pragma unroll 8
+    for (int col = 0; col < kStage; ++col) {
+      const f32x4 a = an, b = bn;
+      an = pa[(col + 1) * RS];
+      bn = pb[(col + 1) * RS];
+      __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from sinking the prefetch to its use
+      pair_ab(a, b, acc);
+    }
+  } else {
+    for (int col = 0; col < w; ++col) pair_ab(pa[col * RS], pb[col * RS], acc);
   }
 }
 
@@ -251,8 +271,8 @@ __device__ __forceinline__ int2 tile_of(int tp, int T) {
 __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __restrict__ src, int K,
                                                        const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
                                                        double* __restrict__ partial) {
-  __shared__ f32x4 sA[kStage * kRowF / 4];
-  __shared__ f32x4 sB[kStage * kRowF / 4];
+  __shared__ f32x4 sA[(kStage + 1) * kRowF / 4];  // + the pad row pair_stage's last prefetch reads
+  __shared__ f32x4 sB[(kStage + 1) * kRowF / 4];
   const int tp = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
   const int2 tile = tile_of(tp, (K + kPT - 1) / kPT);
   const int I = tile.x * kPT, J = tile.y * kPT;
@@ -296,12 +316,7 @@ __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __res
     f32x2 acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
-    if (w == kStage) {  // full stage: unrolled so the LDS reads of 8 columns are in flight together
-#pragma unroll 8
-      for (int col = 0; col < kStage; ++col) pair_column(sA, sJ, col, ti, tj, acc);
-    } else {
-      for (int col = 0; col < w; ++col) pair_column(sA, sJ, col, ti, tj, acc);
-    }
+    pair_stage<kRowF / 4>(sA + (swz(0, ti) >> 2), sJ + (swz(0, tj) >> 2), w, acc);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       acc64[2 * k] += double(acc[k][0]);
@@ -394,7 +409,7 @@ __device__ __forceinline__ int2 tri_block(int t, int nb) {
 __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __restrict__ src, int K,
                                                         const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
                                                         double* __restrict__ partial) {
-  __shared__ f32x4 sX[kStage * kTriRowF / 4];
+  __shared__ f32x4 sX[(kStage + 1) * kTriRowF / 4];  // + a pad row the last column's prefetch reads
   const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6), W = blockDim.x >> 6;
   const int nb = (K + 3) >> 2, nblk = nb * (nb + 1) / 2;
@@ -453,24 +468,7 @@ __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __r
       f32x2 acc[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
-      auto column = [&](int col) {
-        const f32x4 a = sX[tri_swz(col, blk.x) >> 2];
-        const f32x4 b = sX[tri_swz(col, blk.y) >> 2];
-        const f32x2 b01 = {b[0], b[1]}, b23 = {b[2], b[3]};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const f32x2 ak = {a[k], a[k]};
-          const f32x2 d0 = ak - b01, d1 = ak - b23;
-          acc[2 * k] = __builtin_elementwise_fma(d0, d0, acc[2 * k]);
-          acc[2 * k + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * k + 1]);
-        }
-      };
-      if (w == kStage) {
-#pragma unroll 8
-        for (int col = 0; col < kStage; ++col) column(col);
-      } else {
-        for (int col = 0; col < w; ++col) column(col);
-      }
+      pair_stage<kTriRowF / 4>(sX + (tri_swz(0, blk.x) >> 2), sX + (tri_swz(0, blk.y) >> 2), w, acc);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         acc64[2 * k] += double(acc[k][0]);
