@@ -71,7 +71,9 @@ def parse():
     ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa", "krum", "dist2", "clip",
                                                        "rlr"],
                     help="1 GPU: the reduction measured (median = the wise_median defense kernel; secagg = "
-                         "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction)")
+                         "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction; "
+                         "krum / dist2 / clip = the distance defenses' kernels; rlr = the robust-learning-rate "
+                         "defense's fused pass)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
     ap.add_argument("--clients", type=int, default=None,
