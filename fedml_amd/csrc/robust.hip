@@ -381,8 +381,14 @@ constexpr int kTriMax = 128;   // clients the triangle kernel holds
 constexpr int kTriBS = 576;    // 9 waves: 528 blocks at K = 128
 constexpr int kTriLoads = 6;   // 4-client groups a wave stages per stage
 
-constexpr int kTriRowF = kTriMax + 4;  // padded as the tiles' rows
-__device__ __forceinline__ int tri_swz(int c, int grp) { return c * kTriRowF + (grp << 2); }
+// rows of NB 4-client groups padded by one group (an odd number of 16-byte
+// slots: conflict-free staging writes, as the tiles' rows); the kernel is
+// instantiated for NB = 16 (K <= 64) and 32 (K <= 128) so its two stage
+// buffers take 35 / 69 KB of LDS
+template <int NB>
+constexpr int tri_row_f() { return 4 * (NB + 1); }
+template <int NB>
+__device__ __forceinline__ int tri_swz(int c, int grp) { return c * tri_row_f<NB>() + (grp << 2); }
 
 __host__ __device__ inline int tri_blocks(int K) {
   const int nb = (K + 3) / 4;
@@ -406,10 +412,13 @@ __device__ __forceinline__ int2 tri_block(int t, int nb) {
   return int2{bi, bi + t};
 }
 
+template <int NBMAX>
 __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __restrict__ src, int K,
                                                         const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
                                                         double* __restrict__ partial) {
-  __shared__ f32x4 sX[(kStage + 1) * kTriRowF / 4];  // + a pad row the last column's prefetch reads
+  // two stage buffers (one barrier per stage), each with the pad row
+  // pair_stage's last prefetch reads
+  __shared__ f32x4 sX[2][(kStage + 1) * tri_row_f<NBMAX>() / 4];
   const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6), W = blockDim.x >> 6;
   const int nb = (K + 3) >> 2, nblk = nb * (nb + 1) / 2;
@@ -455,25 +464,39 @@ __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __r
     }
     return true;
   };
-  bool have = fetch();
-  while (have) {
-    const int w = w_next;
-    __syncthreads();  // the previous stage's LDS reads are done
+  auto stage_to = [&](f32x4* buf) {  // the staged registers -> a stage buffer
 #pragma unroll
     for (int q = 0; q < kTriLoads; ++q)
-      if (wave + W * q < nb) sX[tri_swz(lane, wave + W * q) >> 2] = v[q];
-    have = fetch();  // next stage's loads in flight during this stage's compute
+      if (wave + W * q < nb) buf[tri_swz<NBMAX>(lane, wave + W * q) >> 2] = v[q];
+  };
+  // Stage s computes from buffer s & 1 while stage s + 1 is written into the
+  // other one and stage s + 2's loads are in flight: one barrier per stage.
+  // A buffer is rewritten only after the barrier that ends its readers' stage.
+  bool have = fetch();
+  if (have) {
+    int w = w_next;
+    stage_to(sX[0]);
+    have = fetch();
     __syncthreads();
-    if (active) {
-      f32x2 acc[8];
+    for (int buf = 0;; buf ^= 1) {
+      if (active) {
+        f32x2 acc[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
-      pair_stage<kTriRowF / 4>(sX + (tri_swz(0, blk.x) >> 2), sX + (tri_swz(0, blk.y) >> 2), w, acc);
+        for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
+        pair_stage<tri_row_f<NBMAX>() / 4>(sX[buf] + (tri_swz<NBMAX>(0, blk.x) >> 2),
+                                           sX[buf] + (tri_swz<NBMAX>(0, blk.y) >> 2), w, acc);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        acc64[2 * k] += double(acc[k][0]);
-        acc64[2 * k + 1] += double(acc[k][1]);
+        for (int k = 0; k < 8; ++k) {
+          acc64[2 * k] += double(acc[k][0]);
+          acc64[2 * k + 1] += double(acc[k][1]);
+        }
       }
+      if (!have) break;
+      const int wn = w_next;
+      stage_to(sX[buf ^ 1]);
+      have = fetch();
+      __syncthreads();
+      w = wn;
     }
   }
   if (active) {
@@ -640,8 +663,12 @@ int fedagg_pairdist2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     const int64_t per = int64_t(16) * tri_blocks(K);
     if (work_len < per) return rset(FEDAGG_EINVAL, "fedagg_pairdist2_f32: workspace too small (fedagg_robust_work_len)");
     const int G = grid_groups(4, n_chunks, work_len, per);
-    hipLaunchKernelGGL(pairtri_kernel, dim3(unsigned(G)), dim3(unsigned(tri_threads(K))), 0, st, d_src, K, d_chunks,
-                       n_chunks, G, d_work);
+    if (K <= 64)
+      hipLaunchKernelGGL(pairtri_kernel<16>, dim3(unsigned(G)), dim3(unsigned(tri_threads(K))), 0, st, d_src, K,
+                         d_chunks, n_chunks, G, d_work);
+    else
+      hipLaunchKernelGGL(pairtri_kernel<32>, dim3(unsigned(G)), dim3(unsigned(tri_threads(K))), 0, st, d_src, K,
+                         d_chunks, n_chunks, G, d_work);
     hipLaunchKernelGGL(tri_finish_kernel, dim3(unsigned((per + 63) / 64)), dim3(256), 0, st, d_work, G, K, d_out);
     return rcheck("fedagg_pairdist2_f32");
   }
