@@ -157,9 +157,10 @@ def median_kernel_name(K: int, dt) -> str:
     if K <= 128:
         kmax = next(m for m in ((32, 64, 96, 128) if packed else (8, 16, 24, 32, 48, 64, 96, 128)) if K <= m)
         return f"median_{'pk16_' if packed else ''}kernel<{kmax}> ({name})"
-    if K > 2048:
+    if K > 4096 or (not packed and 2048 < K <= 2560):
         return f"median_radix_stream_kernel ({name})"
-    p, r = (4, 64) if K <= 256 else (4, 128) if K <= 512 else (8, 128) if K <= 1024 else (16, 128)
+    p, r = (4, 64) if K <= 256 else (4, 128) if K <= 512 else (8, 128) if K <= 1024 else \
+        (16, 128) if K <= 2048 else (32, 128)
     return f"median_{'pk16_' if packed else ''}lanes_kernel<{p}, {r}> ({name})"
 
 

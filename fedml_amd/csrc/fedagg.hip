@@ -1411,7 +1411,7 @@ int launch_median_pk16(const uint16_t* const* src, int K, int64_t N, uint16_t* o
 // More than 128 clients, in registers: P adjacent lanes share one column,
 // each holding R of its KMAX = P·R (±inf-padded) values, slot s = sub·R + j =
 // client s (shipped: P = 4, R = 64 up to 256 clients, then R = 128 with P = 4,
-// 8 or 16, i.e. up to 2048 clients).  Every lane sorts its R values with the pairwise network (all outputs
+// 8, 16 or 32, i.e. up to 4096 clients).  Every lane sorts its R values with the pairwise network (all outputs
 // used, so nothing is pruned); the sorted runs are then merged across lanes as
 // in a bitonic merge sort:
 //   - "reverse pairing" of two sorted runs A, B of length L held by lane
@@ -1439,6 +1439,18 @@ constexpr int dpp_xor_ctrl() {
   return M == 1 ? 0xB1 : M == 2 ? 0x4E : M == 3 ? 0x1B : M == 7 ? 0x141 : 0x140;
 }
 
+// The value of lane ^ M: one DPP mov where a pattern exists (xor 1, 2, 3,
+// 7, 15), two for xor 4 (xor 7 then xor 3), else ds_bpermute (xor 31: the
+// last level of the 32-lane groups above 2,048 clients).
+template <int M>
+constexpr bool dpp_xor_ok() { return M == 1 || M == 2 || M == 3 || M == 7 || M == 15; }
+template <int M>
+__device__ __forceinline__ float xor_mov(float x) {
+  if constexpr (dpp_xor_ok<M>()) return dpp_mov<dpp_xor_ctrl<M>()>(x);
+  else if constexpr (M == 4) return dpp_mov<dpp_xor_ctrl<3>()>(dpp_mov<dpp_xor_ctrl<7>()>(x));  // (i ^ 7) ^ 3
+  else return __int_as_float(__shfl_xor(__float_as_int(x), M, 64));
+}
+
 // min (lower lanes, sel = -inf) or max (upper lanes, sel = +inf) of own
 // register i and the partner lane's register R-1-i, for every i
 template <int M, int R>
@@ -1448,8 +1460,8 @@ __device__ __forceinline__ void lanes_reverse_pair(float (&v)[R], float sel) {
   asm volatile("" : "+v"(sel));
 #pragma unroll
   for (int i = 0; i < R / 2; ++i) {
-    const float a = dpp_mov<dpp_xor_ctrl<M>()>(v[R - 1 - i]);
-    const float b = dpp_mov<dpp_xor_ctrl<M>()>(v[i]);
+    const float a = xor_mov<M>(v[R - 1 - i]);
+    const float b = xor_mov<M>(v[i]);
     v[i] = __builtin_amdgcn_fmed3f(v[i], a, sel);
     v[R - 1 - i] = __builtin_amdgcn_fmed3f(v[R - 1 - i], b, sel);
   }
@@ -1461,7 +1473,7 @@ __device__ __forceinline__ void lanes_cross_stage(float (&v)[R], int sub) {
   float sel = (sub & M) ? __builtin_huge_valf() : -__builtin_huge_valf();
   asm volatile("" : "+v"(sel));
 #pragma unroll
-  for (int i = 0; i < R; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], dpp_mov<dpp_xor_ctrl<M>()>(v[i]), sel);
+  for (int i = 0; i < R; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], xor_mov<M>(v[i]), sel);
 }
 
 // in-lane half-cleaner cascade: a bitonic register array -> ascending
@@ -1480,9 +1492,10 @@ __device__ __forceinline__ void lane_bitonic_merge(float (&v)[R]) {
 template <int G, int P, int R>
 __device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
   if constexpr (G < P) {
-    static_assert(G <= 8, "a level of 16 lanes would need an xor-4 stage");
+    static_assert(G <= 16, "lane groups of at most 32");
     lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) ? __builtin_huge_valf() : -__builtin_huge_valf());
-    if constexpr (G == 8) lanes_cross_stage<2>(v, sub);  // slot distance 2R
+    if constexpr (G == 16) lanes_cross_stage<4>(v, sub);  // slot distance 4R
+    if constexpr (G >= 8) lanes_cross_stage<2>(v, sub);  // slot distance 2R
     if constexpr (G >= 4) lanes_cross_stage<1>(v, sub);  // slot distance R
     lane_bitonic_merge(v);
     lanes_merge_levels<G * 2, P, R>(v, sub);
@@ -1493,7 +1506,7 @@ template <int P, int R, bool FULL, class E = MedF32, int BS = 256>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
     const typename E::S* const* __restrict__ src, int K, int64_t N, typename E::S* __restrict__ out) {
   using S = typename E::S;
-  static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2, 4, 8 or 16 lanes per column");
+  static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column");
   static_assert(R == 64 || R == 128, "64 or 128 values per lane");
   constexpr int KMAX = P * R, PAD = 2;
   // Row pointer of every slot, skewed by PAD entries per lane group so the P
@@ -1574,6 +1587,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   if constexpr (P >= 4) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
   if constexpr (P >= 8) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
   if constexpr (P >= 16) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima across the two quads
+  if constexpr (P >= 32) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<15>()>(m));  // the two 8-lane halves of a row
   if (sub == 0 && e < N) out[e] = nan_slot < KMAX ? nan_raw : E::narrow(m);
 }
 
@@ -1605,6 +1619,12 @@ template <int CTRL>
 __device__ __forceinline__ short2_t dpp_mov(short2_t x) {
   return __builtin_bit_cast(short2_t, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
+template <int M>
+__device__ __forceinline__ short2_t xor_mov(short2_t x) {
+  if constexpr (dpp_xor_ok<M>()) return dpp_mov<dpp_xor_ctrl<M>()>(x);
+  else if constexpr (M == 4) return dpp_mov<dpp_xor_ctrl<3>()>(dpp_mov<dpp_xor_ctrl<7>()>(x));
+  else return __builtin_bit_cast(short2_t, __shfl_xor(__builtin_bit_cast(int, x), M, 64));
+}
 __device__ __forceinline__ short2_t pk_pick(short2_t a, short2_t b, bool up) {
   const short2_t lo = __builtin_elementwise_min(a, b), hi = __builtin_elementwise_max(a, b);
   return up ? hi : lo;
@@ -1613,8 +1633,8 @@ template <int M, int R>
 __device__ __forceinline__ void pk_lanes_reverse_pair(short2_t (&v)[R], bool up) {
 #pragma unroll
   for (int i = 0; i < R / 2; ++i) {
-    const short2_t a = dpp_mov<dpp_xor_ctrl<M>()>(v[R - 1 - i]);
-    const short2_t b = dpp_mov<dpp_xor_ctrl<M>()>(v[i]);
+    const short2_t a = xor_mov<M>(v[R - 1 - i]);
+    const short2_t b = xor_mov<M>(v[i]);
     v[i] = pk_pick(v[i], a, up);
     v[R - 1 - i] = pk_pick(v[R - 1 - i], b, up);
   }
@@ -1623,7 +1643,7 @@ template <int M, int R>
 __device__ __forceinline__ void pk_lanes_cross_stage(short2_t (&v)[R], int sub) {
   const bool up = (sub & M) != 0;
 #pragma unroll
-  for (int i = 0; i < R; ++i) v[i] = pk_pick(v[i], dpp_mov<dpp_xor_ctrl<M>()>(v[i]), up);
+  for (int i = 0; i < R; ++i) v[i] = pk_pick(v[i], xor_mov<M>(v[i]), up);
 }
 template <int R>
 __device__ __forceinline__ void pk_lane_bitonic_merge(short2_t (&v)[R]) {
@@ -1637,9 +1657,10 @@ __device__ __forceinline__ void pk_lane_bitonic_merge(short2_t (&v)[R]) {
 template <int G, int P, int R>
 __device__ __forceinline__ void pk_lanes_merge_levels(short2_t (&v)[R], int sub) {
   if constexpr (G < P) {
-    static_assert(G <= 8, "a level of 16 lanes would need an xor-4 stage");
+    static_assert(G <= 16, "lane groups of at most 32");
     pk_lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) != 0);
-    if constexpr (G == 8) pk_lanes_cross_stage<2>(v, sub);
+    if constexpr (G == 16) pk_lanes_cross_stage<4>(v, sub);
+    if constexpr (G >= 8) pk_lanes_cross_stage<2>(v, sub);
     if constexpr (G >= 4) pk_lanes_cross_stage<1>(v, sub);
     pk_lane_bitonic_merge(v);
     pk_lanes_merge_levels<G * 2, P, R>(v, sub);
@@ -1653,7 +1674,7 @@ __device__ uint32_t g_median_pad2[2] = {E::kNegInf * 0x10001u, E::kPosInf * 0x10
 template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
     const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out) {
-  static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2, 4, 8 or 16 lanes per column pair");
+  static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column pair");
   static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
   constexpr int KMAX = P * R, PAD = 2;
   __shared__ const uint16_t* rows[KMAX + PAD * P];
@@ -1725,6 +1746,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   if constexpr (P >= 4) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
   if constexpr (P >= 8) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
   if constexpr (P >= 16) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima
+  if constexpr (P >= 32) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<15>()>(m));  // row halves
   uint32_t bits = pk16_bits(m);
   if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
   if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
@@ -2153,17 +2175,22 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
                     hipStream_t st) {
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
     if constexpr (sizeof(typename E::S) == 2) {
-      if (aligned && K <= 2048) {  // two columns per lane on packed int16 keys
+      if (aligned && K <= 4096) {  // two columns per lane on packed int16 keys
         if (K <= 256) return launch_median_pk16_lanes<4, 64, E>(d_src, K, N, d_out, st);
         if (K <= 512) return launch_median_pk16_lanes<4, 128, E>(d_src, K, N, d_out, st);
         if (K <= 1024) return launch_median_pk16_lanes<8, 128, E>(d_src, K, N, d_out, st);
-        return launch_median_pk16_lanes<16, 128, E>(d_src, K, N, d_out, st);
+        if (K <= 2048) return launch_median_pk16_lanes<16, 128, E>(d_src, K, N, d_out, st);
+        return launch_median_pk16_lanes<32, 128, E>(d_src, K, N, d_out, st);
       }
     }
     if (K <= 256) return launch_median_lanes<4, 64, E>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
     if (K <= 512) return launch_median_lanes<4, 128, E>(d_src, K, N, d_out, st);
     if (K <= 1024) return launch_median_lanes<8, 128, E>(d_src, K, N, d_out, st);
     if (K <= 2048) return launch_median_lanes<16, 128, E>(d_src, K, N, d_out, st);
+    // 32 lanes per column pay off against the radix select only well inside
+    // their range (1M columns: 18.9 vs 18.7 ms at K = 2,049, 22.9 vs 35.4 ms
+    // at 4,096 in fp32; the packed 16-bit kernels win at every K, above)
+    if (K > 2560 && K <= 4096) return launch_median_lanes<32, 128, E>(d_src, K, N, d_out, st);
     return launch_median_radix_stream<E>(d_src, K, N, d_out, st);  // no bound on K
   }
   if constexpr (sizeof(typename E::S) == 2) {

@@ -234,8 +234,8 @@ int fedagg_wsum_fedopt_rmsprop_f32(const float* const* d_src, const float* d_w,
  * element (K-1)/2) of {src_i[e]}; if the column holds a NaN, the first NaN in
  * client order.  Any K >= 1 and N (K <= 128: one lane per element, a pruned
  * sorting network in registers, launched in chunks of 2^30 columns;
- * 128 < K <= 2048: 4, 8 or 16 lanes per element, each sorting 64 or 128
- * values in registers, merged across lanes; K > 2048: an 8-bit MSD radix
+ * 128 < K <= 4096: 4 to 32 lanes per element, each sorting 64 or 128
+ * values in registers, merged across lanes; otherwise an 8-bit MSD radix
  * select per column over LDS histograms, the column re-read per digit).  Where +0.0 and
  * -0.0 tie at the median the sign of the zero returned may differ from
  * torch's (nth_element order). */
@@ -247,7 +247,7 @@ int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N,
  * (torch.cat keeps the 16-bit dtype).  Values are widened to fp32 exactly,
  * selected, and the selected input narrowed back exactly; a NaN column
  * returns a NaN.  With FEDAGG_ALIGNED16 (4-byte aligned rows and output)
- * 16-bit rows up to K = 2048 take the packed kernels instead: two columns per
+ * 16-bit rows up to K = 4096 take the packed kernels instead: two columns per
  * register as order-preserving int16 keys, the same networks on
  * v_pk_min_i16 / v_pk_max_i16. */
 int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K,

@@ -115,11 +115,12 @@ def test_median_lanes_large_sampled(cuda_device):
 
 @pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K", [1025, 1500, 2048, 2049, 4097])
+@pytest.mark.parametrize("K", [1025, 1500, 2048, 2049, 2561, 3000, 4096, 4097])
 def test_median_more_than_1024_clients(aligned, dtype, K, cuda_device):
     """No client bound, as torch.median has none (coordinate_wise_median_
-    defense.py:24-32): up to 2048 clients the 16-lane group kernels (packed for
-    aligned 16-bit rows), above that the radix-select kernel; every dtype,
+    defense.py:24-32): up to 4096 clients the 16- and 32-lane group kernels
+    (packed for aligned 16-bit rows; widening rows take the radix select
+    between 2049 and 2560), above that the radix-select kernel; every dtype,
     with duplicates, infinities, NaN columns (first NaN in client order) and
     -0.0, a ragged last tile and an odd column count."""
     N = 1_037
@@ -200,9 +201,9 @@ def test_median_16bit_rows_vs_oracle(aligned, dtype, K, cuda_device):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K,N", [(256, 1_000), (512, 999), (700, 65), (1024, 1), (2048, 77)])
+@pytest.mark.parametrize("K,N", [(256, 1_000), (512, 999), (700, 65), (1024, 1), (2048, 77), (4096, 33)])
 def test_median_16bit_lanes_first_nan_payload(dtype, K, N, cuda_device):
-    """The packed lane-group kernel (16-bit rows, 128 < K <= 2048): a NaN
+    """The packed lane-group kernel (16-bit rows, 128 < K <= 4096): a NaN
     column returns ITS FIRST NaN in client order, payload included, per half of
     a packed pair, when the NaNs sit in different lanes of the column group;
     an odd N takes the lone-last-column launch (N = 1: that launch alone)."""

@@ -30,6 +30,7 @@ SHAPES = [
     (torch.float32, 129, 4_000_037), (torch.float32, 256, 4_000_037), (torch.float32, 512, 4_000_037),
     (torch.float32, 1024, 4_000_037), (torch.bfloat16, 512, 4_000_037),
     (torch.float32, 1025, 1_000_003), (torch.float32, 2048, 1_000_003), (torch.float32, 2049, 1_000_003),
+    (torch.float32, 4096, 1_000_003), (torch.float32, 4097, 1_000_003),
 ]
 
 
@@ -71,7 +72,7 @@ def main():
     shapes = [(dt, K, N, False) for dt, K, N in SHAPES]
     if "--sixteen" in sys.argv:  # 16-bit rows above 128 clients (packed lane-group kernel), config 4's K = 512
         shapes = [(torch.bfloat16, K, 4_000_037, False) for K in (129, 256, 384, 512, 700, 1024)]
-        shapes += [(torch.bfloat16, K, 1_000_003, False) for K in (1025, 2048)]
+        shapes += [(torch.bfloat16, K, 1_000_003, False) for K in (1025, 2048, 4096)]
         shapes += [(torch.float16, 512, 4_000_037, False), (torch.bfloat16, 512, 86_567_656, False)]
     if "--one-row" in sys.argv:
         shapes += [(torch.float32, 128, 25_610_152, True), (torch.float32, 512, 4_000_037, True),
