@@ -249,3 +249,20 @@ def test_plugin_identity_defenses_read_their_config():
         _check_flags(SimpleNamespace(enable_defense=True, defense_type="weak_dp"))
     with pytest.raises(NotImplementedError):
         _check_flags(SimpleNamespace(enable_defense=True, defense_type="foolsgold"))
+
+
+def test_robust_learning_rate_host_checks_before_device_work():
+    """The reference's behaviour that needs no GPU: threshold 0 hands the list
+    to the base function untouched; Σn = 0 raises ZeroDivisionError (at the
+    first weight, as `local_sample_number / total_sample_num` does); a bf16
+    model is refused by name rather than aggregated another way."""
+    raw = [(3, OrderedDict(w=torch.ones(4))), (5, OrderedDict(w=torch.zeros(4)))]
+    seen = []
+    assert dfn.robust_learning_rate(raw, 0, lambda lst: seen.append(lst) or "base") == "base"
+    assert seen == [raw]
+    with pytest.raises(ZeroDivisionError):
+        dfn.robust_learning_rate([(0, OrderedDict(w=torch.ones(2))), (0, OrderedDict(w=torch.ones(2)))], 1)
+    with pytest.raises(NotImplementedError):
+        dfn.robust_learning_rate([(1, OrderedDict(w=torch.ones(2, dtype=torch.bfloat16)))], 1)
+    d = dfn.RobustLearningRateDefense(type("A", (), {"robust_threshold": 0})())
+    assert d.run(raw, lambda lst: "base") == "base" and d.get_malicious_client_idxs() == []
