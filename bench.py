@@ -2,21 +2,35 @@
 """Headline benchmark: device-resident FedAvg aggregation on MI355X.
 
 One step = one server aggregation round over client updates already resident
-in HBM: host computes the weights w_i = n_i/Σn, uploads them, and the
-weighted-sum kernels reduce every client row (one launch per dtype group;
-with --gpus > 1 also the RCCL reduce-scatter of the client-axis mode).
+in HBM: host computes the weights w_i = n_i/Σn, and the weighted-sum kernels
+reduce every client row (one launch per dtype group).
 
 Default workload = BASELINE.json config 3: 128 clients x ResNet-50 state dict
 (25,610,152 fp32 + 53 int64 elements per client), synthetic data generated
-in HBM.  With --gpus N each rank holds its own 128 clients (weak scaling).
+in HBM.
+
+With --gpus N (one process per GPU) the round keeps the config's client
+count (strong scaling, ``--clients-total``, default the config's K):
+
+  --mode param (default)  every rank holds ITS KEYS of every client (whole
+                          keys dealt to ranks by bytes, the same partition as
+                          the in-process fedml_amd.multidev bucket) and
+                          reduces them in the reference order: no exchange,
+                          bit-exact with one GPU.
+  --mode client           every rank holds its K/N clients' whole updates,
+                          computes an fp32 partial and joins one chunked RCCL
+                          reduce-scatter (timed separately on the comm stream).
+  --weak                  round 2's weak scaling: every rank gets the
+                          config's K clients of its own.
 
     python bench.py                       # 1 GPU, default steps
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8
 
-Prints ONE JSON line on rank 0 (contract in the task statement); the
+Prints ONE JSON line on rank 0 (contract in the task statement); at N = 1 the
 cpu_baseline leg times the reference's own CPU loop (oracle/cpu_baseline.py)
-on a bounded sample of the same workload.
+over the FULL workload (every key, every client) at the job's CPU quota and
+at one thread.
 """
 from __future__ import annotations
 
@@ -34,7 +48,9 @@ sys.path.insert(0, ROOT)
 
 from fedml_amd import shapes  # noqa: E402
 from fedml_amd.bucket import ClientBucket  # noqa: E402
-from fedml_amd.sharded import ClientAxisAggregator, ParamAxisAggregator  # noqa: E402
+from fedml_amd import multidev  # noqa: E402
+from fedml_amd.layout import RowLayout  # noqa: E402
+from fedml_amd.sharded import ClientAxisAggregator  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -59,8 +75,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
-    ap.add_argument("--mode", default="client", choices=["client", "param"],
-                    help="multi-GPU partitioning (ignored at 1 GPU)")
+    ap.add_argument("--mode", default="param", choices=["client", "param"],
+                    help="multi-GPU partitioning (ignored at 1 GPU): param = whole keys per rank, no exchange; "
+                         "client = clients per rank + RCCL reduce-scatter")
+    ap.add_argument("--clients-total", type=int, default=None,
+                    help="multi-GPU: clients of the round over all ranks (default: the config's K)")
+    ap.add_argument("--weak", action="store_true",
+                    help="multi-GPU: every rank aggregates the config's K clients of its own (weak scaling)")
     ap.add_argument("--chunks", type=int, default=8, help="client mode: reduce-scatter pipeline depth")
     ap.add_argument("--acc", default="reference", choices=["reference", "fp32"],
                     help="bf16/f16 accumulation: torch's per-op chain (bit-exact) or fp32")
@@ -142,6 +163,8 @@ def cpu_baseline(bucket, ns, reps: int) -> dict:
                       f"median of {reps} after 1 warm-up: {full['median_s'] * 1e3:.1f} ms/aggregation at "
                       f"{full['threads']} threads, {one['median_s'] * 1e3:.1f} ms at 1 thread",
             "threads": full["threads"],
+            "cores_basis": "threads used = the CPUs this job may use (the box's cgroup quota), not the host's "
+                           "nproc; see host",
             "ms_per_aggregation": round(full["median_s"] * 1e3, 2),
             "single_thread": {"value": K * n_elems / one["median_s"], "threads": 1,
                               "ms_per_aggregation": round(one["median_s"] * 1e3, 2)},
@@ -194,19 +217,50 @@ def main():
 
     cfg = CONFIGS[a.config]
     entries = shapes.MODELS[cfg["model"]]()
+    full_layout = RowLayout(entries)
+    n_elems = sum(sum(g.numels) for g in full_layout.groups.values())  # per client, the whole model
     K = cfg["K"]
     if a.clients is not None:
         if world > 1 or a.clients < 1:
             raise SystemExit("--clients is a 1-GPU override (>= 1)")
         K = a.clients
     mode = a.mode if world > 1 else "single"
+    weak = a.weak and world > 1
+    if world > 1 and not weak:
+        K_total = a.clients_total if a.clients_total is not None else cfg["K"]
+        if K_total < 1:
+            raise SystemExit("--clients-total must be >= 1")
+    else:
+        K_total = K * world
+    # this rank's clients: all of them (single / param axis) or its share (client axis)
+    if mode == "client" and not weak:
+        base_k, extra = divmod(K_total, world)
+        K_loc = base_k + (1 if rank < extra else 0)
+        first = rank * base_k + min(rank, extra)
+    elif mode == "client" or weak:
+        K_loc, first = K, rank * K
+    else:
+        K_loc, first = K_total, 0
+    if K_loc < 1:
+        raise SystemExit(f"rank {rank} would hold no clients: --clients-total {K_total} < --gpus {world}")
+    # the keys this rank reduces: all of them, or its whole-key shard (param axis)
+    my_entries = entries
+    if mode == "param":
+        plan = multidev.shard_plan(entries, world)
+        if len(plan) < world:
+            raise SystemExit(f"{a.config} has data in {len(plan)} keys: too few for {world} ranks in --mode param")
+        my_entries = plan[rank]
+
+    from fedml_amd.synth import sample_nums
+    ns_all = sample_nums(K_total, seed=1)
+    ns_local = ns_all[first:first + K_loc]
+    total_n = sum(ns_all)
+    w_local = [n / total_n for n in ns_local]  # global weights of this rank's clients
 
     server = None
     sharded_opt = None
-    if a.fedopt and world > 1:
-        if mode != "client":
-            raise SystemExit("--fedopt over several GPUs shards the client axis (--mode client)")
-        bucket = ClientBucket(entries, K, dev)  # integer buffers promoted into the fp32 row
+    if a.fedopt and mode == "client":
+        bucket = ClientBucket(entries, K_loc, dev)  # integer buffers promoted into the fp32 row
         if set(bucket.groups) != {torch.float32}:
             raise SystemExit("--fedopt over several GPUs takes an fp32 model (integer buffers promoted)")
     elif a.fedopt:
@@ -214,9 +268,10 @@ def main():
 
         from fedml_amd.fedopt import FedOptServer
 
-        init = OrderedDict((k, torch.zeros(s, dtype=d)) for k, s, d in entries)
-        params = shapes.param_names(entries)
-        server = FedOptServer(init, params, K, a.fedopt, 1.0, 0.9, dev)
+        init = OrderedDict((k, torch.zeros(s, dtype=d)) for k, s, d in my_entries)
+        mine = {k for k, _, _ in my_entries}
+        params = [p for p in shapes.param_names(entries) if p in mine]
+        server = FedOptServer(init, params, K_loc, a.fedopt, 1.0, 0.9 if a.fedopt == "sgd" else 0.0, dev)
         bucket = server.bucket
     elif a.op in ("secagg", "lsa"):
         if world > 1:
@@ -225,44 +280,41 @@ def main():
         # transform_tensor_to_finite output), one group
         bucket = ClientBucket([(k, s, torch.int64) for k, s, _ in entries], K, dev, promote_ints=False)
     else:
-        bucket = ClientBucket(entries, K, dev, low_precision_acc=a.acc)
+        bucket = ClientBucket(my_entries, K_loc, dev, low_precision_acc=a.acc)
     for gi, (dt, g) in enumerate(bucket.groups.items()):
         if a.op in ("secagg", "lsa"):
             gen = torch.Generator(device=dev).manual_seed(1000 * rank + gi)
             g.rows.random_(0, LSA_PRIME, generator=gen)
         else:
             fill_rows(g.rows, g.length, seed=1000 * rank + gi, round_idx=3)
-    from fedml_amd.synth import sample_nums
-    ns_all = sample_nums(K * world, seed=1)
-    ns_local = ns_all[rank * K:(rank + 1) * K]
     torch.cuda.synchronize()
 
     groups = list(bucket.groups.items())
     dom_dt = max(groups, key=lambda kv: kv[1].length * kv[1].rows.element_size())[0]
-    n_elems = bucket.num_elements()
+    comm_evs = None  # client axis: (start, end) per chunk on the comm stream
+    xgmi_bytes = 0
 
     # per-step work -------------------------------------------------------------
-    if a.fedopt and world > 1:
+    if a.fedopt and mode == "client":
         from fedml_amd.sharded import ShardedFedOpt, buffer_ranges
 
         gd = bucket.groups[torch.float32]
         init = torch.zeros(gd.length, dtype=torch.float32, device=dev)
-        sharded_opt = ShardedFedOpt(gd.rows, gd.length, init, a.fedopt, 1.0, 0.9, chunks=a.chunks,
-                                    buffers=buffer_ranges(bucket, shapes.param_names(entries)))
-        total = sum(ns_all)
-        w = [n / total for n in ns_all[rank * K:(rank + 1) * K]]
+        sharded_opt = ShardedFedOpt(gd.rows, gd.length, init, a.fedopt, 1.0, 0.9 if a.fedopt == "sgd" else 0.0,
+                                    chunks=a.chunks, buffers=buffer_ranges(bucket, shapes.param_names(entries)))
 
-        def step(ev=None):
-            sharded_opt.aggregate(w, events=ev)
+        def step(ev=None, cev=None):
+            sharded_opt.aggregate(w_local, events=ev, comm_events=cev)
 
         n_launch = len(sharded_opt.agg.bounds)
-        sharded_opt.aggregate(w)  # first step (no state read) before timing
-        dom_bytes = K * gd.length * 4 + gd.length * 4  # rows in, fp32 partial out (the step is 1/G of a pass)
+        sharded_opt.aggregate(w_local)  # first step (no state read) before timing
+        dom_bytes = K_loc * gd.length * 4 + gd.length * 4  # rows in, fp32 partial out (the step is 1/G of a pass)
+        xgmi_bytes = (world - 1) * sharded_opt.agg.piece * len(sharded_opt.agg.bounds) * 4
     elif server is not None:
         for i, n in enumerate(ns_local):
             server.sample_num_dict[i] = n
 
-        def step(ev=None):
+        def step(ev=None, cev=None):
             server.aggregate(events=ev)
 
         n_launch = 1
@@ -271,10 +323,12 @@ def main():
     elif a.op == "median":
         from fedml_amd import defense as dfn
 
+        if world > 1:
+            raise SystemExit("--op median is a 1-GPU measurement")
         gd = bucket.groups[dom_dt]
         med_out = torch.empty(gd.padded, dtype=gd.rows.dtype, device=dev)  # the median is one of the inputs
 
-        def step(ev=None):
+        def step(ev=None, cev=None):
             if ev is not None:
                 ev[0].record()
             dfn.median_rows(gd.d_ptrs, K, gd.length, med_out, aligned=True)
@@ -288,11 +342,13 @@ def main():
         # sum + the lr rule, one pass over the fp32 row (threshold K/4)
         from fedml_amd import kernels as kn
 
+        if world > 1:
+            raise SystemExit("--op rlr is a 1-GPU measurement")
         gd = bucket.groups[torch.float32]
         rlr_out = torch.empty(gd.padded, dtype=torch.float32, device=dev)
         rlr_w = kn.weights_for([n / sum(ns_local) for n in ns_local], torch.float32, dev)
 
-        def step(ev=None):
+        def step(ev=None, cev=None):
             if ev is not None:
                 ev[0].record()
             kn.wsum_rlr_ptrs(gd.d_ptrs, rlr_w, K, gd.length, float(max(1, K // 4)), rlr_out, True)
@@ -340,7 +396,7 @@ def main():
         dom_bytes = {"krum": 3 * K * (K - 1) // 2 * n_weight, "dist2": (K + 1) * n_weight * 4,
                      "clip": (2 * K + 1) * gd.length * 4}[a.op]
 
-        def step(ev=None):
+        def step(ev=None, cev=None):
             if ev is not None:
                 ev[0].record()
             nat.check(call(), a.op)
@@ -365,7 +421,7 @@ def main():
                 sec_out.data_ptr(), nat.FEDAGG_ALIGNED16, nat.stream_handle())
             dom_bytes = (K + 1) * gd.length * 8 + gd.length * 4
 
-        def step(ev=None):
+        def step(ev=None, cev=None):
             if ev is not None:
                 ev[0].record()
             nat.check(call(), a.op)
@@ -373,62 +429,50 @@ def main():
                 ev[1].record()
 
         n_launch = 1
-    elif mode == "single":
+    elif mode in ("single", "param"):
+        # one GPU, or this rank's whole-key shard of every client: the
+        # single-GPU reduction over the bucket, no exchange
         outs = bucket.new_outputs()
-        w = bucket.weights(ns_local)
+        w = w_local if mode == "param" else bucket.weights(ns_local)
 
-        def step(ev=None):
-            bucket.reduce_into(outs, w, events={dom_dt: ev} if ev is not None else None)
+        def step(ev=None, cev=None):
+            bucket.reduce_into(outs, w, events={dom_dt: ev[0]} if ev is not None else None)
 
         n_launch = 1
-        dom_bytes = K * bucket.groups[dom_dt].length * bucket.groups[dom_dt].rows.element_size() + \
-            bucket.groups[dom_dt].length * torch.empty((), dtype=bucket.groups[dom_dt].out_dtype).element_size()
-    elif mode == "client":
-        total = sum(ns_all)
-        w = [n / total for n in ns_all[rank * K:(rank + 1) * K]]
+        gd = bucket.groups[dom_dt]
+        dom_bytes = K_loc * gd.length * gd.rows.element_size() + \
+            gd.length * torch.empty((), dtype=gd.out_dtype).element_size()
+    else:  # client axis: this rank's clients' partial + chunked RCCL reduce-scatter
         aggs = {dt: ClientAxisAggregator(g.rows, g.length, chunks=a.chunks if dt == dom_dt else 1)
                 for dt, g in groups}
 
-        def step(ev=None):
+        def step(ev=None, cev=None):
             for dt, agg in aggs.items():
-                agg.aggregate(w, events=ev if dt == dom_dt else None)
+                agg.aggregate(w_local, events=ev if dt == dom_dt else None,
+                              comm_events=cev if dt == dom_dt else None)
                 if dt in (torch.bfloat16, torch.float16):
                     agg.shard_in_model_dtype()  # the one rounding of a 16-bit model, after the exchange
 
         n_launch = len(aggs[dom_dt].bounds)
         gd = bucket.groups[dom_dt]
-        dom_bytes = K * gd.length * gd.rows.element_size() + gd.length * 4  # rows in, fp32 partial out
-    else:  # param axis: this rank's rows ARE its column shard of every client
-        w = bucket.weights(ns_local)
-        aggs = {dt: ParamAxisAggregator(g.rows, g.length) for dt, g in groups}
+        dom_bytes = K_loc * gd.length * gd.rows.element_size() + gd.length * 4  # rows in, fp32 partial out
+        xgmi_bytes = (world - 1) * aggs[dom_dt].piece * len(aggs[dom_dt].bounds) * 4
 
-        def step(ev=None):
-            for dt, agg in aggs.items():
-                agg.aggregate(w, events=ev if dt == dom_dt else None)
+    def new_events(n):
+        return [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(n)]
 
-        n_launch = 1
-        gd = bucket.groups[dom_dt]
-        dom_bytes = K * gd.length * gd.rows.element_size() + \
-            gd.length * torch.empty((), dtype=gd.out_dtype).element_size()
-
-    def new_events():
-        return [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-                for _ in range(n_launch)]
-
+    timed_comm = mode == "client" and world > 1 and a.backend == "nccl"
     for _ in range(a.warmup):
         step()
-    evs = [new_events() for _ in range(a.steps)]
+    evs = [new_events(n_launch) for _ in range(a.steps)]
+    cevs = [new_events(n_launch) for _ in range(a.steps)] if timed_comm else [None] * a.steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(a.steps):
-        ev = evs[s]
-        if mode == "single":
-            step(ev[0])
-        else:
-            step(ev)
+        step(evs[s], cevs[s])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -437,16 +481,30 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = sum(e0.elapsed_time(e1) for ev in evs for e0, e1 in ev) / a.steps  # per step
+    comm_ms = sum(e0.elapsed_time(e1) for ev in cevs for e0, e1 in ev) / a.steps if timed_comm else None
     achieved = dom_bytes / (kern_ms / 1e3) / 1e9  # GB/s (GFLOP/s for --op krum)
+    hbm_all = dom_bytes / (elapsed / a.steps) / 1e9  # this rank's algorithmic bytes over the step time
     if world > 1:
         t = torch.tensor([achieved], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)  # slowest rank's kernel
         achieved = float(t.item())
+        t = torch.tensor([hbm_all, comm_ms or 0.0], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        hbm_all = float(t[0].item())
+        if comm_ms is not None:
+            comm_ms = float(t[1].item()) / world
 
     ms_per_step = elapsed / a.steps * 1e3
-    value = world * K * n_elems / (elapsed / a.steps)
+    value = K_total * n_elems / (elapsed / a.steps)
     variant = (a.fedopt or ("" if a.op == "fedavg" else a.op)) + (f"@K{K}" if a.clients is not None else "")
     traffic = load_traffic(a.config, mode, world, variant)
+    parallelism = {"single": "1 GPU",
+                   "client": f"client-axis x{world}: {K_total} clients, ~{K_total // world} per GPU, fp32 partial + "
+                             f"RCCL reduce-scatter, {a.chunks}-chunk pipeline",
+                   "param": f"parameter-axis x{world}: every GPU holds its whole keys of all {K_total} clients "
+                            f"(fedml_amd.multidev.shard_plan), no collective, bit-exact"}[mode]
+    if weak:
+        parallelism += f" [weak: {K} clients per GPU]"
     line = {
         "metric": METRIC,
         "value": value,
@@ -456,14 +514,14 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if weak or world == 1 else "strong",
         "vs_baseline": None,
         "dtype": "int64" if a.op in ("secagg", "lsa") else "bf16" if dom_dt == torch.bfloat16 else "f32",
         "data": "synthetic (base~N(0,0.05^2), client=base+0.01*eps, generated in HBM)",
         "config": {
             "workload": cfg["desc"] + (f" [--clients {K}]" if a.clients is not None else ""),
-            "clients_per_gpu": K,
-            "clients_total": K * world,
+            "clients_per_gpu": K_loc,
+            "clients_total": K_total,
             "elements_per_client": n_elems,
             "layout": "ClientBucket rows [K, L] per dtype, 256-B aligned rows",
             "low_precision_acc": a.acc,
@@ -474,9 +532,7 @@ def main():
                             + (" fused" if server is not None else
                                f", on each rank's 1/{world} shard after the reduce-scatter, sharded state")
                             if a.fedopt else None),
-            "parallelism": {"single": "1 GPU", "client": f"client-axis x{world}, RCCL reduce-scatter, "
-                                                         f"{a.chunks}-chunk pipeline",
-                            "param": f"parameter-axis x{world}, no collective"}[mode],
+            "parallelism": parallelism,
         },
         "roofline": {
             "bound": "valu" if a.op == "krum" else "hbm",
@@ -486,7 +542,10 @@ def main():
             "frac": round(achieved / 1e3 / VALU_PEAK_TFLOPS if a.op == "krum" else achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>",
-                        "krum": "pairdist_kernel (packed fp32)", "dist2": "dist2_kernel",
+                        "krum": ("pairtri_kernel<16> + tri_finish_kernel" if K <= 64 else
+                                 "pairtri_kernel<32> + tri_finish_kernel" if K <= 128 else
+                                 "pairdist_kernel + pair_finish_kernel") + " (packed fp32)",
+                        "dist2": "dist2_kernel + sum_rows_kernel",
                         "clip": "clip_diff_kernel", "rlr": "reduce_kernel<OpF32Rlr, RlrEpi>"}[a.op]
                        if a.op in ("secagg", "lsa", "krum", "dist2", "clip", "rlr") else
                        median_kernel_name(K, dom_dt) if a.op == "median" else
@@ -502,6 +561,16 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if world > 1:
+        # whole-job HBM rate: every rank's algorithmic bytes over the step time
+        line["roofline"]["aggregate_gbps"] = round(hbm_all, 1)
+        line["roofline"]["aggregate_frac_of_n_peaks"] = round(hbm_all / (world * HBM_PEAK_GBPS), 4)
+        if mode == "client":
+            line["exchange"] = {"collective": "reduce_scatter_tensor (RCCL)" if a.backend == "nccl" else "gloo (host)",
+                                "xgmi_bytes_per_rank_per_step": xgmi_bytes,
+                                "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
+                                "note": "comm_ms: mean over ranks of the chunks' reduce-scatter time on the comm "
+                                        "stream (overlapping the next chunk's reduction)"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
         line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
     if rank == 0:

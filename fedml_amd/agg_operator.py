@@ -31,6 +31,7 @@ import torch
 
 from . import _native as nat
 from . import kernels as kn
+from . import multidev
 from .bucket import ClientBucket
 
 _ACC_NAME = {kn.ACC_REFERENCE: "reference", kn.ACC_FP32: "fp32"}
@@ -212,6 +213,22 @@ def _chunks(order: Sequence[int]):
         lo += _TAIL_CHUNK
 
 
+def _device_chunks(groups):
+    """(chunk index within its device, key indices) over every device's keys:
+    each device's own chunk schedule, the devices interleaved, so every GPU
+    gets its largest keys early (a multi-device bucket's views put a round on
+    several GPUs, fedml_amd.multidev)."""
+    its = [enumerate(_chunks(order)) for _, order in groups]
+    while its:
+        nxt = []
+        for it in its:
+            got = next(it, None)
+            if got is not None:
+                yield got
+                nxt.append(it)
+        its = nxt
+
+
 def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
     """Every key a contiguous, 16-byte aligned device tensor of one device
     (what the native walker verifies): one multi-tensor launch per dtype and
@@ -219,9 +236,12 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
     per-tensor Python work.  None if the walker declines any chunk (the caller
     then runs the general path, which raises the reference's errors; launches
     already made for earlier chunks only wrote outputs nobody sees)."""
-    order = w.order_by_size(dicts[0], keys)
-    if order is None:
-        return None
+    groups = w.group_by_device(dicts[0], keys) if hasattr(w, "group_by_device") else None
+    if groups is None:
+        order = w.order_by_size(dicts[0], keys)
+        if order is None:
+            return None
+        groups = [(None, order)]
     K = len(dicts)
     results: Dict[str, torch.Tensor] = {}
     keep = []  # device tables of the launches, alive until enqueued
@@ -229,7 +249,7 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
     start = {}  # device -> event on the caller's stream before this call's first kernel there
     joins = []  # (caller's stream, side stream) pairs to rejoin before returning
     try:
-        for ci, idx in enumerate(_chunks(order)):
+        for ci, idx in _device_chunks(groups):
             ck = [keys[i] for i in idx]
             walked = w.walk(dicts, ck, True)
             if walked is None:
@@ -321,9 +341,12 @@ def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDic
     K = len(dicts)
     d0 = dicts[0]
     device = _host_device(args)
+    layout = [(k, tuple(d0[k].shape), d0[k].dtype) for k in keys]
+    devices = multidev.devices_for_round(args, layout, K, device)
+    if len(devices) > 1:
+        return _reduce_host_multi(layout, devices, tables, numels, codes, dicts, weights, acc_mode)
     with torch.cuda.device(device):
-        bucket = _cached_bucket([(k, tuple(d0[k].shape), d0[k].dtype) for k in keys], K, device,
-                                _ACC_NAME[acc_mode])
+        bucket = _cached_bucket(layout, K, device, _ACC_NAME[acc_mode])
         if K * sum(n * _ROW_ESZ[c] for n, c in zip(numels, codes)) <= _BATCH_MAX_BYTES:
             bucket.put_batch(tables, dicts, [1] * K)
         else:  # large round: per client, packing the next while the last one's DMA runs
@@ -331,6 +354,37 @@ def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDic
             for i in range(K):
                 bucket.put_from_table(i, t2d, dicts[i], 1)
         return bucket.reduce_to_host(weights)  # reduce, D2H and host scatter overlapped
+
+
+_MULTI: "OrderedDict[tuple, multidev.MultiDeviceBucket]" = OrderedDict()
+
+
+def _reduce_host_multi(layout, devices, tables, numels, codes, dicts, weights, acc_mode
+                       ) -> "OrderedDict[str, torch.Tensor]":
+    """A host round over several GPUs of this process (multidev): whole keys
+    per device, each client's keys packed and sent over each device's own
+    PCIe link, every device reducing its keys in the reference order (no
+    exchange, bit-exact), results scattered back into per-key host tensors.
+    The bucket is cached per (layout, K, devices) like the one-device one."""
+    K = len(dicts)
+    key = (tuple((k, s, str(d)) for k, s, d in layout), K, tuple(str(d) for d in devices), acc_mode)
+    b = _MULTI.pop(key, None)
+    if b is None:
+        _MULTI.clear()  # one multi-device round resident at a time: they are the big ones
+        b = multidev.MultiDeviceBucket(layout, K, devices, low_precision_acc=_ACC_NAME[acc_mode])
+    _MULTI[key] = b
+    t2d = {c: np.frombuffer(t, dtype=np.int64).reshape(-1, K) for c, t in tables.items()}
+    per_shard = b.split_tables(t2d)
+    if K * sum(n * _ROW_ESZ[c] for n, c in zip(numels, codes)) <= _BATCH_MAX_BYTES:
+        b.put_batch(per_shard, dicts, [1] * K)
+    else:
+        for i in range(K):
+            b.put_from_tables(i, per_shard, dicts[i], 1)
+    return b.reduce_to_host(weights)
+
+
+def _multi_requested(args) -> bool:
+    return len(multidev.parse_devices(getattr(args, "fedagg_devices", None))) > 1
 
 
 def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights: Sequence[float], args
@@ -344,7 +398,7 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
         dicts, keys = list(dicts), list(keys)
         t0 = dicts[0].get(keys[0]) if isinstance(dicts[0], dict) else None
         if isinstance(t0, torch.Tensor) and not t0.is_cuda and getattr(args, "fedagg_device", None) is None \
-                and torch.cuda.is_available():
+                and torch.cuda.is_available() and not _multi_requested(args):
             res = _reduce_host_round(w, dicts, keys, weights)
             if res is not None:
                 return res

@@ -544,6 +544,15 @@ class ClientBucket:
         of the scatter); ``into`` as in to_host.  Same results as
         reduce_into + to_host (the chunked launches are the same per-element
         chains)."""
+        return self.finish_to_host(self.launch_to_host(weights, num_clients, into, chunks, timings))
+
+    def launch_to_host(self, weights: Sequence[float], num_clients: Optional[int] = None,
+                       into: Optional[Dict[str, torch.Tensor]] = None, chunks: int = 8,
+                       timings: Optional[dict] = None) -> tuple:
+        """The GPU half of reduce_to_host: every reduction and D2H enqueued,
+        nothing waited for.  finish_to_host(state) then scatters into the
+        per-key host tensors.  A multi-device bucket launches every device's
+        half before finishing any (fedml_amd.multidev)."""
         K = num_clients if num_clients is not None else self.capacity
         if not 1 <= K <= self.capacity:
             raise ValueError(f"num_clients {K} outside [1, {self.capacity}]")
@@ -598,6 +607,13 @@ class ClientBucket:
                 kn.wsum_ptrs(dt, gg.d_ptrs, w64 if dt == torch.float64 else w32, K, gg.length, outs[dt], True,
                              self.acc_mode)
             t["launched"] = True
+        return pooled, per_key, dom, plan, done, minor, outs
+
+    def finish_to_host(self, state: tuple) -> "OrderedDict[str, torch.Tensor]":
+        """The host half of reduce_to_host (see launch_to_host)."""
+        pooled, per_key, dom, plan, done, minor, outs = state
+        g = self.groups[dom]
+        with torch.cuda.device(self.device):
             dst = np.array([per_key[k].data_ptr() for k in g.keys], dtype=np.int64)
             src = self._pinned_result(dom).data_ptr()
             for (lo, hi, _, (idx, src_off, dst_off, nbytes)), fin in zip(plan, done):

@@ -46,6 +46,7 @@ import torch
 from .bucket import ClientBucket
 from .context import Context, shared_context
 from .layout import ROW_DTYPES
+from .multidev import MultiDeviceBucket, devices_for_round, parse_devices
 
 
 class FedMLAggregator:
@@ -100,16 +101,27 @@ class FedMLAggregator:
         to device views of it.  False when the bucket cannot hold this update
         exactly (the caller then moves it key by key)."""
         device = torch.device(self.device) if not isinstance(self.device, torch.device) else self.device
-        if device.type != "cuda" or not 0 <= index < self.client_num:
+        devices = parse_devices(getattr(self.args, "fedagg_devices", None))
+        if (device.type != "cuda" and not devices) or not 0 <= index < self.client_num:
             return False
+        if device.type != "cuda":
+            device = devices[0]
         entries = []
         for key, t in model_params.items():
             if not isinstance(t, torch.Tensor) or t.dtype not in ROW_DTYPES or t.is_sparse:
                 return False
             entries.append((key, tuple(t.shape), t.dtype))
         if self.bucket is None:
-            # int64 keys keep int64 rows, so the views have the update's dtypes
-            self.bucket = ClientBucket(entries, self.client_num, device, promote_ints=False)
+            # int64 keys keep int64 rows, so the views have the update's dtypes.
+            # A round that does not fit one GPU (or args.fedagg_devices listing
+            # several) is spread over the node's GPUs, whole keys per device:
+            # the views are then one-device tensors on different GPUs, and
+            # agg() reduces each GPU's keys where they are (fedml_amd.multidev)
+            devices = devices_for_round(self.args, entries, self.client_num, device, promote_ints=False)
+            if len(devices) > 1:
+                self.bucket = MultiDeviceBucket(entries, self.client_num, devices, promote_ints=False)
+            else:
+                self.bucket = ClientBucket(entries, self.client_num, devices[0], promote_ints=False)
         elif self.bucket.entries != entries:
             return False
         self.bucket.put(index, model_params, sample_num)
@@ -202,6 +214,38 @@ class FedMLAggregator:
                 ctx.add(Context.KEY_METRICS_ON_LAST_ROUND, metric_result_in_current_round)
             logging.info("key_metrics_on_last_round = {}".format(ctx.get(Context.KEY_METRICS_ON_LAST_ROUND)))
         logging.info("round_idx = %d" % round_idx)  # mlops.log({"round_idx": ...}) in the reference
+
+    # ---- model-serving metadata (:211-258) -------------------------------------------
+
+    def _dummy_features(self):
+        """First sample of the first batch of the server's test loader (or of
+        the first non-empty client test loader when there is none), every
+        tensor of the batch but the last (the label), as the reference does."""
+        loader = self.test_global
+        if not loader:
+            for _, v in self.test_data_local_dict.items():
+                if v:
+                    loader = v
+                    break
+        with torch.no_grad():
+            batch = next(iter(loader))
+            firsts = [t[:1] for t in batch]
+        return firsts[:-1]
+
+    def get_dummy_input_tensor(self):
+        """:211-227, called by FedMLServerManager before the first round
+        (fedml_server_manager.py:71-85) to log the model's input for serving."""
+        return self._dummy_features()
+
+    def get_input_shape_type(self):
+        """:229-258: per input feature its shape and "int" for integer / bool
+        dtypes, "float" otherwise."""
+        ints = (torch.int8, torch.int16, torch.int32, torch.int64, torch.uint8, torch.bool)
+        shapes, types = [], []
+        for f in self._dummy_features():
+            shapes.append(list(f.shape))
+            types.append("int" if f.dtype in ints else "float")
+        return shapes, types
 
     # ---- client selection (:113-165, the same seeded numpy draws) ------------------
 

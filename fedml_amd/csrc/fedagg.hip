@@ -557,7 +557,9 @@ struct LsaEpi {
 struct RlrAcc {
   float a, s;
 };
-__device__ __forceinline__ float sign_of(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : x); }  // ±0, NaN: x
+// torch.sign: (0 < x) - (x < 0), so +0 for ±0 AND for NaN (the sign sum of a
+// column holding a NaN still counts the other clients' signs)
+__device__ __forceinline__ float sign_of(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 struct OpF32Rlr {
   using in_t = float; using out_t = float; using acc_t = RlrAcc; using w_t = float;
   static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return {x * w, sign_of(x)}; }

@@ -385,6 +385,11 @@ PyObject* host_round(PyObject*, PyObject* args) {
       w[size_t(i)] = static_cast<float>(v);  // RNE, as torch rounds the scalar of p * w
     }
     std::vector<const void*> src(size_t(T) * K);
+    // every source tensor, held (a handle copy holds its storage) until the
+    // native call returns: the GIL is released around it, and another thread
+    // (e.g. a transport's receive thread) may rebind or drop a dict entry
+    std::vector<at::Tensor> keep;
+    keep.reserve(size_t(T) * K);
     std::vector<int32_t> codes(T);
     std::vector<int64_t> numels(T);
     std::vector<at::Tensor> outs;
@@ -414,6 +419,7 @@ PyObject* host_round(PyObject*, PyObject* args) {
           Py_RETURN_NONE;
         }
         src[size_t(t) * K + i] = x.data_ptr();
+        keep.push_back(x);
       }
       total += numels[t];
       if (total * 4 * K > max_bytes) Py_RETURN_NONE;  // a big round: the staging-ring path
@@ -445,7 +451,59 @@ PyObject* host_round(PyObject*, PyObject* args) {
   }
 }
 
+// group_by_device(d: dict, keys: list) -> None | [(device, [key indices])]
+//   The keys of one state dict grouped by the CUDA device their tensor lives
+//   on (devices in order of first appearance), each group largest tensor
+//   first (stable).  A multi-device bucket (fedml_amd.multidev) leaves a
+//   round's keys spread over several GPUs; the pipelined device reduction
+//   walks and launches each device's keys as their own chunks.  None if a
+//   value is not a plain tensor on a CUDA device (the caller's general path
+//   handles it).
+PyObject* group_by_device(PyObject*, PyObject* args) {
+  PyObject* d;
+  PyObject* keys;
+  if (!PyArg_ParseTuple(args, "OO!", &d, &PyList_Type, &keys)) return nullptr;
+  if (!plain_lookup(d)) Py_RETURN_NONE;
+  const Py_ssize_t T = PyList_GET_SIZE(keys);
+  std::vector<int> dev_order;
+  std::vector<std::vector<std::pair<int64_t, Py_ssize_t>>> groups;
+  for (Py_ssize_t t = 0; t < T; ++t) {
+    PyObject* v = PyDict_GetItemWithError(d, PyList_GET_ITEM(keys, t));
+    if (!v) {
+      if (PyErr_Occurred()) return nullptr;
+      Py_RETURN_NONE;
+    }
+    if (Py_TYPE(v) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) Py_RETURN_NONE;
+    const at::Tensor& x = THPVariable_Unpack(v);
+    if (!x.defined() || x.device().type() != c10::DeviceType::CUDA) Py_RETURN_NONE;
+    const int dev = x.get_device();
+    size_t g = 0;
+    while (g < dev_order.size() && dev_order[g] != dev) ++g;
+    if (g == dev_order.size()) {
+      dev_order.push_back(dev);
+      groups.emplace_back();
+    }
+    groups[g].push_back({-x.numel(), t});
+  }
+  PyObject* out = PyList_New(Py_ssize_t(groups.size()));
+  if (!out) return nullptr;
+  for (size_t g = 0; g < groups.size(); ++g) {
+    auto& sz = groups[g];
+    std::stable_sort(sz.begin(), sz.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    PyObject* idx = PyList_New(Py_ssize_t(sz.size()));
+    if (!idx) {
+      Py_DECREF(out);
+      return nullptr;
+    }
+    for (size_t j = 0; j < sz.size(); ++j) PyList_SET_ITEM(idx, Py_ssize_t(j), PyLong_FromSsize_t(sz[j].second));
+    PyList_SET_ITEM(out, Py_ssize_t(g), Py_BuildValue("(iN)", dev_order[g], idx));
+  }
+  return out;
+}
+
 PyMethodDef kMethods[] = {
+    {"group_by_device", group_by_device, METH_VARARGS,
+     "Key indices of a state dict grouped by CUDA device, largest first, or None."},
     {"host_round", host_round, METH_VARARGS, "One small host round through fedagg_host_round_f32, or None."},
     {"walk", walk, METH_VARARGS, "Pointer tables of K device state dicts for fedagg_wsum_multi, or None."},
     {"order_by_size", order_by_size, METH_VARARGS, "Key indices of a state dict, largest tensor first, or None."},

@@ -70,6 +70,19 @@ def _weight_decay(optimizer: str, weight_decay: Optional[float]) -> float:
     return 0.0
 
 
+def _check_momentum(optimizer: str, momentum) -> None:
+    """torch.optim.RMSprop takes `momentum=` and applies it (a momentum buffer
+    over g / (sqrt(v) + eps)); the MPI FedOptAggregator passes
+    server_momentum to the constructor (FedOptAggregator.py:49-54), so an
+    RMSprop server with momentum is a different optimizer from the fused one.
+    Refuse it rather than silently dropping the momentum.  Adam / AdamW /
+    Adagrad have no `momentum` argument (torch raises TypeError there; the SP
+    FedOptAPI passes lr only, fedopt_api.py:78-85), so it is ignored for them."""
+    if optimizer == "rmsprop" and momentum:
+        raise NotImplementedError(f"server_optimizer 'rmsprop' with server_momentum={momentum}: only the "
+                                  "momentum-free RMSprop step is fused")
+
+
 class FedOptServer:
     def __init__(self, global_state: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],
                  worker_num: int, server_optimizer: str = "sgd", server_lr: float = 1.0,
@@ -78,6 +91,7 @@ class FedOptServer:
         if self.optimizer not in FUSED_OPTIMIZERS:
             raise NotImplementedError(f"server_optimizer {server_optimizer!r}: {FUSED_OPTIMIZERS} are fused")
         self.lr = float(server_lr)
+        _check_momentum(self.optimizer, server_momentum)
         self.momentum = float(server_momentum) if self.optimizer == "sgd" else 0.0
         # torch.optim defaults (sp/fedopt/fedopt_api.py:79-85 passes lr only)
         self.betas, self.eps = (0.9, 0.999), (1e-10 if self.optimizer == "adagrad" else 1e-8)

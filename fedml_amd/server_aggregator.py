@@ -41,6 +41,17 @@ from .agg_operator import FedMLAggOperator
 _UNSUPPORTED_FLAGS = ("enable_fhe", "enable_dp", "enable_attack", "enable_contribution")
 
 
+# attributes each defender's __init__ reads (krum_defense.py, norm_diff_clipping_
+# defense.py, cclip_defense.py, slsgd_defense.py; FedMLDefender.init builds it)
+_DEFENSE_ATTRS = {
+    dfn.DEFENSE_KRUM: ("byzantine_client_num",),
+    dfn.DEFENSE_MULTIKRUM: ("byzantine_client_num",),
+    dfn.DEFENSE_NORM_DIFF_CLIPPING: ("norm_bound",),
+    dfn.DEFENSE_CCLIP: ("bucket_size",),
+    dfn.DEFENSE_SLSGD: ("trim_param_b",),  # then the alpha check, then option_type
+}
+
+
 def _check_flags(args) -> None:
     for flag in _UNSUPPORTED_FLAGS:
         if getattr(args, flag, False):
@@ -51,8 +62,13 @@ def _check_flags(args) -> None:
         dt = str(getattr(args, "defense_type", "")).strip()
         if dt not in dfn.SUPPORTED:
             raise NotImplementedError(f"defense_type {dt!r}: fedml_amd runs {dfn.SUPPORTED} on the GPU")
+        # the defender's constructor reads these at FedMLDefender.init, so a
+        # missing one fails at construction there, not at the first round
+        for attr in _DEFENSE_ATTRS.get(dt, ()):
+            getattr(args, attr)
         if dt == dfn.DEFENSE_SLSGD:
             dfn.slsgd_alpha_check(args.alpha)  # SLSGDDefense.__init__ raises at FedMLDefender.init
+            args.option_type
         if dt == dfn.DEFENSE_ROBUST_LEARNING_RATE:
             args.robust_threshold  # RobustLearningRateDefense.__init__ reads it at FedMLDefender.init
         if dt == dfn.DEFENSE_WEAK_DP:
@@ -151,15 +167,19 @@ class ServerAggregator(ABC):
 
 def _evaluate(model, test_data, device, task: str) -> dict:
     """The `_test` loops of default_aggregator.py:25-75 ("classification", and
-    its stackoverflow_lr branch "tag_prediction"), my_server_aggregator_
-    prediction.py:19-60 ("tag_prediction") and my_server_aggregator_nwp.py:
-    19-43 ("nwp"): the same criteria, predictions and metric sums.  Server
+    its stackoverflow_lr branch "default_multilabel": BCE and the precision /
+    recall sums, with the default class's test_total rule, size(0) for 1-D
+    targets and size(0)*size(1) for 2-D ones, :71-74), my_server_aggregator_
+    prediction.py:19-60 ("tag_prediction": test_total += size(0)) and
+    my_server_aggregator_nwp.py:19-43 ("nwp"): the same criteria, predictions
+    and metric sums.  Server
     evaluation is model inference, not aggregation; it runs with torch on
     `device` exactly as in the reference."""
     model.to(device)
     model.eval()
     metrics = {"test_correct": 0, "test_loss": 0, "test_total": 0}
-    if task == "tag_prediction":
+    multilabel = task in ("tag_prediction", "default_multilabel")
+    if multilabel:
         metrics.update(test_precision=0, test_recall=0)
         criterion = nn.BCELoss(reduction="sum").to(device)
     elif task == "nwp":
@@ -173,7 +193,7 @@ def _evaluate(model, test_data, device, task: str) -> dict:
             target = target.to(device)
             pred = model(x)
             loss = criterion(pred, target)
-            if task == "tag_prediction":
+            if multilabel:
                 predicted = (pred > 0.5).int()
                 correct = predicted.eq(target).sum(axis=-1).eq(target.size(1)).sum()
                 true_positive = ((target * predicted) > 0.1).int().sum(axis=-1)
@@ -238,7 +258,7 @@ class MI355XServerAggregator(ServerAggregator):
     def _test(self, test_data, device, args):
         task = self._task
         if task == "classification" and getattr(args, "dataset", None) == "stackoverflow_lr":
-            task = "tag_prediction"  # default_aggregator.py:45-63
+            task = "default_multilabel"  # default_aggregator.py:45-63
         return _evaluate(self.model, test_data, device, task)
 
     def test(self, test_data, device, args):

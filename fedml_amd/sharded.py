@@ -105,8 +105,12 @@ class ClientAxisAggregator:
             out.append((a, a + self.piece))
         return out
 
-    def aggregate(self, weights: Sequence[float], events: Optional[List] = None) -> torch.Tensor:
-        """weights: the GLOBAL w_i of this rank's K_local clients, in order."""
+    def aggregate(self, weights: Sequence[float], events: Optional[List] = None,
+                  comm_events: Optional[List] = None) -> torch.Tensor:
+        """weights: the GLOBAL w_i of this rank's K_local clients, in order.
+        events[c] / comm_events[c]: (start, end) torch.cuda.Events around
+        chunk c's reduction (caller's stream) and its reduce-scatter (the
+        comm stream, from the partial being ready to the collective's end)."""
         if not self.on_gpu:
             return self._aggregate_host(weights)
         cur = torch.cuda.current_stream(self.device)
@@ -133,10 +137,16 @@ class ClientAxisAggregator:
                 # chunk c's exchange overlaps chunk c+1's reduction
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):
-                    works.append(dist.reduce_scatter_tensor(
+                    if comm_events is not None:
+                        comm_events[c][0].record(self.comm_stream)
+                    work = dist.reduce_scatter_tensor(
                         self.shard[c * self.piece:(c + 1) * self.piece],
                         self.partial[c * self.chunk_len:(c + 1) * self.chunk_len],
-                        op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+                        op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                    if comm_events is not None:
+                        work.wait()  # the comm stream waits for RCCL's own stream: the end event follows it
+                        comm_events[c][1].record(self.comm_stream)
+                    works.append(work)
             else:
                 self.shard[c * self.piece:(c + 1) * self.piece].copy_(
                     self.partial[c * self.chunk_len:(c + 1) * self.chunk_len])
@@ -279,11 +289,12 @@ class ShardedFedOpt:
     def __init__(self, rows: torch.Tensor, length: int, global_flat: torch.Tensor, optimizer: str = "sgd",
                  lr: float = 1.0, momentum: float = 0.0, group=None, chunks: int = 8, reducer=None, stepper=None,
                  buffers: Sequence[Tuple[int, int]] = (), weight_decay: Optional[float] = None):
-        from .fedopt import FUSED_OPTIMIZERS, _weight_decay
+        from .fedopt import FUSED_OPTIMIZERS, _check_momentum, _weight_decay
 
         self.optimizer = optimizer.lower()
         if self.optimizer not in FUSED_OPTIMIZERS:
             raise NotImplementedError(f"server_optimizer {optimizer!r}: {FUSED_OPTIMIZERS} are fused")
+        _check_momentum(self.optimizer, momentum)
         self.lr, self.momentum = float(lr), float(momentum) if self.optimizer == "sgd" else 0.0
         self.betas, self.eps = (0.9, 0.999), (1e-10 if self.optimizer == "adagrad" else 1e-8)
         self.alpha = 0.99
@@ -322,10 +333,11 @@ class ShardedFedOpt:
         if self.agg.on_gpu and stepper is None:
             self._src = kn.upload_i64([self.agg.shard.data_ptr()], dev)  # one source: the reduced shard
 
-    def aggregate(self, weights: Sequence[float], events: Optional[List] = None) -> torch.Tensor:
+    def aggregate(self, weights: Sequence[float], events: Optional[List] = None,
+                  comm_events: Optional[List] = None) -> torch.Tensor:
         """One round: weights are the GLOBAL w_i of this rank's clients.
         Returns this rank's updated parameter shard."""
-        avg = self.agg.aggregate(weights, events=events)
+        avg = self.agg.aggregate(weights, events=events, comm_events=comm_events)
         first = self.step_count == 0
         step = self.step_count + 1
         if self.stepper is not None:

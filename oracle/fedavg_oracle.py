@@ -754,7 +754,9 @@ def robust_learning_rate(raw_grad_list, robust_threshold, base_aggregation_func=
         avg = to_np(wsum(ts, ws)).astype(np.float32)
         sgn = np.zeros(avg.shape, dtype=np.float32)
         for t in ts:
-            sgn = np.asarray(sgn + np.sign(_f32(t)), dtype=np.float32)
+            x = _f32(t)
+            # torch.sign is (0 < x) - (x < 0): +0 for ±0 and for NaN (np.sign(NaN) is NaN)
+            sgn = np.asarray(sgn + ((x > 0).astype(np.float32) - (x < 0).astype(np.float32)), dtype=np.float32)
         lr = np.abs(sgn)
         with np.errstate(invalid="ignore"):
             lr = np.where(lr < thr, np.float32(-1), lr)

@@ -328,6 +328,10 @@ _dist("rlr_ragged_k9_t3_5", "robust_learning_rate", 9, [k for k in RAGGED_F32 if
       robust_threshold=3.5, flip=[2, 6])
 _dist("rlr_ragged_k5_tneg", "robust_learning_rate", 5, RAGGED_F32[:4], 343, robust_threshold=-2, flip=[0])
 _dist("rlr_resnet_mini_k6_t0", "robust_learning_rate", 6, RESNET_MINI, 344, robust_threshold=0)
+# NaN / ±0 / ±inf coordinates: torch.sign(NaN) = 0 and torch.sign(-0.0) = +0
+_dist("rlr_specials_k7_t2", "robust_learning_rate", 7, RAGGED_F32[:4], 345, robust_threshold=2, flip=[3],
+      specials={1: [(0, "nan"), (1, "-0"), (2, "inf"), (5, "nan")], 4: [(1, "nan"), (3, "-inf"), (6, "0")],
+                6: [(2, "-0"), (5, "-0"), (7, "nan")]})
 
 
 def dist_inputs(spec):
@@ -345,6 +349,14 @@ def dist_inputs(spec):
         for k, t in raw[int(i)][1].items():
             if t.is_floating_point():
                 t.neg_()
+    vals = {"nan": float("nan"), "inf": float("inf"), "-inf": float("-inf"), "-0": -0.0, "0": 0.0}
+    for i, marks in spec.get("specials", {}).items():
+        for k, t in raw[int(i)][1].items():
+            if t.is_floating_point() and t.numel():
+                flat = t.view(-1)
+                for pos, v in marks:
+                    if pos < flat.numel():
+                        flat[pos] = vals[v]
     glob = host_clients(entries, 1, spec["seed"] + 7)[0][1]
     return raw, glob
 

@@ -140,6 +140,62 @@ def test_server_test_tag_prediction_and_nwp():
     assert acc == exp_acc and loss > 0
 
 
+def test_default_aggregator_counts_2d_targets_on_stackoverflow_lr():
+    """DefaultServerAggregator on stackoverflow_lr (default_aggregator.py:45-74)
+    uses BCE and the multi-label metrics, but counts test_total as
+    size(0) * size(1) for a 2-D target (:71-74); the task-specific
+    MyServerAggregatorTAGPred counts size(0) (my_server_aggregator_prediction.py)."""
+    from fedml_amd.server_aggregator import MI355XServerAggregator, MI355XServerAggregatorTAGPred
+
+    class A(_EvalArgs):
+        dataset = "stackoverflow_lr"
+
+    torch.manual_seed(4)
+    model = torch.nn.Sequential(torch.nn.Linear(6, 4), torch.nn.Sigmoid())
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(20, 6, generator=g)
+    y = (torch.rand(20, 4, generator=g) > 0.5).float()
+    loader = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(x, y), batch_size=7)
+    d = MI355XServerAggregator(model, A())._test(loader, torch.device("cpu"), A())
+    t = MI355XServerAggregatorTAGPred(model, A())._test(loader, torch.device("cpu"), A())
+    assert d["test_total"] == 20 * 4 and t["test_total"] == 20
+    assert d["test_correct"] == t["test_correct"] and d["test_loss"] == t["test_loss"]
+    assert d["test_precision"] == t["test_precision"] and d["test_recall"] == t["test_recall"]
+
+
+def test_dummy_input_and_shape_type():
+    """fedml_aggregator.py:211-258: the first sample of the test loader's
+    first batch, all tensors but the label; "int" for integer dtypes."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(9, 3, 4, generator=g)
+    tok = torch.randint(0, 5, (9, 7), generator=g)
+    y = torch.randint(0, 2, (9,), generator=g)
+    loader = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(x, tok, y), batch_size=4)
+    s = FedMLAggregator(None, loader, 0, {}, {}, {}, 2, torch.device("cpu"), _Args(), None)
+    feats = s.get_dummy_input_tensor()
+    assert len(feats) == 2 and torch.equal(feats[0], x[:1]) and torch.equal(feats[1], tok[:1])
+    assert s.get_input_shape_type() == ([[1, 3, 4], [1, 7]], ["float", "int"])
+    # no server test set: the first non-empty client loader
+    s2 = FedMLAggregator(None, None, 0, {}, {0: None, 1: loader}, {}, 2, torch.device("cpu"), _Args(), None)
+    assert s2.get_input_shape_type() == ([[1, 3, 4], [1, 7]], ["float", "int"])
+
+
+def test_rmsprop_server_momentum_is_refused():
+    """torch's RMSprop applies `momentum=` and the MPI FedOptAggregator passes
+    server_momentum (FedOptAggregator.py:49-54): the fused momentum-free step
+    must not stand in for it."""
+    import pytest
+
+    from fedml_amd.fedopt import FedOptServer
+    from fedml_amd.sharded import ShardedFedOpt
+
+    sd = OrderedDict(w=torch.zeros(4))
+    with pytest.raises(NotImplementedError, match="rmsprop"):
+        FedOptServer(sd, ["w"], 2, "rmsprop", 0.1, 0.9, "cpu")
+    with pytest.raises(NotImplementedError, match="rmsprop"):
+        ShardedFedOpt(torch.zeros(2, 4), 4, torch.zeros(4), "rmsprop", 0.1, 0.9, reducer=lambda *a: None)
+
+
 class _RoundArgs:
     federated_optimizer = "FedAvg"
     dataset = "mnist"

@@ -251,6 +251,35 @@ def test_plugin_identity_defenses_read_their_config():
         _check_flags(SimpleNamespace(enable_defense=True, defense_type="foolsgold"))
 
 
+@pytest.mark.parametrize("dt,full", [
+    ("krum", dict(byzantine_client_num=1)),
+    ("multikrum", dict(byzantine_client_num=1)),
+    ("norm_diff_clipping", dict(norm_bound=0.5)),
+    ("cclip", dict(bucket_size=2)),
+    ("slsgd", dict(trim_param_b=1, alpha=0.5, option_type=2)),
+])
+def test_before_aggregation_defenses_read_their_config_at_construction(dt, full):
+    """The defenders' constructors read their config values at
+    FedMLDefender.init (krum_defense.py:20, norm_diff_clipping_defense.py:17,
+    cclip_defense.py:23, slsgd_defense.py:30-34): each missing one raises
+    AttributeError when the server aggregator is built, not at the first
+    round.  SLSGD checks alpha's bound before reading option_type."""
+    from types import SimpleNamespace
+
+    from fedml_amd.server_aggregator import MI355XServerAggregator
+
+    MI355XServerAggregator(torch.nn.Linear(2, 2), SimpleNamespace(enable_defense=True, defense_type=dt, **full))
+    for drop in full:
+        args = SimpleNamespace(enable_defense=True, defense_type=dt,
+                               **{k: v for k, v in full.items() if k != drop})
+        with pytest.raises(AttributeError):
+            MI355XServerAggregator(torch.nn.Linear(2, 2), args)
+    if dt == "slsgd":
+        with pytest.raises(ValueError):
+            MI355XServerAggregator(torch.nn.Linear(2, 2),
+                                   SimpleNamespace(enable_defense=True, defense_type=dt, trim_param_b=1, alpha=2))
+
+
 def test_robust_learning_rate_host_checks_before_device_work():
     """The reference's behaviour that needs no GPU: threshold 0 hands the list
     to the base function untouched; Σn = 0 raises ZeroDivisionError (at the

@@ -1,0 +1,135 @@
+"""Host logic of the in-process multi-device bucket (fedml_amd.multidev), no
+GPU: the key partition, the split of the walker's pointer tables, the device
+selection, and split -> per-device reduction -> reassembly against the oracle
+(each device's rows built with the same RowLayout its ClientBucket uses, the
+reduction done by the oracle in numpy)."""
+from __future__ import annotations
+
+import copy
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import cases
+from fedml_amd import multidev as md
+from fedml_amd import shapes
+from fedml_amd.layout import RowLayout
+from fedml_amd.synth import host_clients
+from oracle import fedavg_oracle as orc
+
+
+@pytest.mark.parametrize("model", ["resnet50", "vit_b16", "llama2_7b_lora", "cnn_web"])
+@pytest.mark.parametrize("G", [1, 2, 3, 4, 8])
+def test_shard_plan_partitions_whole_keys(model, G):
+    entries = shapes.MODELS[model]()
+    plan = md.shard_plan(entries, G)
+    assert 1 <= len(plan) <= G
+    seen = [e for s in plan for e in s]
+    assert sorted(k for k, _, _ in seen) == sorted(k for k, _, _ in entries)
+    order = {k: i for i, (k, _, _) in enumerate(entries)}
+    for s in plan:  # the model's key order inside every device
+        idx = [order[k] for k, _, _ in s]
+        assert idx == sorted(idx)
+    loads = md.shard_loads(plan)
+    biggest = max(md.entry_bytes(e) for e in entries)
+    assert max(loads) - min(loads) <= biggest  # LPT: within one key of each other
+    if len(plan) == G:
+        mean = sum(loads) / G
+        # the balance DESIGN.md / multidev.py quote
+        bound = {"resnet50": 1e-5, "vit_b16": 0.04, "llama2_7b_lora": 0.008, "cnn_web": 6.2}[model]
+        assert max(loads) <= mean * (1 + bound)
+
+
+def test_shard_plan_exact_cases():
+    e = [("a", (10,), torch.float32), ("b", (0,), torch.float32), ("c", (10,), torch.float32),
+         ("n", (), torch.int64), ("d", (5,), torch.bfloat16)]
+    plan = md.shard_plan(e, 2)
+    # bytes a 40, c 40, d 10, n 4: LPT a->0, c->1, d->0, n->1; no move or swap lowers 50 / 44
+    assert [k for k, _, _ in plan[0]] == ["a", "b", "d"] and [k for k, _, _ in plan[1]] == ["c", "n"]
+    # more devices than keys with data: the empty ones are dropped
+    assert len(md.shard_plan(e, 16)) == 4
+    assert md.shard_plan(e, 1) == [e]
+    with pytest.raises(ValueError):
+        md.shard_plan(e, 0)
+
+
+def test_split_tables_rows_follow_each_device():
+    entries = [("a", (3,), torch.float32), ("h", (2,), torch.bfloat16), ("b", (7,), torch.float32),
+               ("n", (), torch.int64), ("c", (1,), torch.float32), ("g", (4,), torch.bfloat16)]
+    K = 3
+    # fake pointers: key index * 1000 + client
+    f32 = [k for k, _, d in entries if d == torch.float32]
+    b16 = [k for k, _, d in entries if d == torch.bfloat16]
+    tables = {0: np.array([[1000 * [k for k, _, _ in entries].index(k) + i for i in range(K)] for k in f32]),
+              1: np.array([[1000 * [k for k, _, _ in entries].index(k) + i for i in range(K)] for k in b16])}
+    plan = md.shard_plan(entries, 2)
+    parts = md.split_tables(entries, plan, tables)
+    names = [k for k, _, _ in entries]
+    for shard, t in zip(plan, parts):
+        for code, dt in ((0, torch.float32), (1, torch.bfloat16)):
+            keys = [k for k, _, d in shard if d == dt]
+            if not keys:
+                assert code not in t
+                continue
+            want = np.array([[1000 * names.index(k) + i for i in range(K)] for k in keys])
+            np.testing.assert_array_equal(t[code], want)
+
+
+def test_parse_devices_and_selection():
+    assert md.parse_devices(None) == []
+    assert md.parse_devices("0, 1") == [torch.device("cuda", 0), torch.device("cuda", 1)]
+    assert md.parse_devices([0, "cuda:2", torch.device("cuda", 0)]) == \
+        [torch.device("cuda", 0), torch.device("cuda", 2), torch.device("cuda", 0)]
+    assert md.parse_devices(["cuda"]) == [torch.device("cuda", 0)]
+    with pytest.raises(ValueError):
+        md.parse_devices(["cpu"])
+    e = shapes.resnet50()
+    args = SimpleNamespace(fedagg_devices="0,0,0")
+    assert md.devices_for_round(args, e, 128, torch.device("cuda", 0)) == [torch.device("cuda", 0)] * 3
+    # ResNet-50 x 128 clients: 13.1 GB of rows + the result row
+    rb = md.round_bytes(e, 128)
+    assert 128 * 25_610_205 * 4 < rb < 129 * 25_620_000 * 4
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 4])
+def test_split_reduce_reassemble_matches_oracle(G):
+    """Each device's rows are packed with the RowLayout its ClientBucket uses
+    (integer keys as fl32(v) in the fp32 row), reduced by the oracle's FedAvg
+    chain per row, cut back into keys and merged in the model's order: equal
+    bit for bit to the oracle over the whole dicts."""
+    entries = cases._entries(cases.RESNET_MINI) + [("zz.big", (4099,), torch.float32), ("zz.empty", (0,), torch.float32),
+                                                    ("zz.half", (37,), torch.bfloat16)]
+    K = 5
+    raw = host_clients(entries, K, seed=11)
+    args = cases.Args(dict(optimizer="FedAvg"))
+    expected = orc.agg(args, copy.deepcopy(raw))
+    ns = [n for n, _ in raw]
+    w = [n / sum(ns) for n in ns]
+    plan = md.shard_plan(entries, G)
+    parts = []
+    for shard in plan:
+        lay = RowLayout(shard, promote_ints=True)
+        part = OrderedDict()
+        for dt, g in lay.groups.items():
+            rows = np.zeros((K, max(g.length, 1)), dtype=np.float32 if dt == torch.float32 else np.uint16)
+            for i, (_, d) in enumerate(raw):
+                for key, off, n in zip(g.keys, g.offsets, g.numels):
+                    t = d[key].reshape(-1)
+                    t = t.to(torch.float32) if key in lay.int_keys else t
+                    rows[i, off:off + n] = t.view(torch.int16).numpy().view(np.uint16) if dt == torch.bfloat16 \
+                        else t.numpy()
+            flat = [torch.from_numpy(rows[i]) if dt == torch.float32 else
+                    torch.from_numpy(rows[i].view(np.int16)).view(torch.bfloat16) for i in range(K)]
+            out = orc.wsum(flat, w)
+            for key, off, n, shape in zip(g.keys, g.offsets, g.numels, g.shapes):
+                part[key] = out[off:off + n].reshape(shape)
+        parts.append(part)
+    got = md.merge_in_order(entries, parts)
+    assert list(got) == list(expected)
+    for k, e in expected.items():
+        assert got[k].dtype == e.dtype and got[k].shape == e.shape, k
+        assert torch.equal(got[k].view(torch.int16) if e.dtype == torch.bfloat16 else got[k].view(torch.int32),
+                           e.view(torch.int16) if e.dtype == torch.bfloat16 else e.view(torch.int32)), k
