@@ -815,7 +815,16 @@ template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; st
 // LoRA-sized keys) use 256-element tiles of 64 lanes with 16 clients in flight
 // per lane: ~16x more workgroups and one memory round trip per 16 clients.
 struct SmallCfg { static constexpr int U = 16, V = 1, BS = 64; static constexpr bool NT = true; };
-constexpr int64_t kSmallBelowBlocks = 1024;  // shipped-tile workgroups below which SmallCfg is used
+// shipped-tile workgroups below which SmallCfg is used.  Round 3 re-measured
+// the sizes between configs 2 and 5 (the per-rank shards of strong scaling,
+// tools/tune_mid.py, profiles/r03/tune_mid.txt, 25 interleaved rounds): the
+// small tiles lead up to 128 blocks and trail U2V4 by 8-10 % at 256 blocks
+// and U1V4 by 5-7 % at 512-1,023 blocks, where round 2 still used them.
+constexpr int64_t kSmallBelowBlocks = 256;
+// 256-511 blocks: two clients in flight per lane (U2V4), 0-1 % off the best
+// variant at K = 32, 64 and 128; U1V4 trails it there by 10-17 %.
+struct Mid2Cfg { static constexpr int U = 2, V = 4, BS = 256; static constexpr bool NT = true; };
+constexpr int64_t kMid2BelowBlocks = 512;
 
 // Many clients over a tensor too small to give every CU a workgroup (e.g. 1,000
 // clients x a 7,850-element model): each lane's chain over the clients is a
@@ -869,6 +878,8 @@ int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t
     return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
+  if (blocks < kMid2BelowBlocks)
+    return launch_uvn<OP, Mid2Cfg::U, Mid2Cfg::V, Mid2Cfg::NT, Mid2Cfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks <= kMidUpToBlocks)
     return launch_uvn<OP, MidCfg::U, MidCfg::V, MidCfg::NT, MidCfg::BS, WS>(s, w, K, N, o, al, st, name);
   return launch_uvn<OP, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS, WS>(s, w, K, N, o, al, st, name);
@@ -898,6 +909,9 @@ int launch_epi(const Seg<OP>& s, const EPI& epi, const WS& w, int32_t K, bool al
   if (blocks < kSmallBelowBlocks)
     return launch_epi_cfg<OP, EPI, WS, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS>(s, epi, w, K, aligned,
                                                                                             st, name);
+  if (blocks < kMid2BelowBlocks)
+    return launch_epi_cfg<OP, EPI, WS, Mid2Cfg::U, Mid2Cfg::V, Mid2Cfg::NT, Mid2Cfg::BS>(s, epi, w, K, aligned, st,
+                                                                                        name);
   if (blocks <= kMidUpToBlocks)
     return launch_epi_cfg<OP, EPI, WS, MidCfg::U, MidCfg::V, MidCfg::NT, MidCfg::BS>(s, epi, w, K, aligned, st, name);
   return launch_epi_cfg<OP, EPI, WS, Cfg<OP>::U, Cfg<OP>::V, Cfg<OP>::NT, Cfg<OP>::BS>(s, epi, w, K, aligned, st,
@@ -967,6 +981,11 @@ int persistent_fn(const float* const* src, const float* w, int32_t K, int64_t N,
   return check_launch("persistent");
 }
 
+// what fedagg_wsum_f32 dispatches for this size (Tiny / Small / Mid / shipped tiles)
+int shipped_fn(const float* const* src, const float* w, int32_t K, int64_t N, float* out, hipStream_t st) {
+  return launch_ws<OpF32>(src, PtrW<float>{w}, K, N, out, true, st, "fedagg_wsum_f32_variant");
+}
+
 const Variant kVariants[] = {
     {"U8V1nt", variant_fn<8, 1, true, 256>},      {"U8V2nt", variant_fn<8, 2, true, 256>},
     {"U4V4nt", variant_fn<4, 4, true, 256>},      {"U2V4nt", variant_fn<2, 4, true, 256>},
@@ -980,6 +999,10 @@ const Variant kVariants[] = {
     {"U1V4nt", variant_fn<1, 4, true, 256>},      {"U1V2nt", variant_fn<1, 2, true, 256>},
     {"U2V2nt", variant_fn<2, 2, true, 256>},
     {"U4V4nt_xcd", xcd_fn<4, 4, 256>},            {"U1V4nt_xcd", xcd_fn<1, 4, 256>},
+    {"U16V1nt_b64", variant_fn<16, 1, true, 64>}, {"U8V1nt_b64", variant_fn<8, 1, true, 64>},
+    {"U8V2nt_b64", variant_fn<8, 2, true, 64>},   {"U4V4nt_b64", variant_fn<4, 4, true, 64>},
+    {"U2V4nt_b128", variant_fn<2, 4, true, 128>}, {"U1V4nt_b128", variant_fn<1, 4, true, 128>},
+    {"shipped", shipped_fn},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 

@@ -172,30 +172,36 @@ class ClientAxisAggregator:
         return self.shard
 
     def shard_in_model_dtype(self) -> torch.Tensor:
-        """This rank's shard rounded once to the rows' dtype (bf16/f16 models);
+        """This rank's shard rounded once (RNE) to the rows' dtype (bf16/f16
+        models; fedagg_round_f32 on the GPU, torch's RNE cast for host rows);
         fp32 rows return the fp32 shard itself."""
-        if self.dtype in (torch.bfloat16, torch.float16) and self.on_gpu:
-            return kn.round_f32(self.shard, self.dtype)
+        if self.dtype in (torch.bfloat16, torch.float16):
+            return kn.round_f32(self.shard, self.dtype) if self.on_gpu else self.shard.to(self.dtype)
         return self.shard
 
-    def gather_full(self) -> torch.Tensor:
+    def gather_full(self, shard: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Reassemble the full [length] result on every rank (all-gather of the
-        shards; used by tests and when the model must be replicated)."""
+        shards; used by tests and when the model must be replicated).  shard:
+        a tensor shaped like this rank's shard (default: the fp32 shard; e.g.
+        shard_in_model_dtype()'s 16-bit one, gathered widened to fp32, which
+        is exact both ways: gloo has no 16-bit types)."""
+        src = self.shard if shard is None else shard
+        words = src.to(torch.float32) if src.dtype in (torch.bfloat16, torch.float16) else src
         if not self.collective:
-            parts = [self.shard]
+            parts = [words]
         elif self.host_staged:
-            parts = [torch.empty_like(self.shard, device="cpu") for _ in range(self.world)]
-            dist.all_gather(parts, self.shard.cpu(), group=self.group)
-            parts = [p.to(self.shard.device) for p in parts]
+            parts = [torch.empty_like(words, device="cpu") for _ in range(self.world)]
+            dist.all_gather(parts, words.cpu(), group=self.group)
+            parts = [p.to(words.device) for p in parts]
         else:
-            parts = [torch.empty_like(self.shard) for _ in range(self.world)]
-            dist.all_gather(parts, self.shard, group=self.group)
-        full = torch.empty(len(self.bounds) * self.chunk_len, dtype=self.shard.dtype, device=self.shard.device)
+            parts = [torch.empty_like(words) for _ in range(self.world)]
+            dist.all_gather(parts, words, group=self.group)
+        full = torch.empty(len(self.bounds) * self.chunk_len, dtype=words.dtype, device=words.device)
         for c in range(len(self.bounds)):
             for r in range(self.world):
                 full[c * self.chunk_len + r * self.piece: c * self.chunk_len + (r + 1) * self.piece] = \
                     parts[r][c * self.piece:(c + 1) * self.piece]
-        return full[:self.length]
+        return full[:self.length].to(src.dtype)
 
     @staticmethod
     def tolerance(abs_terms_sum: torch.Tensor, k_total: int, world: int) -> torch.Tensor:

@@ -45,6 +45,21 @@ RAGGED_BF16 = [["a", [37], BF16], ["b", [1007], BF16], ["c", [3, 5, 7], BF16], [
 RAGGED_F32 = [["a", [1], F32], ["b", [5], F32], ["c", [1023], F32], ["d", [4099], F32],
               ["e", [0], F32], ["scalar", [], F32], ["big", [70001], F32]]
 
+# ViT-B/16's key structure (shapes.vit_b16, torchvision names) at width 64, one layer
+_VP = "encoder.layers.encoder_layer_0"
+VIT_MINI = [["class_token", [1, 1, 64], BF16], ["conv_proj.weight", [64, 3, 4, 4], BF16], ["conv_proj.bias", [64], BF16],
+            ["encoder.pos_embedding", [1, 17, 64], BF16],
+            [f"{_VP}.ln_1.weight", [64], BF16], [f"{_VP}.ln_1.bias", [64], BF16],
+            [f"{_VP}.self_attention.in_proj_weight", [192, 64], BF16],
+            [f"{_VP}.self_attention.in_proj_bias", [192], BF16],
+            [f"{_VP}.self_attention.out_proj.weight", [64, 64], BF16],
+            [f"{_VP}.self_attention.out_proj.bias", [64], BF16],
+            [f"{_VP}.ln_2.weight", [64], BF16], [f"{_VP}.ln_2.bias", [64], BF16],
+            [f"{_VP}.mlp.0.weight", [256, 64], BF16], [f"{_VP}.mlp.0.bias", [256], BF16],
+            [f"{_VP}.mlp.3.weight", [64, 256], BF16], [f"{_VP}.mlp.3.bias", [64], BF16],
+            ["encoder.ln.weight", [64], BF16], ["encoder.ln.bias", [64], BF16],
+            ["heads.head.weight", [10, 64], BF16], ["heads.head.bias", [10], BF16]]
+
 CASES: List[Dict[str, Any]] = []
 
 
@@ -64,6 +79,11 @@ for _k in (1, 2, 3, 9, 17, 128):
 # 16-bit and 64-bit floats
 for _k in (2, 3, 32):
     _add(f"ragged_bf16_k{_k}", "FedAvg", _k, RAGGED_BF16, seed=30 + _k)
+# config 4's client count (512 x ViT-B/16 bf16): the reference rounds to bf16
+# after every client, so K is what matters; a ragged key set and a one-block
+# ViT with config 4's key structure, at K = 512
+_add("ragged_bf16_k512", "FedAvg", 512, RAGGED_BF16, seed=35)
+_add("vit_mini_bf16_k512", "FedAvg", 512, VIT_MINI, seed=36)
 _add("ragged_f16_k3", "FedAvg", 3, [[k, s, F16] for k, s, _ in RAGGED_BF16], seed=40)
 _add("ragged_f64_k3", "FedAvg", 3, [[k, s, F64] for k, s, _ in RAGGED_BF16], seed=41)
 _add("mixed_dtypes_k4", "FedAvg", 4, [["w", [513], F32], ["h", [257], BF16], ["d", [33], F64],

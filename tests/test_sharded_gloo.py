@@ -310,3 +310,103 @@ def test_sharded_fedopt_steps_parameters_only(world, spec_name):
             else:
                 tol = 64 * 2.0 ** -24 * (e.abs() + 1e-3)
                 assert torch.all((v - e).abs() <= tol), (k, r, (v - e).abs().max())
+
+
+def _bf16_partial_reducer(rows, weights, out):
+    """fedagg_wsum_bf16_f32out restated: bf16 rows widened exactly, the fp32
+    chain fl32(acc + fl32(x_i * fl32(w_i))) in client order, NO final
+    rounding (the fp32 partial a rank sends into the reduce-scatter)."""
+    w32 = [np.float32(w) for w in weights]
+    x = [orc.bf16_bits_to_f32(rows[i].contiguous().view(torch.int16).numpy().view(np.uint16))
+         for i in range(rows.shape[0])]
+    acc = x[0] * w32[0]
+    for xi, wi in zip(x[1:], w32[1:]):
+        acc = acc + xi * wi
+    out.copy_(torch.from_numpy(np.asarray(acc, dtype=np.float32)))
+
+
+def _bf16_worker(rank, world, port, K_local, L, chunks, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        K = K_local * world
+        allrows = _clients(K, L).to(torch.bfloat16)
+        ns = [int(v) for v in np.random.default_rng(11).integers(100, 1001, K)]
+        ws = [n / sum(ns) for n in ns]
+        mine = allrows[rank * K_local:(rank + 1) * K_local].clone()
+        agg = ClientAxisAggregator(mine, L, chunks=chunks, reducer=_bf16_partial_reducer)
+        agg.aggregate(ws[rank * K_local:(rank + 1) * K_local])
+        full32 = agg.gather_full()
+        full16 = agg.gather_full(agg.shard_in_model_dtype())
+        assert full16.dtype == torch.bfloat16
+        q.put((rank, full32.numpy().copy(), full16.view(torch.int16).numpy().copy(), None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,K_local,L,chunks", [(2, 3, 4_099, 3), (4, 2, 1_031, 8), (4, 128, 4_099, 3)])
+def test_client_axis_bf16_rows(world, K_local, L, chunks):
+    """Config 4's multi-GPU path at world 2 and 4 (the last case is config
+    4's 512 clients over 4 ranks): bf16 rows -> per-rank fp32 partial
+    (fedagg_wsum_bf16_f32out) -> fp32 reduce-scatter -> ONE bf16 rounding per
+    element (shard_in_model_dtype).  Stated tolerances:
+
+    * vs the one-GPU fp32-accumulate result (fedagg_low_precision_acc="fp32",
+      orc.wsum_acc32): the fp32 sums differ by at most the reordering bound
+      T = 2(K + ceil(log2 G) + 1)·2^-24·Σ|fl(w_i p_i)|, and each side's
+      rounding to bf16 by half a bf16 ulp: |Δ| <= T + 2^-7·|acc32|;
+    * vs the exact sum (fp64): |Δ| <= T + 2^-8·|exact| + 2^-24·K·Σ|w_i p_i|;
+    * vs the reference's own bf16 chain (a bf16 rounding after every mul and
+      add, agg_operator.py:40-44): each bf16 rounding errs by at most
+      u = 2^-8 relative, so the chain is within 2^-8·(Σ_k |S_k| +
+      Σ_i |w_i p_i|) of the exact sum (S_k its running sums), and |Δ| <= that
+      + the exact-sum bound above."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bf16_worker, args=(r, world, port, K_local, L, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [e for *_, e in res if e]
+    assert not errs, "\n".join(errs)
+    K = K_local * world
+    allrows = _clients(K, L).to(torch.bfloat16)
+    ns = [int(v) for v in np.random.default_rng(11).integers(100, 1001, K)]
+    ws = [n / sum(ns) for n in ns]
+    x64 = np.stack([orc.bf16_bits_to_f32(allrows[i].view(torch.int16).numpy().view(np.uint16))
+                    for i in range(K)]).astype(np.float64)
+    w32 = np.array([np.float32(w) for w in ws], dtype=np.float64)
+    exact = (x64 * w32[:, None]).sum(0)
+    terms = np.abs(x64 * w32[:, None]).sum(0)
+    T = ClientAxisAggregator.tolerance(torch.from_numpy(terms), K, world).numpy()
+    acc32 = orc.bf16_bits_to_f32(orc.wsum_acc32([allrows[i] for i in range(K)], ws).view(torch.int16)
+                                 .numpy().view(np.uint16)).astype(np.float64)
+    ref = orc.bf16_bits_to_f32(orc.wsum([allrows[i] for i in range(K)], ws).view(torch.int16)
+                               .numpy().view(np.uint16)).astype(np.float64)
+    # the reference chain's running sums, for its own error bound
+    run = np.zeros(L)
+    s_abs = np.zeros(L)
+    for i in range(K):
+        run = run + x64[i] * w32[i]
+        s_abs += np.abs(run)
+    for rank, full32, full16, _ in res:
+        np.testing.assert_array_equal(full16, res[0][2])  # every rank gathers the same model
+        np.testing.assert_array_equal(full32.view(np.uint32), res[0][1].view(np.uint32))
+        # the bf16 shard is the RNE rounding of the fp32 shard
+        np.testing.assert_array_equal(full16.view(np.uint16), orc.f32_to_bf16_bits(full32))
+    got = orc.bf16_bits_to_f32(res[0][2].view(np.uint16)).astype(np.float64)
+    assert np.all(np.abs(got - acc32) <= T + 2.0 ** -7 * np.abs(acc32))
+    b_exact = T + 2.0 ** -8 * np.abs(exact) + 2.0 ** -24 * K * terms
+    assert np.all(np.abs(got - exact) <= b_exact)
+    assert np.all(np.abs(got - ref) <= b_exact + 2.0 ** -8 * (s_abs + terms))
+    if world == 2:  # two partials: the reduce-scatter sum is one fp32 rounding, then one bf16 rounding
+        parts = []
+        for r in range(world):
+            out = torch.empty(L)
+            _bf16_partial_reducer(allrows[r * K_local:(r + 1) * K_local], ws[r * K_local:(r + 1) * K_local], out)
+            parts.append(out.numpy())
+        np.testing.assert_array_equal(res[0][1].view(np.uint32), (parts[0] + parts[1]).view(np.uint32))
