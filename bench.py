@@ -54,8 +54,10 @@ from fedml_amd.sharded import ClientAxisAggregator  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# packed fp32 vector peak (v_pk_fma_f32: 256 CUs x 64 lanes x 2 x 2 flops x 2.4 GHz), the ceiling of
-# the Krum pair kernel, whose packed subtract + packed FMA are 3 flops per client pair and element
+# packed fp32 vector peak (v_pk_fma_f32: 64 FLOP/clk/SIMD x 1,024 SIMDs x 2.4 GHz), the ceiling of
+# the exact-difference Krum pair kernel, whose packed subtract + packed FMA are 3 flops per client pair and
+# element; the fp32 MFMA (v_mfma_f32_16x16x4_f32, the centred-Gram kernel) has the same 157.3 TF peak
+# (MI355X_MICROARCH.md, chip-level parameters)
 VALU_PEAK_TFLOPS = 157.3
 LSA_PRIME, LSA_QBITS = 2 ** 15 - 19, 10  # the reference's example LightSecAgg config (fedml_config.yaml:58-59)
 
@@ -95,6 +97,8 @@ def parse():
                          "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction; "
                          "krum / dist2 / clip = the distance defenses' kernels; rlr = the robust-learning-rate "
                          "defense's fused pass)")
+    ap.add_argument("--pair-distance", default="auto", choices=["auto", "gram", "exact"],
+                    help="--op krum: the centred fp32-MFMA Gram (K <= 128) or the exact-difference VALU kernel")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
     ap.add_argument("--clients", type=int, default=None,
@@ -372,8 +376,10 @@ def main():
         if a.op == "krum":
             chunks, n_chunks = dfn.weight_chunks(gd, nat.PAIR_CHUNK, dev)
             pd_out = torch.empty((K, K), dtype=torch.float64, device=dev)
-            work = dfn._work(nat.WORK_PAIRDIST2, K, n_chunks, dev)
-            call = lambda: nat.lib().fedagg_pairdist2_f32(  # noqa: E731
+            gram = a.pair_distance == "gram" or (a.pair_distance == "auto" and K <= dfn.GRAM_MAX_CLIENTS)
+            work = dfn._work(nat.WORK_PAIRGRAM if gram else nat.WORK_PAIRDIST2, K, n_chunks, dev)
+            pair_fn = nat.lib().fedagg_pairgram2_f32 if gram else nat.lib().fedagg_pairdist2_f32
+            call = lambda: pair_fn(  # noqa: E731
                 gd.d_ptrs.data_ptr(), K, chunks.data_ptr(), n_chunks, pd_out.data_ptr(), work.data_ptr(),
                 work.numel(), nat.stream_handle())
         elif a.op == "dist2":
@@ -391,10 +397,12 @@ def main():
                 gd.d_ptrs.data_ptr(), K, ref_row.data_ptr(), d_div.data_ptr(), gd.length, d_dst.data_ptr(),
                 nat.stream_handle())
         n_weight = sum(n for k, n in zip(gd.keys, gd.numels) if dfn.is_weight_param(k))
+        gram = a.op == "krum" and (a.pair_distance == "gram" or (a.pair_distance == "auto" and K <= 128))
         # krum: 3 flops (sub, mul, add) per client pair and weight element;
         # dist2: K rows + the reference row read once; clip: K rows in + K out + the reference row
-        dom_bytes = {"krum": 3 * K * (K - 1) // 2 * n_weight, "dist2": (K + 1) * n_weight * 4,
-                     "clip": (2 * K + 1) * gd.length * 4}[a.op]
+        # krum, gram: 2 flops (one FMA on the matrix cores) per client pair and weight element
+        dom_bytes = {"krum": (2 if a.op == "krum" and gram else 3) * K * (K - 1) // 2 * n_weight,
+                     "dist2": (K + 1) * n_weight * 4, "clip": (2 * K + 1) * gd.length * 4}[a.op]
 
         def step(ev=None, cev=None):
             if ev is not None:
@@ -496,6 +504,7 @@ def main():
             comm_ms = float(t[1].item()) / world
 
     ms_per_step = elapsed / a.steps * 1e3
+    gram_op = a.op == "krum" and (a.pair_distance == "gram" or (a.pair_distance == "auto" and K <= 128))
     value = K_total * n_elems / (elapsed / a.steps)
     variant = (a.fedopt or ("" if a.op == "fedavg" else a.op)) + (f"@K{K}" if a.clients is not None else "")
     traffic = load_traffic(a.config, mode, world, variant)
@@ -536,16 +545,19 @@ def main():
             "parallelism": parallelism,
         },
         "roofline": {
-            "bound": "valu" if a.op == "krum" else "hbm",
+            "bound": ("mfma" if gram_op else "valu") if a.op == "krum" else "hbm",
             "achieved": round(achieved / 1e3, 2) if a.op == "krum" else round(achieved, 1),
             "peak": VALU_PEAK_TFLOPS if a.op == "krum" else HBM_PEAK_GBPS,
             "unit": "TFLOP/s" if a.op == "krum" else "GB/s",
             "frac": round(achieved / 1e3 / VALU_PEAK_TFLOPS if a.op == "krum" else achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>",
-                        "krum": ("pairtri_kernel<16> + tri_finish_kernel" if K <= 64 else
-                                 "pairtri_kernel<32> + tri_finish_kernel" if K <= 128 else
-                                 "pairdist_kernel + pair_finish_kernel") + " (packed fp32)",
+                        "krum": ((f"pairgram_kernel<{4 if K <= 64 else 8}> + gram_sum_kernel + gram_dist_kernel "
+                                  "(fp32 MFMA 16x16x4, centred Gram)") if a.pair_distance == "gram" or
+                                 (a.pair_distance == "auto" and K <= 128) else
+                                 ("pairtri_kernel<16> + tri_finish_kernel" if K <= 64 else
+                                  "pairtri_kernel<32> + tri_finish_kernel" if K <= 128 else
+                                  "pairdist_kernel + pair_finish_kernel") + " (packed fp32)"),
                         "dist2": "dist2_kernel + sum_rows_kernel",
                         "clip": "clip_diff_kernel", "rlr": "reduce_kernel<OpF32Rlr, RlrEpi>"}[a.op]
                        if a.op in ("secagg", "lsa", "krum", "dist2", "clip", "rlr") else

@@ -25,7 +25,7 @@ FEDAGG_ACC_FP32 = 1
 
 DT_F32, DT_BF16, DT_F16, DT_F64, DT_I64, DT_I32 = 0, 1, 2, 3, 4, 5
 DIST_CHUNK, PAIR_CHUNK = 1024, 256  # FEDAGG_DIST_CHUNK / FEDAGG_PAIR_CHUNK
-WORK_DIST2, WORK_PAIRDIST2 = 0, 1
+WORK_DIST2, WORK_PAIRDIST2, WORK_PAIRGRAM = 0, 1, 2
 
 # Every symbol include/fedagg.h declares, with its ctypes signature.
 _P = ctypes.c_void_p
@@ -65,6 +65,7 @@ SIGNATURES = {
     "fedagg_robust_work_len": (_I64, [_I32, _I32, _I64]),
     "fedagg_dist2_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "fedagg_pairdist2_f32": (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P, _I64, _P]),
+    "fedagg_pairgram2_f32": (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P, _I64, _P]),
     "fedagg_clip_diff_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "fedagg_scale_diff_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "fedagg_last_error": (ctypes.c_char_p, []),

@@ -33,6 +33,16 @@
 
 #include "../../include/fedagg.h"
 
+#ifndef FEDAGG_CLIP_CLIENTS
+#define FEDAGG_CLIP_CLIENTS 2
+#endif
+#ifndef FEDAGG_DIST2_BATCH
+#define FEDAGG_DIST2_BATCH 32
+#endif
+#ifndef FEDAGG_DIST2_REF_NT
+#define FEDAGG_DIST2_REF_NT false
+#endif
+
 extern "C" int fedagg_set_error_internal(int code, const char* msg);
 
 namespace {
@@ -55,7 +65,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBS = 256;
 constexpr int kWaves = kBS / 64;
 constexpr int kLaneCols = FEDAGG_DIST_CHUNK / 64;  // columns per lane per chunk (kLaneCols / 4 f32x4)
-constexpr int kBatch = 16;                         // clients per wave per pass (kWaves * kBatch per block)
+// clients per wave per pass of dist2_kernel (kWaves * kBatch per block): 32
+// covers up to 128 clients in ONE pass, so the reference row is read once
+constexpr int kBatch = FEDAGG_DIST2_BATCH;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -67,20 +79,30 @@ __device__ __forceinline__ double wave_sum(double v) {
 // `p`: 16-byte loads where a whole f32x4 lies in the chunk and p is 16-byte
 // aligned (bucket rows and key offsets are), 4-byte loads otherwise; columns
 // past len read 0.
+// NT = false for a row every wave of the block reads (the reference row):
+// a plain load leaves it in L2 for the other three waves; non-temporal loads
+// made each wave fetch it from HBM again (dist2's traffic was 1.05x the
+// algorithmic bytes, ~7 extra reference rows per call at config 3)
+template <bool NT = true>
+__device__ __forceinline__ f32x4 ld4(const float* p) {
+  const auto q = reinterpret_cast<const f32x4 __attribute__((address_space(1)))*>(gptr(p));
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  return *q;
+}
+
+template <bool NT = true>
 __device__ __forceinline__ void load_chunk(const float* p, int len, int lane, f32x4 (&v)[kLaneCols / 4]) {
   const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   if (al && len == FEDAGG_DIST_CHUNK) {  // wave-uniform: a full aligned chunk, no per-lane conditions
 #pragma unroll
-    for (int u = 0; u < kLaneCols / 4; ++u)
-      v[u] = __builtin_nontemporal_load(
-          reinterpret_cast<const f32x4 __attribute__((address_space(1)))*>(gptr(p) + lane * 4 + 256 * u));
+    for (int u = 0; u < kLaneCols / 4; ++u) v[u] = ld4<NT>(p + lane * 4 + 256 * u);
     return;
   }
 #pragma unroll
   for (int u = 0; u < kLaneCols / 4; ++u) {
     const int c = lane * 4 + 256 * u;
     if (al && c + 4 <= len) {
-      v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 __attribute__((address_space(1)))*>(gptr(p) + c));
+      v[u] = ld4<NT>(p + c);
     } else {
       v[u].x = c < len ? gptr(p)[c] : 0.f;
       v[u].y = c + 1 < len ? gptr(p)[c + 1] : 0.f;
@@ -115,7 +137,7 @@ __global__ __launch_bounds__(kBS) void dist2_kernel(const float* const* __restri
       const int len = int(chunks[2 * c + 1]);
       f32x4 r[kLaneCols / 4];
       if (ref) {
-        load_chunk(ref + start, len, lane, r);
+        load_chunk<FEDAGG_DIST2_REF_NT>(ref + start, len, lane, r);
       } else {
 #pragma unroll
         for (int u = 0; u < kLaneCols / 4; ++u) r[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -147,13 +169,26 @@ __global__ __launch_bounds__(kBS) void dist2_kernel(const float* const* __restri
   }
 }
 
-// out[i] = sum over g of partial[i][g], in g order (deterministic)
-__global__ void sum_rows_kernel(const double* __restrict__ partial, int rows, int G, double* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows) return;
+// out[i] = sum over g of partial[i][g]: one block per row, thread t sums
+// g = t, t + 256, ... in order, then a fixed LDS tree (deterministic).  The
+// first version, one thread per row summing all G in sequence, was a chain of
+// G dependent loads: 0.218 ms per call at config 3 (G = 1,024), a tenth of
+// the whole dist2 call.
+__global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict__ partial, int G,
+                                                       double* __restrict__ out) {
+  __shared__ double red[256];
+  const int i = blockIdx.x, t = threadIdx.x;
+  const double* p = partial + int64_t(i) * G;
   double s = 0.0;
-  for (int g = 0; g < G; ++g) s += partial[int64_t(i) * G + g];
-  out[i] = s;
+  for (int g = t; g < G; g += 256) s += p[g];
+  red[t] = s;
+  __syncthreads();
+#pragma unroll
+  for (int m = 128; m > 0; m >>= 1) {
+    if (t < m) red[t] += red[t + m];
+    __syncthreads();
+  }
+  if (t == 0) out[i] = red[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -539,6 +574,253 @@ __global__ __launch_bounds__(256) void tri_finish_kernel(const double* __restric
 }
 
 // ---------------------------------------------------------------------------
+// Pairwise squared distances as a CENTRED Gram on fp32 MFMA (K <= 128).
+//
+// D_ij = sum_e (x_i[e] - x_j[e])^2 = sum_e (c_i[e] - c_j[e])^2 with c = x - r
+// for ANY per-column r, so D = G_ii + G_jj - 2 G_ij over the Gram G of the
+// centred rows: one FMA per client pair and column on the matrix cores
+// (v_mfma_f32_16x16x4_f32) instead of the exact-difference kernel's packed
+// subtract + packed FMA on the VALU.  Centring is what keeps the Gram form
+// accurate: honest clients are close to one another (base + small
+// updates), so uncentred |x|^2 would dwarf D and cancel.  Per 64-column stage
+// r is the column mean over the K clients, so |c|^2 is of the order of the
+// distances themselves.
+//
+// Layout: a block owns chunk groups g, g + G, ... (like pairtri_kernel); per
+// stage its 4 waves stage all NB*16 client rows of 64 columns into LDS
+// ([client][column], rows of kGramRS floats; lane = column, so every global
+// load is one coalesced 256-B row segment with a wave-uniform base) and
+// write per-wave column sums beside them.  After one barrier each wave
+// builds, for each of its tiles (a 16 x 16 block of the client-group
+// triangle, row-major, a wave owning a contiguous run of them), the A / B
+// fragments of the 16x16x4 MFMA: lane (i = l & 15, q = l >> 4) supplies
+// client 16a + i (A) / 16b + i (B) at columns 16q + m of MFMA m, centred by
+// the stage's column mean, so 16 MFMAs cover the stage.  Stage sums are fp32
+// (MFMA accumulation: an fmaf chain over 64 columns) and are added into fp64
+// per stage.  Partials go to the workspace [g][tile][16 x 16]; the finish
+// kernels sum them over g in a fixed order into the K x K Gram M (fp64) and
+// form D = max(0, M_ii + M_jj - 2 M_ij).
+//
+// Accuracy: each centred value is one fp32 rounding of x - r, each stage's
+// Gram entry an fp32 fmaf chain over 64 products (~1e-7 relative to
+// sum |c_i c_j|), so |D - D_exact| is ~1e-7 * (|c_i|^2 + |c_j|^2): the same
+// order as the reference's own fp32 torch.norm when the clients' spread is
+// of the order of their distances (tests/test_gpu_dist_defenses.py checks
+// the Krum selections and D against the exact-difference kernel).
+constexpr int kGramMax = 128;          // clients the Gram kernel holds (8 groups of 16)
+constexpr int kGramBS = 256;           // 4 waves: one per SIMD
+constexpr int kGramRS = kStage + 4;    // LDS row stride in floats
+constexpr int kGramBlocksPerCU = 2;    // 2 x (2 stage buffers of 128 rows) = 143 KB of LDS per CU
+
+__host__ __device__ inline int gram_groups(int K) { return (K + 15) / 16; }
+__host__ __device__ inline int gram_tiles(int K) {
+  const int nb = gram_groups(K);
+  return nb * (nb + 1) / 2;
+}
+
+// tile index -> (a, b), row-major over the upper triangle of nb x nb
+__device__ __forceinline__ int2 gram_tile(int t, int nb) {
+  int a = 0;
+  while (t >= nb - a) {
+    t -= nb - a;
+    ++a;
+  }
+  return int2{a, a + t};
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+template <int NB>
+__global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
+    const float* const* __restrict__ src, int K, const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
+    double* __restrict__ partial) {
+  constexpr int ROWS = NB * 16;
+  constexpr int TPW = (NB * (NB + 1) / 2 + 3) / 4;  // tiles per wave, at most
+  constexpr int RPW = ROWS / 4;                     // rows each wave stages
+  // the tiles of THIS K (the finish kernel and the workspace size use the
+  // same count): nb groups of 16 clients, NT tiles, TPWr per wave
+  const int nb = gram_groups(K), NT = nb * (nb + 1) / 2, TPWr = (NT + 3) / 4;
+  __shared__ float sX[2][ROWS * kGramRS];
+  __shared__ float sSum[2][4][kStage];
+  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int i16 = lane & 15, q = lane >> 4;
+  // staged rows: wave, wave + 4, ...; lane u holds row wave + 4u's pointer
+  // (a row past K points at row 0 and is zeroed by the mask) and each load
+  // takes it with two readlanes: 32 pointers kept in SGPRs spilled 131 of them
+  uint64_t my_row = 0;
+  {
+    const int cl = wave + 4 * (lane < RPW ? lane : 0);
+    my_row = reinterpret_cast<uint64_t>(src[cl < K ? cl : 0]);
+  }
+  const uint32_t row_lo = uint32_t(my_row), row_hi = uint32_t(my_row >> 32);
+  const int t0 = wave * TPWr;
+  const int nmine = NT - t0 < TPWr ? (NT - t0 > 0 ? NT - t0 : 0) : TPWr;
+  double acc64[TPW][4];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc64[j][r] = 0.0;
+  const float invK = 1.0f / float(K);
+  int64_t c = g;
+  int s0 = 0;
+  float v[RPW];
+  int w_next = 0;
+  auto fetch = [&]() {
+    if (c >= n_chunks) return false;
+    const int len = int(chunks[2 * c + 1]);
+    const int64_t col0 = chunks[2 * c] + s0;
+    w_next = len - s0 < kStage ? len - s0 : kStage;
+    const int cc = lane < w_next ? lane : 0;
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+      // readlane returns a signed int: widen each half through uint32_t, or a
+      // low half >= 2^31 sign-extends over the high half
+      const uint64_t p = uint64_t(uint32_t(__builtin_amdgcn_readlane(int(row_lo), u))) |
+                         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(row_hi), u))) << 32);
+      const float x = __builtin_nontemporal_load(gptr(reinterpret_cast<const float*>(p)) + col0 + cc);
+      const uint32_t m = (wave + 4 * u < K && lane < w_next) ? 0xffffffffu : 0u;  // a mask, not a branch
+      v[u] = __uint_as_float(__float_as_uint(x) & m);
+    }
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
+  auto stage_to = [&](int buf) {
+    float cs = 0.f;
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+      sX[buf][(wave + 4 * u) * kGramRS + lane] = v[u];
+      cs += v[u];
+    }
+    sSum[buf][wave][lane] = cs;
+  };
+  auto compute = [&](int buf) {
+    // the stage's column means for this lane's 16 columns (16q .. 16q + 15),
+    // the four waves' sums added in a fixed order; 0 past the stage's width
+    float r[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x4v s0v = *reinterpret_cast<const f32x4v*>(&sSum[buf][0][16 * q + 4 * k]);
+      const f32x4v s1v = *reinterpret_cast<const f32x4v*>(&sSum[buf][1][16 * q + 4 * k]);
+      const f32x4v s2v = *reinterpret_cast<const f32x4v*>(&sSum[buf][2][16 * q + 4 * k]);
+      const f32x4v s3v = *reinterpret_cast<const f32x4v*>(&sSum[buf][3][16 * q + 4 * k]);
+      const f32x4v m = ((s0v + s1v) + (s2v + s3v)) * invK;
+      r[4 * k] = m.x;
+      r[4 * k + 1] = m.y;
+      r[4 * k + 2] = m.z;
+      r[4 * k + 3] = m.w;
+    }
+    f32x4v acc[TPW];
+    float A[16], B[16];
+    int prev_a = -1;
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (j < nmine) {
+        const int2 ab = gram_tile(t0 + j, nb);
+        if (ab.x != prev_a) {
+          const float* pa = &sX[buf][(16 * ab.x + i16) * kGramRS + 16 * q];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const f32x4v x = *reinterpret_cast<const f32x4v*>(pa + 4 * k);
+            A[4 * k] = x.x - r[4 * k];
+            A[4 * k + 1] = x.y - r[4 * k + 1];
+            A[4 * k + 2] = x.z - r[4 * k + 2];
+            A[4 * k + 3] = x.w - r[4 * k + 3];
+          }
+          prev_a = ab.x;
+        }
+        const float* pb = &sX[buf][(16 * ab.y + i16) * kGramRS + 16 * q];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x4v x = *reinterpret_cast<const f32x4v*>(pb + 4 * k);
+          B[4 * k] = x.x - r[4 * k];
+          B[4 * k + 1] = x.y - r[4 * k + 1];
+          B[4 * k + 2] = x.z - r[4 * k + 2];
+          B[4 * k + 3] = x.w - r[4 * k + 3];
+        }
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[m], B[m], acc[j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      acc64[j][0] += double(acc[j].x);
+      acc64[j][1] += double(acc[j].y);
+      acc64[j][2] += double(acc[j].z);
+      acc64[j][3] += double(acc[j].w);
+    }
+  };
+  // stage s computes from buffer s & 1 while stage s + 1 is staged into the
+  // other and stage s + 2's loads are in flight: one barrier per stage
+  bool have = fetch();
+  if (have) {
+    stage_to(0);
+    have = fetch();
+    __syncthreads();
+    for (int buf = 0;; buf ^= 1) {
+      compute(buf);
+      if (!have) break;
+      stage_to(buf ^ 1);
+      have = fetch();
+      __syncthreads();
+    }
+  }
+  // C/D layout of the 16x16 MFMA: lane l holds row 4 * (l >> 4) + r, column l & 15
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    if (j < nmine) {
+      double* out = partial + (int64_t(g) * NT + t0 + j) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(4 * q + r) * 16 + i16] = acc64[j][r];
+    }
+  }
+}
+
+// M (K x K, fp64, both triangles) = the tiles' partials summed over the chunk
+// groups in four fixed-order quarters (as tri_finish_kernel)
+__global__ __launch_bounds__(256) void gram_sum_kernel(const double* __restrict__ partial, int G, int K,
+                                                       double* __restrict__ M) {
+  __shared__ double quarter[4][64];
+  const int nb = gram_groups(K), NT = nb * (nb + 1) / 2, E = NT * 256;
+  const int lane = threadIdx.x & 63, qq = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const int ec = e < E ? e : E - 1;
+  const double* p = partial + ec;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int gg = qq;
+  for (; gg + 28 < G; gg += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += p[int64_t(gg + 4 * u) * E];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (gg + 4 * u < G) s[u] += p[int64_t(gg + 4 * u) * E];
+  quarter[qq][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (qq != 0 || e >= E) return;
+  const double v = (quarter[0][lane] + quarter[1][lane]) + (quarter[2][lane] + quarter[3][lane]);
+  const int2 ab = gram_tile(e >> 8, nb);
+  const int row = 16 * ab.x + ((e >> 4) & 15), col = 16 * ab.y + (e & 15);
+  if (row >= K || col >= K) return;
+  M[int64_t(row) * K + col] = v;  // a diagonal tile writes both orders itself (the same fp32 chains)
+  if (ab.x != ab.y) M[int64_t(col) * K + row] = v;
+}
+
+// D[i][j] = max(0, M_ii + M_jj - 2 M_ij), 0 on the diagonal
+__global__ __launch_bounds__(256) void gram_dist_kernel(const double* __restrict__ M, int K, double* __restrict__ D) {
+  const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= int64_t(K) * K) return;
+  const int i = int(e / K), j = int(e % K);
+  const double d = (M[int64_t(i) * K + i] + M[int64_t(j) * K + j]) - 2.0 * M[e];
+  D[e] = i == j ? 0.0 : (d > 0.0 ? d : 0.0);
+}
+
+// ---------------------------------------------------------------------------
 // Clipped rebuild (norm_diff_clipping_defense.py:38-54): y = (x - r) / c + r
 // in fp32 with the reference's three roundings (c = fl32 of the clip divisor;
 // torch divides an fp32 tensor by a Python scalar in fp32).  Same shape as
@@ -555,7 +837,31 @@ __device__ __forceinline__ f32x4 clip4(f32x4 x, f32x4 r, float c, bool one) {
   return f32x4{d.x + r.x, d.y + r.y, d.z + r.z, d.w + r.w};
 }
 
+// one client's rebuilt chunk -> its destination row
 template <bool MUL>
+__device__ __forceinline__ void clip_store(float* y, const f32x4 (&x)[kLaneCols / 4], const f32x4 (&r)[kLaneCols / 4],
+                                           float c, int len, int lane) {
+  const bool one = c == 1.0f;
+  const bool al = (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+#pragma unroll
+  for (int u = 0; u < kLaneCols / 4; ++u) {
+    const int col = lane * 4 + 256 * u;
+    const f32x4 v = clip4<MUL>(x[u], r[u], c, one);
+    if (al && col + 4 <= len) {
+      __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(y + col));
+    } else {
+      if (col < len) y[col] = v.x;
+      if (col + 1 < len) y[col + 1] = v.y;
+      if (col + 2 < len) y[col + 2] = v.z;
+      if (col + 3 < len) y[col + 3] = v.w;
+    }
+  }
+}
+
+// CU clients per wave and step: all their loads are issued before the first
+// store, so a lane keeps CU * kLaneCols / 4 16-byte loads in flight (one
+// client at a time kept only 4, and stalled on every load before storing)
+template <bool MUL, int CU>
 __global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __restrict__ src, int K,
                                                         const float* __restrict__ ref, const float* __restrict__ div,
                                                         int64_t N, float* const* __restrict__ dst, int G) {
@@ -565,30 +871,25 @@ __global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __re
     const int64_t start = t * FEDAGG_DIST_CHUNK;
     const int len = int(N - start < FEDAGG_DIST_CHUNK ? N - start : FEDAGG_DIST_CHUNK);
     f32x4 r[kLaneCols / 4];
-    load_chunk(ref + start, len, lane, r);
-    for (int i = w; i < K; i += kWaves) {
-      const float c = div[i];
-      const bool one = c == 1.0f;
+    load_chunk<false>(ref + start, len, lane, r);
+    int i = w;
+    for (; i + kWaves * (CU - 1) < K; i += kWaves * CU) {
+      f32x4 x[CU][kLaneCols / 4];
+#pragma unroll
+      for (int j = 0; j < CU; ++j) load_chunk(src[i + kWaves * j] + start, len, lane, x[j]);
+#pragma unroll
+      for (int j = 0; j < CU; ++j)
+        clip_store<MUL>(dst[i + kWaves * j] + start, x[j], r, div[i + kWaves * j], len, lane);
+    }
+    for (; i < K; i += kWaves) {  // the last < CU clients of this wave
       f32x4 x[kLaneCols / 4];
       load_chunk(src[i] + start, len, lane, x);
-      float* y = dst[i] + start;
-      const bool al = (reinterpret_cast<uintptr_t>(y) & 15) == 0;
-#pragma unroll
-      for (int u = 0; u < kLaneCols / 4; ++u) {
-        const int col = lane * 4 + 256 * u;
-        const f32x4 v = clip4<MUL>(x[u], r[u], c, one);
-        if (al && col + 4 <= len) {
-          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(y + col));
-        } else {
-          if (col < len) y[col] = v.x;
-          if (col + 1 < len) y[col + 1] = v.y;
-          if (col + 2 < len) y[col + 2] = v.z;
-          if (col + 3 < len) y[col + 3] = v.w;
-        }
-      }
+      clip_store<MUL>(dst[i] + start, x, r, div[i], len, lane);
     }
   }
 }
+
+constexpr int kClipClients = FEDAGG_CLIP_CLIENTS;  // clients in flight per wave in clip_diff_kernel
 
 int grid_groups(int per_group_blocks, int64_t n_chunks, int64_t work_len, int64_t per_group_work) {
   int64_t G = (4096 + per_group_blocks - 1) / per_group_blocks;
@@ -607,8 +908,8 @@ int launch_diff(const char* what, const float* const* d_src, int32_t K, const fl
   if (!d_src || !d_ref || !d_c || !d_dst) return rset(FEDAGG_EINVAL, std::string(what) + ": null pointer");
   if (N == 0) return FEDAGG_OK;
   const int G = grid_groups(2, (N + FEDAGG_DIST_CHUNK - 1) / FEDAGG_DIST_CHUNK, 0, 0);
-  hipLaunchKernelGGL(clip_diff_kernel<MUL>, dim3(unsigned(G)), dim3(kBS), 0, static_cast<hipStream_t>(stream), d_src,
-                     K, d_ref, d_c, N, d_dst, G);
+  hipLaunchKernelGGL((clip_diff_kernel<MUL, kClipClients>), dim3(unsigned(G)), dim3(kBS), 0,
+                     static_cast<hipStream_t>(stream), d_src, K, d_ref, d_c, N, d_dst, G);
   return rcheck(what);
 }
 
@@ -623,6 +924,11 @@ int64_t fedagg_robust_work_len(int32_t kind, int32_t K, int64_t n_chunks) {
   // block streams its column ranges from start to end with no second round
   // of blocks (2,048: 2.31 ms at config 3, 1,024: 2.22 ms)
   if (kind == FEDAGG_WORK_DIST2) return int64_t(K) * grid_groups(4, n_chunks, 0, 0);
+  if (kind == FEDAGG_WORK_PAIRGRAM) {
+    if (K > kGramMax) return -1;
+    const int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, 0, 0);
+    return int64_t(G) * gram_tiles(K) * 256 + int64_t(K) * K;
+  }
   if (kind == FEDAGG_WORK_PAIRDIST2) {
     if (K <= kTriMax) return int64_t(16) * tri_blocks(K) * grid_groups(4, n_chunks, 0, 0);
     const int NT = pair_tiles(K);
@@ -645,7 +951,7 @@ int fedagg_dist2_f32(const float* const* d_src, int32_t K, const float* d_ref, c
   const int G = grid_groups(4, n_chunks, work_len, K);
   hipLaunchKernelGGL(dist2_kernel, dim3(unsigned(G)), dim3(kBS), 0, st, d_src, K, d_ref, d_chunks, n_chunks, G,
                      d_work);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(unsigned((K + 255) / 256)), dim3(256), 0, st, d_work, K, G, d_out);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(unsigned(K)), dim3(256), 0, st, d_work, G, d_out);
   return rcheck("fedagg_dist2_f32");
 }
 
@@ -681,6 +987,34 @@ int fedagg_pairdist2_f32(const float* const* d_src, int32_t K, const int64_t* d_
   hipLaunchKernelGGL(pair_finish_kernel, dim3(unsigned(kPT * kPT / 64), unsigned(NT)), dim3(256), 0, st, d_work, G,
                      K, d_out);
   return rcheck("fedagg_pairdist2_f32");
+}
+
+int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_chunks, int64_t n_chunks,
+                         double* d_out, double* d_work, int64_t work_len, fedagg_stream_t stream) {
+  if (K < 1 || K > kGramMax || n_chunks < 0)
+    return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: K must be in [1, 128] and n_chunks >= 0");
+  if (!d_src || !d_out || (n_chunks > 0 && (!d_chunks || !d_work)))
+    return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: null pointer");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_chunks == 0) {
+    if (hipMemsetAsync(d_out, 0, sizeof(double) * K * K, st) != hipSuccess) return rcheck("fedagg_pairgram2_f32");
+    return FEDAGG_OK;
+  }
+  const int64_t per = int64_t(gram_tiles(K)) * 256;
+  const int64_t mat = int64_t(K) * K;
+  if (work_len < per + mat)
+    return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: workspace too small (fedagg_robust_work_len)");
+  const int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, work_len - mat, per);
+  double* M = d_work + int64_t(G) * per;
+  if (K <= 64)
+    hipLaunchKernelGGL(pairgram_kernel<4>, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G,
+                       d_work);
+  else
+    hipLaunchKernelGGL(pairgram_kernel<8>, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G,
+                       d_work);
+  hipLaunchKernelGGL(gram_sum_kernel, dim3(unsigned((per + 63) / 64)), dim3(256), 0, st, d_work, G, K, M);
+  hipLaunchKernelGGL(gram_dist_kernel, dim3(unsigned((mat + 255) / 256)), dim3(256), 0, st, M, K, d_out);
+  return rcheck("fedagg_pairgram2_f32");
 }
 
 int fedagg_clip_diff_f32(const float* const* d_src, int32_t K, const float* d_ref, const float* d_div, int64_t N,

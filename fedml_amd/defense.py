@@ -217,13 +217,26 @@ def _work(kind: int, K: int, n_chunks: int, device) -> torch.Tensor:
     return torch.empty(max(n, 1), dtype=torch.float64, device=device)
 
 
-def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks: int, device) -> torch.Tensor:
+GRAM_MAX_CLIENTS = 128  # fedagg_pairgram2_f32 holds up to 128 clients
+
+
+def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks: int, device,
+                   method: str = "auto") -> torch.Tensor:
     """K x K fp64 squared distances of K fp32 device rows over the chunked
-    columns (fedagg_pairdist2_f32)."""
+    columns.  method "exact": the reference's fp32 differences, squared and
+    summed on the VALU (fedagg_pairdist2_f32); "gram": the centred Gram on the
+    fp32 matrix cores (fedagg_pairgram2_f32, K <= 128); "auto": gram when K
+    allows it (same Krum selections, ~3x faster at config 3)."""
+    if method not in ("auto", "gram", "exact"):
+        raise ValueError(f"pair distance method {method!r}: 'auto', 'gram' or 'exact'")
+    gram = method == "gram" or (method == "auto" and K <= GRAM_MAX_CLIENTS)
+    if gram and K > GRAM_MAX_CLIENTS:
+        raise ValueError(f"the Gram pair kernel holds at most {GRAM_MAX_CLIENTS} clients (K = {K})")
     out = torch.empty((K, K), dtype=torch.float64, device=device)
-    work = _work(nat.WORK_PAIRDIST2, K, n_chunks, device)
-    nat.check(nat.lib().fedagg_pairdist2_f32(d_ptrs.data_ptr(), K, chunks.data_ptr(), n_chunks, out.data_ptr(),
-                                             work.data_ptr(), work.numel(), nat.stream_handle()), "pairdist2")
+    work = _work(nat.WORK_PAIRGRAM if gram else nat.WORK_PAIRDIST2, K, n_chunks, device)
+    fn = nat.lib().fedagg_pairgram2_f32 if gram else nat.lib().fedagg_pairdist2_f32
+    nat.check(fn(d_ptrs.data_ptr(), K, chunks.data_ptr(), n_chunks, out.data_ptr(), work.data_ptr(), work.numel(),
+                 nat.stream_handle()), "pairgram2" if gram else "pairdist2")
     return out
 
 
@@ -282,9 +295,10 @@ def krum_scores(D: np.ndarray, byzantine_client_num: int) -> list:
 
 
 def krum_before_aggregation(raw_client_grad_list: Sequence, byzantine_client_num: int, krum_param_m: int = 1,
-                            device=None) -> list:
+                            device=None, method: str = "auto") -> list:
     """KrumDefense.defend_before_aggregation (krum_defense.py:28-45): the
-    krum_param_m lowest-scoring clients' original tuples, in score order."""
+    krum_param_m lowest-scoring clients' original tuples, in score order.
+    method: the pair-distance kernel (pairdist2_rows)."""
     num_client = len(raw_client_grad_list)
     if not 2 * byzantine_client_num + 2 <= num_client - krum_param_m:
         raise ValueError("byzantine_client_num conflicts with requirements in Krum: "
@@ -292,7 +306,7 @@ def krum_before_aggregation(raw_client_grad_list: Sequence, byzantine_client_num
     bucket, g, _, dev = _weight_bucket([item[1] for item in raw_client_grad_list], "krum", device)
     with torch.cuda.device(dev):
         chunks, n_chunks = weight_chunks(g, nat.PAIR_CHUNK, dev)
-        D = pairdist2_rows(g.d_ptrs, num_client, chunks, n_chunks, dev).cpu().numpy()
+        D = pairdist2_rows(g.d_ptrs, num_client, chunks, n_chunks, dev, method).cpu().numpy()
     scores = krum_scores(D, byzantine_client_num)
     score_index = torch.argsort(torch.Tensor(scores)).tolist()[0:krum_param_m]
     return [raw_client_grad_list[i] for i in score_index]

@@ -119,7 +119,8 @@ class ServerAggregator(ABC):
                 raw_client_model_or_grad_list, self.args.beta)
         elif dt in (dfn.DEFENSE_KRUM, dfn.DEFENSE_MULTIKRUM):
             raw_client_model_or_grad_list = dfn.krum_before_aggregation(
-                raw_client_model_or_grad_list, self.args.byzantine_client_num, dfn.krum_param_m(self.args), dev)
+                raw_client_model_or_grad_list, self.args.byzantine_client_num, dfn.krum_param_m(self.args), dev,
+                getattr(self.args, "fedagg_pair_distance", "auto"))
         elif dt == dfn.DEFENSE_NORM_DIFF_CLIPPING:
             # extra_auxiliary_info = the server's current model (server_aggregator.py:66-70)
             raw_client_model_or_grad_list = dfn.norm_diff_clipping_before_aggregation(

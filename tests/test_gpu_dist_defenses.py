@@ -42,15 +42,22 @@ def _to(raw, dev):
     return [(n, OrderedDict((k, t.to(dev)) for k, t in d.items())) for n, d in raw]
 
 
+@pytest.mark.parametrize("method", ["gram", "exact"])
 @pytest.mark.parametrize("device_inputs", [False, True])
 @pytest.mark.parametrize("name", KRUM)
-def test_krum_matches_reference(name, device_inputs, cuda_device):
+def test_krum_matches_reference(name, device_inputs, method, cuda_device):
+    """Both pair-distance kernels (the centred fp32-MFMA Gram, K <= 128, and
+    the exact-difference VALU kernel) select what the reference selects."""
     meta, arrays = gu.load(name)
     spec = meta["spec"]
+    if method == "gram" and spec["K"] > dfn.GRAM_MAX_CLIENTS:
+        pytest.skip("the Gram kernel holds at most 128 clients")
     raw, _ = cases.dist_inputs(spec)
     if device_inputs:
         raw = _to(raw, cuda_device)
-    agg = _Agg(cases.DefenseArgs(spec))
+    args = cases.DefenseArgs(spec)
+    args.fedagg_pair_distance = method
+    agg = _Agg(args)
     if meta["error"]:
         with pytest.raises(Exception) as ei:
             agg.on_before_aggregation(raw)
@@ -134,11 +141,62 @@ def test_pairdist2_vs_numpy(K, cuda_device):
     segs = [(0, 1), (3, 700), (704, 1), (960, 2500), (4000, 999)]  # ragged, partial stages
     chunks, n = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
     ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
-    D = dfn.pairdist2_rows(ptrs, K, chunks, n, cuda_device).cpu().numpy()
+    D = dfn.pairdist2_rows(ptrs, K, chunks, n, cuda_device, "exact").cpu().numpy()
     want = _np_pair(rows.cpu().numpy(), segs)
     np.testing.assert_allclose(D, want, rtol=1e-5)
     assert (np.diag(D) == 0).all()
     np.testing.assert_array_equal(D, D.T)
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 16, 17, 63, 64, 65, 100, 127, 128])
+def test_pairgram2_vs_numpy(K, cuda_device):
+    """The centred Gram: every pair within 2e-6 of the exact fp32-difference
+    distances relative to (|c_i|^2 + |c_j|^2) of the column-centred rows (and
+    so, for these rows, within 1e-5 of D itself), symmetric, 0 on the
+    diagonal, never negative."""
+    L = 5000
+    rows = _rows(K, L, cuda_device, 100 + K, outliers=[0] if K > 2 else [])
+    segs = [(0, 1), (3, 700), (704, 1), (960, 2500), (4000, 999)]  # ragged, partial stages
+    chunks, n = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    D = dfn.pairdist2_rows(ptrs, K, chunks, n, cuda_device, "gram").cpu().numpy()
+    want = _np_pair(rows.cpu().numpy(), segs)
+    cols = np.concatenate([np.arange(o, o + m) for o, m in segs])
+    X = rows.cpu().numpy()[:, cols].astype(np.float64)
+    C = X - X.mean(axis=0)[None, :]
+    nrm = (C * C).sum(axis=1)
+    scale = nrm[:, None] + nrm[None, :]
+    assert (np.abs(D - want) <= 2e-6 * scale + 1e-300).all(), np.abs(D - want).max()
+    np.testing.assert_allclose(D, want, rtol=1e-5)
+    assert (np.diag(D) == 0).all() and (D >= 0).all()
+    np.testing.assert_array_equal(D, D.T)
+
+
+def test_pairgram2_rejects_more_than_128_clients(cuda_device):
+    rows = _rows(129, 64, cuda_device, 1)
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(129)], cuda_device)
+    chunks, n = _chunks([(0, 64)], nat.PAIR_CHUNK, cuda_device)
+    with pytest.raises(ValueError):
+        dfn.pairdist2_rows(ptrs, 129, chunks, n, cuda_device, "gram")
+    assert nat.lib().fedagg_robust_work_len(nat.WORK_PAIRGRAM, 129, 1) == -1
+
+
+def test_full_size_gram_agrees_with_exact(cuda_device):
+    """Config 3's size (128 clients x 25.6M columns, two outliers): the Gram
+    matrix within 2e-6 relative of the exact-difference kernel's, and Krum's
+    scores order the clients the same way."""
+    K, L = 128, 25_610_240
+    rows = _rows(K, L, cuda_device, 3, outliers=[5, 77])
+    segs = [(0, 25_610_152)]
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    ch_p, n_p = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
+    Dg = dfn.pairdist2_rows(ptrs, K, ch_p, n_p, cuda_device, "gram").cpu().numpy()
+    De = dfn.pairdist2_rows(ptrs, K, ch_p, n_p, cuda_device, "exact").cpu().numpy()
+    np.testing.assert_allclose(Dg, De, rtol=2e-6)
+    sg, se = dfn.krum_scores(Dg, 10), dfn.krum_scores(De, 10)
+    og = torch.argsort(torch.Tensor(sg)).tolist()
+    oe = torch.argsort(torch.Tensor(se)).tolist()
+    assert og[:32] == oe[:32] and 5 not in og[:5] and 77 not in og[:5]
 
 
 @pytest.mark.parametrize("with_ref", [False, True])
@@ -162,7 +220,8 @@ def test_empty_chunk_table(cuda_device):
     rows = _rows(3, 64, cuda_device, 1)
     ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(3)], cuda_device)
     empty = torch.zeros(2, dtype=torch.int64, device=cuda_device)
-    assert (dfn.pairdist2_rows(ptrs, 3, empty, 0, cuda_device) == 0).all()
+    assert (dfn.pairdist2_rows(ptrs, 3, empty, 0, cuda_device, "exact") == 0).all()
+    assert (dfn.pairdist2_rows(ptrs, 3, empty, 0, cuda_device, "gram") == 0).all()
     assert (dfn.dist2_rows(ptrs, 3, None, empty, 0, cuda_device) == 0).all()
 
 
@@ -174,7 +233,7 @@ def test_full_size_pairdist_agrees_with_dist2(cuda_device):
     segs = [(0, 25_610_152)]
     ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
     ch_p, n_p = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
-    D = dfn.pairdist2_rows(ptrs, K, ch_p, n_p, cuda_device).cpu().numpy()
+    D = dfn.pairdist2_rows(ptrs, K, ch_p, n_p, cuda_device, "exact").cpu().numpy()
     ch_d, n_d = _chunks(segs, nat.DIST_CHUNK, cuda_device)
     for j in (0, 5, 64, 127):
         col = dfn.dist2_rows(ptrs, K, rows[j], ch_d, n_d, cuda_device).cpu().numpy()
