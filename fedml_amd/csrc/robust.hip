@@ -37,7 +37,7 @@
 #define FEDAGG_CLIP_CLIENTS 2
 #endif
 #ifndef FEDAGG_DIST2_BATCH
-#define FEDAGG_DIST2_BATCH 32
+#define FEDAGG_DIST2_BATCH 16
 #endif
 #ifndef FEDAGG_DIST2_REF_NT
 #define FEDAGG_DIST2_REF_NT false
@@ -65,9 +65,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBS = 256;
 constexpr int kWaves = kBS / 64;
 constexpr int kLaneCols = FEDAGG_DIST_CHUNK / 64;  // columns per lane per chunk (kLaneCols / 4 f32x4)
-// clients per wave per pass of dist2_kernel (kWaves * kBatch per block): 32
-// covers up to 128 clients in ONE pass, so the reference row is read once
+// clients per wave per pass of dist2_kernel (kWaves * kBatch per block).  32
+// would cover 128 clients in one pass but costs the occupancy: 2.61 vs 1.99 ms
+// at config 3 (tools/robust_variants.py, profiles/r03/dist/); with the
+// reference row cached in L2 (ld4<false>) the second pass's re-read is cheap
 constexpr int kBatch = FEDAGG_DIST2_BATCH;
+
+// A workgroup barrier that waits for this wave's LDS operations only.
+// __syncthreads() carries a release fence that waits for EVERY outstanding
+// memory operation (s_waitcnt vmcnt(0) lgkmcnt(0) before s_barrier), so the
+// next stage's global loads, issued just before it, were drained at every
+// barrier instead of overlapping the stage's compute.  The "memory" clobber
+// keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -242,19 +252,27 @@ __device__ __forceinline__ void stage_load(f32x4 (&v)[4], const SideRows& rows, 
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float x = __builtin_nontemporal_load(gptr(rows.p[q][k]) + col0 + c);
-      // a mask, not a select: a select on the uniform `live` became a branch
-      // around each load with a full vmcnt(0) wait at every join
-      const uint32_t m = (rows.live[q][k] && lane < w) ? 0xffffffffu : 0u;
-      v[q][k] = __uint_as_float(__float_as_uint(x) & m);
-    }
+    for (int k = 0; k < 4; ++k) v[q][k] = __builtin_nontemporal_load(gptr(rows.p[q][k]) + col0 + c);
 }
 
-__device__ __forceinline__ void stage_store(f32x4* __restrict__ s, const f32x4 (&v)[4], int t) {
+// the staged values, zeroed past column w and past K: a mask applied here,
+// when the stage is written to LDS, not right after the loads, so nothing
+// consumes them early and they stay in flight through the current stage's
+// compute (a select on the uniform `live` had become a branch around each
+// load with a full vmcnt(0) wait at every join)
+__device__ __forceinline__ void stage_store(f32x4* __restrict__ s, const f32x4 (&v)[4], const SideRows& rows, int w,
+                                            int t) {
   const int lane = t & 63, wave = t >> 6;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) s[swz(lane, wave * 4 + q) >> 2] = v[q];
+  for (int q = 0; q < 4; ++q) {
+    f32x4 x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t m = (rows.live[q][k] && lane < w) ? 0xffffffffu : 0u;
+      x[k] = __uint_as_float(__float_as_uint(v[q][k]) & m);
+    }
+    s[swz(lane, wave * 4 + q) >> 2] = x;
+  }
 }
 
 // one column of the thread's 4 x 4 pair block: acc[2k + h] holds pairs
@@ -343,11 +361,11 @@ __global__ __launch_bounds__(kBS) void pairdist_kernel(const float* const* __res
   bool have = fetch();
   while (have) {
     const int w = w_next;
-    __syncthreads();  // the previous stage's LDS reads are done
-    stage_store(sA, va, t);
-    if (!diag) stage_store(sB, vb, t);
+    lds_barrier();  // the previous stage's LDS reads are done
+    stage_store(sA, va, rowsA, w, t);
+    if (!diag) stage_store(sB, vb, rowsB, w, t);
     have = fetch();  // next stage's loads in flight during this stage's compute
-    __syncthreads();
+    lds_barrier();
     f32x2 acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = f32x2{0.f, 0.f};
@@ -487,11 +505,7 @@ __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __r
 #pragma unroll
     for (int q = 0; q < kTriLoads; ++q)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float x = __builtin_nontemporal_load(gptr(rp[q][k]) + col0 + cc);
-        const uint32_t m = (live[q][k] && lane < w_next) ? 0xffffffffu : 0u;  // a mask, not a branch
-        v[q][k] = __uint_as_float(__float_as_uint(x) & m);
-      }
+      for (int k = 0; k < 4; ++k) v[q][k] = __builtin_nontemporal_load(gptr(rp[q][k]) + col0 + cc);
     s0 += kStage;
     if (s0 >= len) {
       s0 = 0;
@@ -499,10 +513,20 @@ __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __r
     }
     return true;
   };
-  auto stage_to = [&](f32x4* buf) {  // the staged registers -> a stage buffer
+  // the staged registers -> a stage buffer, zeroed past the stage's width w
+  // and past K here (not in fetch: the loads stay in flight until now)
+  auto stage_to = [&](f32x4* buf, int w) {
 #pragma unroll
     for (int q = 0; q < kTriLoads; ++q)
-      if (wave + W * q < nb) buf[tri_swz<NBMAX>(lane, wave + W * q) >> 2] = v[q];
+      if (wave + W * q < nb) {
+        f32x4 x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t m = (live[q][k] && lane < w) ? 0xffffffffu : 0u;
+          x[k] = __uint_as_float(__float_as_uint(v[q][k]) & m);
+        }
+        buf[tri_swz<NBMAX>(lane, wave + W * q) >> 2] = x;
+      }
   };
   // Stage s computes from buffer s & 1 while stage s + 1 is written into the
   // other one and stage s + 2's loads are in flight: one barrier per stage.
@@ -510,9 +534,9 @@ __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __r
   bool have = fetch();
   if (have) {
     int w = w_next;
-    stage_to(sX[0]);
+    stage_to(sX[0], w);
     have = fetch();
-    __syncthreads();
+    lds_barrier();
     for (int buf = 0;; buf ^= 1) {
       if (active) {
         f32x2 acc[8];
@@ -528,9 +552,9 @@ __global__ __launch_bounds__(kTriBS) void pairtri_kernel(const float* const* __r
       }
       if (!have) break;
       const int wn = w_next;
-      stage_to(sX[buf ^ 1]);
+      stage_to(sX[buf ^ 1], wn);
       have = fetch();
-      __syncthreads();
+      lds_barrier();
       w = wn;
     }
   }
@@ -636,7 +660,7 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
     double* __restrict__ partial) {
   constexpr int ROWS = NB * 16;
   constexpr int TPW = (NB * (NB + 1) / 2 + 3) / 4;  // tiles per wave, at most
-  constexpr int RPW = ROWS / 4;                     // rows each wave stages
+  constexpr int LPW = ROWS / 16;                    // 16-byte loads per lane and stage (4 rows per wave-load)
   // the tiles of THIS K (the finish kernel and the workspace size use the
   // same count): nb groups of 16 clients, NT tiles, TPWr per wave
   const int nb = gram_groups(K), NT = nb * (nb + 1) / 2, TPWr = (NT + 3) / 4;
@@ -645,15 +669,18 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
   const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int i16 = lane & 15, q = lane >> 4;
-  // staged rows: wave, wave + 4, ...; lane u holds row wave + 4u's pointer
-  // (a row past K points at row 0 and is zeroed by the mask) and each load
-  // takes it with two readlanes: 32 pointers kept in SGPRs spilled 131 of them
-  uint64_t my_row = 0;
-  {
-    const int cl = wave + 4 * (lane < RPW ? lane : 0);
-    my_row = reinterpret_cast<uint64_t>(src[cl < K ? cl : 0]);
+  // Staging: wave w owns rows w * ROWS/4 .. + ROWS/4; each wave-load covers 4
+  // rows (lane group q) x 64 columns (lane i16: columns 4 i16 .. 4 i16 + 3)
+  // with 16-byte loads, so every lane addresses its own row (VGPR pointers:
+  // one pointer per row in SGPRs spilled and serialized the loads).
+  const float* rowp[LPW];
+  bool rlive[LPW];
+#pragma unroll
+  for (int u = 0; u < LPW; ++u) {
+    const int cl = wave * (ROWS / 4) + 4 * u + q;
+    rlive[u] = cl < K;
+    rowp[u] = src[cl < K ? cl : 0];
   }
-  const uint32_t row_lo = uint32_t(my_row), row_hi = uint32_t(my_row >> 32);
   const int t0 = wave * TPWr;
   const int nmine = NT - t0 < TPWr ? (NT - t0 > 0 ? NT - t0 : 0) : TPWr;
   double acc64[TPW][4];
@@ -664,23 +691,29 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
   const float invK = 1.0f / float(K);
   int64_t c = g;
   int s0 = 0;
-  float v[RPW];
+  f32x4 v[LPW];
   int w_next = 0;
   auto fetch = [&]() {
     if (c >= n_chunks) return false;
     const int len = int(chunks[2 * c + 1]);
     const int64_t col0 = chunks[2 * c] + s0;
     w_next = len - s0 < kStage ? len - s0 : kStage;
-    const int cc = lane < w_next ? lane : 0;
+    const int c4 = 4 * i16;
+    if (w_next == kStage) {  // wave-uniform: a full stage, one unconditional 16-byte load per row
+      // raw values: the rows past K are zeroed in stage_to, so nothing here
+      // consumes the loads and they stay in flight through the next compute
 #pragma unroll
-    for (int u = 0; u < RPW; ++u) {
-      // readlane returns a signed int: widen each half through uint32_t, or a
-      // low half >= 2^31 sign-extends over the high half
-      const uint64_t p = uint64_t(uint32_t(__builtin_amdgcn_readlane(int(row_lo), u))) |
-                         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(row_hi), u))) << 32);
-      const float x = __builtin_nontemporal_load(gptr(reinterpret_cast<const float*>(p)) + col0 + cc);
-      const uint32_t m = (wave + 4 * u < K && lane < w_next) ? 0xffffffffu : 0u;  // a mask, not a branch
-      v[u] = __uint_as_float(__float_as_uint(x) & m);
+      for (int u = 0; u < LPW; ++u) v[u] = ld4<true>(rowp[u] + col0 + c4);
+    } else {  // the ragged end of a chunk: element loads, never past column w
+#pragma unroll
+      for (int u = 0; u < LPW; ++u) {
+        const float* p = rowp[u] + col0;
+        const bool ok = rlive[u];
+        v[u].x = ok && c4 < w_next ? p[c4] : 0.f;
+        v[u].y = ok && c4 + 1 < w_next ? p[c4 + 1] : 0.f;
+        v[u].z = ok && c4 + 2 < w_next ? p[c4 + 2] : 0.f;
+        v[u].w = ok && c4 + 3 < w_next ? p[c4 + 3] : 0.f;
+      }
     }
     s0 += kStage;
     if (s0 >= len) {
@@ -689,62 +722,82 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
     }
     return true;
   };
-  auto stage_to = [&](int buf) {
-    float cs = 0.f;
-#pragma unroll
-    for (int u = 0; u < RPW; ++u) {
-      sX[buf][(wave + 4 * u) * kGramRS + lane] = v[u];
-      cs += v[u];
-    }
-    sSum[buf][wave][lane] = cs;
+  // Staging, in two halves around a barrier: stage_sums publishes this
+  // wave's column sums of the loaded rows (still in registers), and once
+  // every wave's sums are in, stage_centred writes the rows minus the column
+  // mean (the fragments then need no centring: no means held in registers
+  // and no subtracts in the MFMA loop).
+  auto masked = [&](int u) {
+    const uint32_t m = rlive[u] ? 0xffffffffu : 0u;  // a row past K (it loaded row 0)
+    return f32x4{__uint_as_float(__float_as_uint(v[u].x) & m), __uint_as_float(__float_as_uint(v[u].y) & m),
+                 __uint_as_float(__float_as_uint(v[u].z) & m), __uint_as_float(__float_as_uint(v[u].w) & m)};
   };
-  auto compute = [&](int buf) {
-    // the stage's column means for this lane's 16 columns (16q .. 16q + 15),
-    // the four waves' sums added in a fixed order; 0 past the stage's width
-    float r[16];
+  auto stage_sums = [&](int buf) {
+    f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < LPW; ++u) cs += masked(u);
+    // the wave's column sums: add the four lane groups (xor 16, xor 32)
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      cs.x += __shfl_xor(cs.x, m, 64);
+      cs.y += __shfl_xor(cs.y, m, 64);
+      cs.z += __shfl_xor(cs.z, m, 64);
+      cs.w += __shfl_xor(cs.w, m, 64);
+    }
+    if (q == 0) *reinterpret_cast<f32x4*>(&sSum[buf][wave][4 * i16]) = cs;
+  };
+  auto stage_centred = [&](int buf) {
+    // this lane's 4 columns' means, the four waves' sums in a fixed order;
+    // 0 past the stage's width (every row is 0 there)
+    const f32x4 s0v = *reinterpret_cast<const f32x4*>(&sSum[buf][0][4 * i16]);
+    const f32x4 s1v = *reinterpret_cast<const f32x4*>(&sSum[buf][1][4 * i16]);
+    const f32x4 s2v = *reinterpret_cast<const f32x4*>(&sSum[buf][2][4 * i16]);
+    const f32x4 s3v = *reinterpret_cast<const f32x4*>(&sSum[buf][3][4 * i16]);
+    const f32x4 r = ((s0v + s1v) + (s2v + s3v)) * invK;
+#pragma unroll
+    for (int u = 0; u < LPW; ++u)
+      *reinterpret_cast<f32x4*>(&sX[buf][(wave * (ROWS / 4) + 4 * u + q) * kGramRS + 4 * i16]) = masked(u) - r;
+  };
+  auto frag = [&](int buf, int grp, float (&F)[16]) {
+    const float* p = &sX[buf][(16 * grp + i16) * kGramRS + 16 * q];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const f32x4v s0v = *reinterpret_cast<const f32x4v*>(&sSum[buf][0][16 * q + 4 * k]);
-      const f32x4v s1v = *reinterpret_cast<const f32x4v*>(&sSum[buf][1][16 * q + 4 * k]);
-      const f32x4v s2v = *reinterpret_cast<const f32x4v*>(&sSum[buf][2][16 * q + 4 * k]);
-      const f32x4v s3v = *reinterpret_cast<const f32x4v*>(&sSum[buf][3][16 * q + 4 * k]);
-      const f32x4v m = ((s0v + s1v) + (s2v + s3v)) * invK;
-      r[4 * k] = m.x;
-      r[4 * k + 1] = m.y;
-      r[4 * k + 2] = m.z;
-      r[4 * k + 3] = m.w;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(p + 4 * k);
+      F[4 * k] = x.x;
+      F[4 * k + 1] = x.y;
+      F[4 * k + 2] = x.z;
+      F[4 * k + 3] = x.w;
     }
+  };
+  auto compute = [&](int buf) {
+    // tiles two at a time, their MFMAs interleaved: two independent
+    // accumulation chains hide the 16x16x4 MFMA's dependent latency (40
+    // cycles against a 32-cycle issue; one chain at a time left the waves
+    // issue-stalled 42 % of their cycles, SQ_WAIT_INST_ANY)
     f32x4v acc[TPW];
-    float A[16], B[16];
-    int prev_a = -1;
+    float A0[16], B0[16], A1[16], B1[16];
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) {
+    for (int j = 0; j < TPW; j += 2) {
       acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (j + 1 < TPW) acc[j + 1] = f32x4v{0.f, 0.f, 0.f, 0.f};
       if (j < nmine) {
-        const int2 ab = gram_tile(t0 + j, nb);
-        if (ab.x != prev_a) {
-          const float* pa = &sX[buf][(16 * ab.x + i16) * kGramRS + 16 * q];
+        const int2 ab0 = gram_tile(t0 + j, nb);
+        const bool two = j + 1 < TPW && j + 1 < nmine;
+        const int2 ab1 = two ? gram_tile(t0 + j + 1, nb) : ab0;
+        frag(buf, ab0.x, A0);
+        frag(buf, ab0.y, B0);
+        frag(buf, ab1.x, A1);
+        frag(buf, ab1.y, B1);
+        if (two) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const f32x4v x = *reinterpret_cast<const f32x4v*>(pa + 4 * k);
-            A[4 * k] = x.x - r[4 * k];
-            A[4 * k + 1] = x.y - r[4 * k + 1];
-            A[4 * k + 2] = x.z - r[4 * k + 2];
-            A[4 * k + 3] = x.w - r[4 * k + 3];
+          for (int m = 0; m < 16; ++m) {
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[m], B0[m], acc[j], 0, 0, 0);
+            acc[j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[m], B1[m], acc[j + 1], 0, 0, 0);
           }
-          prev_a = ab.x;
-        }
-        const float* pb = &sX[buf][(16 * ab.y + i16) * kGramRS + 16 * q];
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const f32x4v x = *reinterpret_cast<const f32x4v*>(pb + 4 * k);
-          B[4 * k] = x.x - r[4 * k];
-          B[4 * k + 1] = x.y - r[4 * k + 1];
-          B[4 * k + 2] = x.z - r[4 * k + 2];
-          B[4 * k + 3] = x.w - r[4 * k + 3];
+          for (int m = 0; m < 16; ++m) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[m], B0[m], acc[j], 0, 0, 0);
         }
-#pragma unroll
-        for (int m = 0; m < 16; ++m) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[m], B[m], acc[j], 0, 0, 0);
       }
     }
 #pragma unroll
@@ -756,18 +809,23 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
     }
   };
   // stage s computes from buffer s & 1 while stage s + 1 is staged into the
-  // other and stage s + 2's loads are in flight: one barrier per stage
+  // other (sums, barrier, centred rows) and stage s + 2's loads are in
+  // flight: two barriers per stage
   bool have = fetch();
   if (have) {
-    stage_to(0);
+    stage_sums(0);
+    lds_barrier();
+    stage_centred(0);
     have = fetch();
-    __syncthreads();
+    lds_barrier();
     for (int buf = 0;; buf ^= 1) {
       compute(buf);
       if (!have) break;
-      stage_to(buf ^ 1);
+      stage_sums(buf ^ 1);
+      lds_barrier();
+      stage_centred(buf ^ 1);
       have = fetch();
-      __syncthreads();
+      lds_barrier();
     }
   }
   // C/D layout of the 16x16 MFMA: lane l holds row 4 * (l >> 4) + r, column l & 15

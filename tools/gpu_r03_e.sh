@@ -2,7 +2,7 @@
 # Round 3: the centred-Gram Krum kernel (parity + speed), the dist2 reference
 # row fix (A/B builds + PMC), rocprofv3 of the shipped krum / dist2.
 set -o pipefail
-O=gpurun_out/r03/gram
+O=gpurun_out/r03/gram3
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 run() { echo "== $*" >&2; "$@"; }

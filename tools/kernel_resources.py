@@ -67,7 +67,7 @@ def kernels(co: bytes):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r02", "kernel_resources.tsv")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r03", "kernel_resources.tsv")
     ks = sorted(kernels(code_object()), key=lambda k: k["kernel"])
     cols = ["kernel", "vgpr_count", "agpr_count", "occupancy", "sgpr_count", "vgpr_spill_count",
             "sgpr_spill_count", "private_segment_fixed_size", "group_segment_fixed_size"]
@@ -76,9 +76,13 @@ def main():
         for k in ks:
             f.write("\t".join(str(k[c]) for c in cols) + "\n")
     scratch = [k for k in ks if int(k["private_segment_fixed_size"] or 0) or int(k["vgpr_spill_count"] or 0)]
-    print(f"{len(ks)} kernels, {len(scratch)} with scratch or spills -> {out}")
+    sgpr = [k for k in ks if int(k["sgpr_spill_count"] or 0)]
+    print(f"{len(ks)} kernels, {len(scratch)} with scratch or VGPR spills, {len(sgpr)} with SGPR spills "
+          f"(SGPR spills go to VGPR lanes, not memory) -> {out}")
     for k in scratch:
         print(f"  {k['kernel']}: scratch {k['private_segment_fixed_size']} B/lane, {k['vgpr_spill_count']} VGPR spills")
+    for k in sgpr:
+        print(f"  {k['kernel']}: {k['sgpr_spill_count']} SGPR spills, {k['vgpr_count']} VGPRs")
 
 
 if __name__ == "__main__":

@@ -22,8 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_build")
 VARIANTS = {"clip1": ["-DFEDAGG_CLIP_CLIENTS=1"], "clip4": ["-DFEDAGG_CLIP_CLIENTS=4"],
-            "d16nt": ["-DFEDAGG_DIST2_BATCH=16", "-DFEDAGG_DIST2_REF_NT=true"],
-            "d16": ["-DFEDAGG_DIST2_BATCH=16"], "d32nt": ["-DFEDAGG_DIST2_REF_NT=true"]}
+            "d16nt": ["-DFEDAGG_DIST2_REF_NT=true"], "d32": ["-DFEDAGG_DIST2_BATCH=32"]}
 STUB = 'extern "C" int fedagg_set_error_internal(int code, const char*) { return code; }\n'
 
 
