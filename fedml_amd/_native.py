@@ -73,6 +73,9 @@ SIGNATURES = {
     "fedagg_wsum_f32_variant": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _I32, _P]),
     "fedagg_variant_name": (ctypes.c_char_p, [_I32]),
     "fedagg_num_variants": (_I32, []),
+    "fedagg_wsum_tiny_variant": (ctypes.c_int, [_I32, _P, _P, _I32, _I64, _P, _I32, _P]),
+    "fedagg_tiny_variant_name": (ctypes.c_char_p, [_I32]),
+    "fedagg_num_tiny_variants": (_I32, []),
 }
 
 

@@ -805,6 +805,88 @@ __global__ __launch_bounds__(BS) void reduce_multi_kernel(
   reduce_block<OP, U, V, NT, true, BS>(s, epi, w, K, (b - block_begin[lo]) * BS * V);
 }
 
+// Many clients over a small tensor (cross-device FedAvg: 1,000 clients x a
+// 62K-element CNN): the element axis is all the parallelism there is (each
+// element's client chain is sequential for bit-exactness), so a lane owns EL
+// elements (a 2-, 4- or 8-byte pack, not 16) — up to 8x the lanes of the
+// 16-byte tiles for 16-bit rows — and keeps U clients' loads in flight.  The
+// wave then walks its chain in K/U memory round trips.
+template <int B>
+struct RawOf;
+template <> struct RawOf<2> { using T = uint16_t; };
+template <> struct RawOf<4> { using T = uint32_t; };
+template <> struct RawOf<8> { using T = u32x2; };
+template <> struct RawOf<16> { using T = u32x4; };
+
+template <class OP, int U, int EL, bool ALIGNED, int BS, class WS>
+__global__ __launch_bounds__(BS) void reduce_narrow_kernel(Seg<OP> s, StoreEpi<OP> epi, WS w, int K) {
+  using in_t = typename OP::in_t;
+  using raw_t = typename RawOf<EL * sizeof(in_t)>::T;
+  const int64_t e0 = (int64_t(blockIdx.x) * BS + threadIdx.x) * EL;
+  if (e0 >= s.numel) return;
+  if (!ALIGNED || e0 + EL > s.numel) {
+    reduce_edge<OP, EL, 1>(s, epi, w, K, e0, s.numel < e0 + EL ? s.numel : e0 + EL);
+    return;
+  }
+  auto ld = [&](int c) {
+    const raw_t r = __builtin_nontemporal_load(reinterpret_cast<const raw_t __attribute__((address_space(1)))*>(
+        as_global(s.src[c]) + e0));
+    Pack<in_t, EL> x;
+    __builtin_memcpy(&x, &r, sizeof(r));
+    return x;
+  };
+  typename OP::acc_t acc[EL];
+  {
+    const auto x = ld(0);
+    const auto w0 = w[0];
+#pragma unroll
+    for (int j = 0; j < EL; ++j) acc[j] = OP::first(x.v[j], w0);
+  }
+  int c = 1;
+  for (; c + U <= K; c += U) {
+    Pack<in_t, EL> x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ld(c + u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const auto wu = w[c + u];
+#pragma unroll
+      for (int j = 0; j < EL; ++j) acc[j] = OP::step(acc[j], x[u].v[j], wu);
+    }
+  }
+  if (c < K) {  // fewer than U clients left (wave-uniform): every load before the first add
+    Pack<in_t, EL> x[U - 1];
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      if (c + u < K) x[u] = ld(c + u);
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      if (c + u < K) {
+        const auto wu = w[c + u];
+#pragma unroll
+        for (int j = 0; j < EL; ++j) acc[j] = OP::step(acc[j], x[u].v[j], wu);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < EL; ++j) epi.one(e0 + j, acc[j]);
+}
+
+template <class OP, int U, int EL, int BS = 64, class WS = PtrW<typename OP::w_t>>
+int launch_narrow(const typename OP::in_t* const* src, const WS& w, int32_t K, int64_t N, typename OP::out_t* out,
+                  bool aligned, hipStream_t stream, const char* name) {
+  const int64_t grid = ((N + EL - 1) / EL + BS - 1) / BS;
+  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, std::string(name) + ": N too large");
+  Seg<OP> s{src, N};
+  StoreEpi<OP> epi{out};
+  if (aligned)
+    hipLaunchKernelGGL((reduce_narrow_kernel<OP, U, EL, true, BS, WS>), dim3(unsigned(grid)), dim3(BS), 0, stream, s,
+                       epi, w, K);
+  else
+    hipLaunchKernelGGL((reduce_narrow_kernel<OP, U, EL, false, BS, WS>), dim3(unsigned(grid)), dim3(BS), 0, stream, s,
+                       epi, w, K);
+  return check_launch(name);
+}
+
 // ---------------------------------------------------------------------------
 // Shipped kernel configuration per op (chosen by tools/tune_wsum.py on MI355X).
 
@@ -829,7 +911,13 @@ constexpr int64_t kMid2BelowBlocks = 512;
 // Many clients over a tensor too small to give every CU a workgroup (e.g. 1,000
 // clients x a 7,850-element model): each lane's chain over the clients is a
 // sequence of memory round trips, so twice the clients in flight halves it.
+// For 16-bit inputs (a 16-byte pack holds 8 elements, widened to fp32 in
+// registers) 32 clients in flight took 262-266 VGPRs, one wave per SIMD: U is
+// halved there (TinyU), which keeps the 16-bit Tiny kernels near the fp32
+// one's register count.
 struct TinyCfg { static constexpr int U = 32, V = 1, BS = 64; static constexpr bool NT = true; };
+template <class OP>
+constexpr int TinyU = sizeof(typename OP::in_t) == 2 ? 16 : TinyCfg::U;
 constexpr int64_t kTinyBelowElems = 65536;  // fewer than 256 small-tile workgroups
 constexpr int32_t kTinyFromClients = 48;
 
@@ -875,7 +963,7 @@ int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t
               hipStream_t st, const char* name) {
   const int64_t blocks = blocks_for<OP>(N);
   if (N < kTinyBelowElems && K >= kTinyFromClients)
-    return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
+    return launch_uvn<OP, TinyU<OP>, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks < kMid2BelowBlocks)
@@ -1005,6 +1093,46 @@ const Variant kVariants[] = {
     {"shipped", shipped_fn},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// Tuning table for many clients over small tensors (fedagg_wsum_tiny_variant):
+// fp32 and bf16 (reference chain), 16-byte tiles against narrow packs.
+using TinyFn = int (*)(const void* const*, const float*, int32_t, int64_t, void*, hipStream_t);
+struct TinyVariant {
+  const char* name;
+  TinyFn f32, bf16;
+};
+template <class OP, int U, int EL>
+int tiny_narrow_fn(const void* const* src, const float* w, int32_t K, int64_t N, void* out, hipStream_t st) {
+  constexpr int BS = 64;
+  const int64_t grid = ((N + EL - 1) / EL + BS - 1) / BS;
+  hipLaunchKernelGGL((reduce_narrow_kernel<OP, U, EL, true, BS, PtrW<float>>), dim3(unsigned(grid)), dim3(BS), 0, st,
+                     Seg<OP>{reinterpret_cast<const typename OP::in_t* const*>(src), N},
+                     StoreEpi<OP>{reinterpret_cast<typename OP::out_t*>(out)}, PtrW<float>{w}, K);
+  return check_launch("fedagg_wsum_tiny_variant");
+}
+template <class OP, int U>
+int tiny_wide_fn(const void* const* src, const float* w, int32_t K, int64_t N, void* out, hipStream_t st) {
+  return launch_uvn<OP, U, 1, true, 64>(reinterpret_cast<const typename OP::in_t* const*>(src), PtrW<float>{w}, K, N,
+                                        reinterpret_cast<typename OP::out_t*>(out), true, st,
+                                        "fedagg_wsum_tiny_variant");
+}
+template <class OP>
+int tiny_shipped_fn(const void* const* src, const float* w, int32_t K, int64_t N, void* out, hipStream_t st) {
+  return launch_ws<OP>(reinterpret_cast<const typename OP::in_t* const*>(src), PtrW<float>{w}, K, N,
+                       reinterpret_cast<typename OP::out_t*>(out), true, st, "fedagg_wsum_tiny_variant");
+}
+#define FEDAGG_TINY_NARROW(U, EL) \
+  { "EL" #EL "_U" #U, tiny_narrow_fn<OpF32, U, EL>, tiny_narrow_fn<OpBF16Ref, U, EL> }
+const TinyVariant kTinyVariants[] = {
+    {"shipped", tiny_shipped_fn<OpF32>, tiny_shipped_fn<OpBF16Ref>},
+    {"wide_U16", tiny_wide_fn<OpF32, 16>, tiny_wide_fn<OpBF16Ref, 16>},
+    {"wide_U32", tiny_wide_fn<OpF32, 32>, tiny_wide_fn<OpBF16Ref, 32>},
+    FEDAGG_TINY_NARROW(16, 1), FEDAGG_TINY_NARROW(32, 1), FEDAGG_TINY_NARROW(64, 1),
+    FEDAGG_TINY_NARROW(16, 2), FEDAGG_TINY_NARROW(32, 2), FEDAGG_TINY_NARROW(64, 2),
+    FEDAGG_TINY_NARROW(16, 4), FEDAGG_TINY_NARROW(32, 4), FEDAGG_TINY_NARROW(64, 4),
+};
+#undef FEDAGG_TINY_NARROW
+constexpr int kNumTinyVariants = sizeof(kTinyVariants) / sizeof(kTinyVariants[0]);
 
 // ---------------------------------------------------------------------------
 // Coordinate-wise median (the reference's "wise_median" defense:
@@ -2746,5 +2874,22 @@ const char* fedagg_variant_name(int32_t variant) {
 }
 
 int32_t fedagg_num_variants(void) { return kNumVariants; }
+
+int fedagg_wsum_tiny_variant(int32_t dtype, const void* const* d_src, const float* d_w, int32_t K, int64_t N,
+                             void* d_out, int32_t variant, fedagg_stream_t stream) {
+  if (variant < 0 || variant >= kNumTinyVariants) return set_error(FEDAGG_EINVAL, "bad variant");
+  if (dtype != FEDAGG_DT_F32 && dtype != FEDAGG_DT_BF16) return set_error(FEDAGG_EINVAL, "tiny variants: f32 or bf16");
+  if (K < 1 || N < 0 || !d_src || !d_w || !d_out) return set_error(FEDAGG_EINVAL, "bad argument");
+  if (N == 0) return FEDAGG_OK;
+  const TinyVariant& v = kTinyVariants[variant];
+  return (dtype == FEDAGG_DT_F32 ? v.f32 : v.bf16)(d_src, d_w, K, N, d_out, reinterpret_cast<hipStream_t>(stream));
+}
+
+const char* fedagg_tiny_variant_name(int32_t variant) {
+  if (variant < 0 || variant >= kNumTinyVariants) return "";
+  return kTinyVariants[variant].name;
+}
+
+int32_t fedagg_num_tiny_variants(void) { return kNumTinyVariants; }
 
 }  // extern "C"

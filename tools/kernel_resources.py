@@ -23,21 +23,26 @@ LIB = os.path.join(ROOT, "fedml_amd", "lib", "libfedagg.so")
 READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 
-def code_object(lib: str = LIB) -> bytes:
+def code_objects(lib: str = LIB):
+    """The gfx950 code object of EVERY offload bundle in the library (one per
+    translation unit: fedagg.hip and robust.hip)."""
     data = open(lib, "rb").read()
+    out = []
     i = data.find(b"__CLANG_OFFLOAD_BUNDLE__")
-    if i < 0:
-        raise SystemExit("no offload bundle in " + lib)
-    n = struct.unpack_from("<Q", data, i + 24)[0]
-    p = i + 32
-    for _ in range(n):
-        off, size, tl = struct.unpack_from("<QQQ", data, p)
-        p += 24
-        triple = data[p:p + tl].decode()
-        p += tl
-        if "gfx950" in triple:
-            return data[i + off:i + off + size]
-    raise SystemExit("no gfx950 code object")
+    while i >= 0:
+        n = struct.unpack_from("<Q", data, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            triple = data[p:p + tl].decode(errors="replace")
+            p += tl
+            if "gfx950" in triple:
+                out.append(data[i + off:i + off + size])
+        i = data.find(b"__CLANG_OFFLOAD_BUNDLE__", i + 24)
+    if not out:
+        raise SystemExit("no gfx950 code object in " + lib)
+    return out
 
 
 def kernels(co: bytes):
@@ -68,7 +73,7 @@ def kernels(co: bytes):
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r03", "kernel_resources.tsv")
-    ks = sorted(kernels(code_object()), key=lambda k: k["kernel"])
+    ks = sorted((k for co in code_objects() for k in kernels(co)), key=lambda k: k["kernel"])
     cols = ["kernel", "vgpr_count", "agpr_count", "occupancy", "sgpr_count", "vgpr_spill_count",
             "sgpr_spill_count", "private_segment_fixed_size", "group_segment_fixed_size"]
     with open(out, "w") as f:

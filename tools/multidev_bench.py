@@ -1,0 +1,121 @@
+"""Cost of spreading one round over G devices in ONE process (fedml_amd.multidev),
+measured with the G shards on the box's one GPU (GPU only).
+
+Two call shapes at config 3's state dict (ResNet-50, 320 keys, int64
+counters), K clients:
+
+  host   FedMLAggOperator.agg(args, host dicts) with args.fedagg_devices listing
+         G devices: per-shard pack + H2D, per-shard reduction, per-shard D2H and
+         scatter into per-key host tensors (FedML's CPU-server call shape);
+  device the cross-silo shape: each client's dict rebound to views of its
+         slot in a MultiDeviceBucket, then agg() on the views (the walker
+         groups the keys by device and launches each device's chunks).
+
+On one GPU the shards share one PCIe link and one HBM, so this measures the
+splitting overhead (more launches, copies, streams), not the G-fold bandwidth
+of G GPUs.  Every G's result is compared bit for bit with G = 1.
+
+    python tools/multidev_bench.py --clients 32 --reps 3
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from collections import OrderedDict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from fedml_amd import agg_operator as ao  # noqa: E402
+from fedml_amd import shapes  # noqa: E402
+from fedml_amd.multidev import MultiDeviceBucket  # noqa: E402
+
+
+class Args:
+    federated_optimizer = "FedAvg"
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--shards", type=int, nargs="*", default=[1, 2, 4])
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    entries = shapes.resnet50()
+    K = a.clients
+    g = torch.Generator(device=dev).manual_seed(0)
+    raw = []
+    for i in range(K):
+        d = OrderedDict()
+        for k, s, dt in entries:
+            if dt == torch.int64:
+                d[k] = torch.full(s, 5 + i, dtype=dt)
+            else:
+                d[k] = (torch.randn(s, generator=g, device=dev) * 0.05).cpu()
+        raw.append((100 + 7 * i, d))
+    nbytes = K * sum(t.numel() * t.element_size() for t in raw[0][1].values())
+    res = {"clients": K, "model": "resnet50", "host_bytes_per_round": nbytes, "host": {}, "device": {}}
+    ref_host = None
+    for G in a.shards:
+        args = Args()
+        args.fedagg_devices = [dev] * G
+        ts = []
+        out = None
+        for r in range(a.reps + 1):
+            lst = [(n, OrderedDict(d)) for n, d in raw]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = ao.FedMLAggOperator.agg(args, lst)
+            torch.cuda.synchronize()
+            if r:
+                ts.append(time.perf_counter() - t0)
+        if ref_host is None:
+            ref_host = out
+        same = all(torch.equal(out[k].view(-1).view(torch.int32) if out[k].dtype == torch.float32 else out[k],
+                               ref_host[k].view(-1).view(torch.int32) if ref_host[k].dtype == torch.float32
+                               else ref_host[k]) for k in out)
+        ms = statistics.median(ts) * 1e3
+        res["host"][f"G{G}"] = {"ms": round(ms, 2), "GBps_host_in": round(nbytes / ms / 1e6, 1),
+                                "bitwise_equal_to_G1": same}
+        print("host", G, res["host"][f"G{G}"], flush=True)
+        ao._MULTI.clear()
+        ao._BUCKETS.clear()
+    ref_dev = None
+    for G in a.shards:
+        b = MultiDeviceBucket([(k, s, dt) for k, s, dt in entries], K, [dev] * G, promote_ints=False)
+        views = []
+        for i, (n, d) in enumerate(raw):
+            b.put(i, d, n)
+            views.append((n, b.view(i)))
+        b.sync_ingest()
+        torch.cuda.synchronize()
+        ts = []
+        out = None
+        for r in range(a.reps * 3 + 1):
+            lst = [(n, OrderedDict(v)) for n, v in views]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = ao.FedMLAggOperator.agg(Args(), lst)
+            torch.cuda.synchronize()
+            if r:
+                ts.append(time.perf_counter() - t0)
+        if ref_dev is None:
+            ref_dev = OrderedDict((k, t.clone()) for k, t in out.items())
+        same = all(torch.equal(out[k], ref_dev[k]) for k in out)
+        ms = statistics.median(ts) * 1e3
+        res["device"][f"G{G}"] = {"ms": round(ms, 3), "bitwise_equal_to_G1": same}
+        print("device", G, res["device"][f"G{G}"], flush=True)
+        del b, views, out
+        torch.cuda.empty_cache()
+    os.makedirs("gpurun_out/r03", exist_ok=True)
+    json.dump(res, open("gpurun_out/r03/multidev_bench.json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
