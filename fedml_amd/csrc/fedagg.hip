@@ -143,11 +143,23 @@ struct OpBF16F32Out {  // bf16 in, fp32 partial out (multi-GPU pre-reduction)
   static __device__ __forceinline__ out_t fin(acc_t a) { return a; }
 };
 
+// f16, torch CPU chain.  torch rounds x * w to fp32 and then to f16 (two
+// roundings); left alone, the compiler folds mul + f16 rounding into one
+// v_fma_mixlo_f16, which rounds the exact product once and differs in rare
+// near-tie cases (1 element in 255 at K = 600).  The product is made opaque
+// so it is materialised in fp32 first.  (a + b of two f16 values is exact in
+// fp32 up to the final rounding, so v_add_f16 there is the same chain.)
+__device__ __forceinline__ float fp32_materialise(float v) {
+  asm("" : "+v"(v));
+  return v;
+}
 struct OpF16Ref {
   using in_t = uint16_t; using out_t = uint16_t; using acc_t = float; using w_t = float;
   static __device__ __forceinline__ float r(float f) { return f16_to_f32(f32_to_f16(f)); }
-  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return r(f16_to_f32(x) * w); }
-  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return r(a + r(f16_to_f32(x) * w)); }
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return r(fp32_materialise(f16_to_f32(x) * w)); }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) {
+    return r(a + r(fp32_materialise(f16_to_f32(x) * w)));
+  }
   static __device__ __forceinline__ out_t fin(acc_t a) { return f32_to_f16(a); }
 };
 
@@ -911,13 +923,10 @@ constexpr int64_t kMid2BelowBlocks = 512;
 // Many clients over a tensor too small to give every CU a workgroup (e.g. 1,000
 // clients x a 7,850-element model): each lane's chain over the clients is a
 // sequence of memory round trips, so twice the clients in flight halves it.
-// For 16-bit inputs (a 16-byte pack holds 8 elements, widened to fp32 in
-// registers) 32 clients in flight took 262-266 VGPRs, one wave per SIMD: U is
-// halved there (TinyU), which keeps the 16-bit Tiny kernels near the fp32
-// one's register count.
+// Since round 3 only the 8-byte element types (fp64, int64) take this tile:
+// 16-bit and fp32 rows go to the narrow packs below (round 2's 16-bit Tiny
+// tiles also sat at 262-266 VGPRs, one wave per SIMD).
 struct TinyCfg { static constexpr int U = 32, V = 1, BS = 64; static constexpr bool NT = true; };
-template <class OP>
-constexpr int TinyU = sizeof(typename OP::in_t) == 2 ? 16 : TinyCfg::U;
 constexpr int64_t kTinyBelowElems = 65536;  // fewer than 256 small-tile workgroups
 constexpr int32_t kTinyFromClients = 48;
 
@@ -958,12 +967,46 @@ int launch_uvn(const typename OP::in_t* const* src, const WS& w, int32_t K, int6
   return check_launch(name);
 }
 
+// Narrow packs (reduce_narrow_kernel) where the 16-byte tiles leave too few
+// lanes (tools/tune_tiny.py, profiles/r03/tiny/: every variant bit-identical).
+//   - 16-bit rows below 8M elements, any K: a 16-byte pack is 8 elements, so
+//     the wide tiles give a 1M-element tensor 2,048 64-lane blocks, each lane
+//     walking 8 reference chains.  Four-byte packs (EL = 2) give 4x the
+//     lanes: 1,000 x 62,006 bf16 0.132 -> 0.050 ms (EL = 1, 32 clients in
+//     flight, from 512 clients), 128 x 1M 0.057 -> 0.044 ms, 32 x 4M 0.052 ->
+//     0.047 ms; from 16M elements the wide tiles lead again.
+//   - fp32 below 1M elements with at least 48 clients: 8-byte packs (4-byte
+//     ones from 32K elements while the tensor is below the Tiny bound):
+//     4,096 x 7,850 0.215 -> 0.138 ms, 1,000 x 200K 0.144 -> 0.125 ms.
+constexpr int64_t kNarrow16BelowElems = int64_t(8) << 20;
+constexpr int64_t kNarrow32BelowElems = int64_t(1) << 20;
+template <class OP, class WS>
+int launch_narrow_policy(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t N,
+                         typename OP::out_t* o, bool al, hipStream_t st, const char* name) {
+  if constexpr (sizeof(typename OP::in_t) == 2) {
+    if (K >= 512 && N < kTinyBelowElems) return launch_narrow<OP, 32, 1, 64, WS>(s, w, K, N, o, al, st, name);
+    if (K >= 512 && N < kNarrow32BelowElems) return launch_narrow<OP, 32, 2, 64, WS>(s, w, K, N, o, al, st, name);
+    return launch_narrow<OP, 16, 2, 64, WS>(s, w, K, N, o, al, st, name);
+  } else {
+    if (N >= 32768 && N < kTinyBelowElems) return launch_narrow<OP, 32, 1, 64, WS>(s, w, K, N, o, al, st, name);
+    return launch_narrow<OP, 32, 2, 64, WS>(s, w, K, N, o, al, st, name);
+  }
+}
+template <class OP>
+constexpr bool narrow_ok() {  // 4- and 8-byte packs of the element type
+  return sizeof(typename OP::in_t) == 2 || sizeof(typename OP::in_t) == 4;
+}
+
 template <class OP, class WS>
 int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t N, typename OP::out_t* o, bool al,
               hipStream_t st, const char* name) {
   const int64_t blocks = blocks_for<OP>(N);
+  if constexpr (narrow_ok<OP>()) {
+    if (sizeof(typename OP::in_t) == 2 ? N < kNarrow16BelowElems : (N < kNarrow32BelowElems && K >= kTinyFromClients))
+      return launch_narrow_policy<OP, WS>(s, w, K, N, o, al, st, name);
+  }
   if (N < kTinyBelowElems && K >= kTinyFromClients)
-    return launch_uvn<OP, TinyU<OP>, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
+    return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks < kMid2BelowBlocks)

@@ -268,7 +268,9 @@ def test_headline_shape_sampled_columns(dtype, cuda_device):
 
 
 @pytest.mark.parametrize("dtype,N", [(torch.float32, 4_194_305), (torch.float32, 16_777_216),
-                                     (torch.bfloat16, 8_388_613), (torch.float16, 8_390_000)])
+                                     (torch.bfloat16, 8_388_613), (torch.float16, 8_390_000),
+                                     (torch.bfloat16, 8_388_607), (torch.float16, 1_000_003),
+                                     (torch.float32, 1_048_575)])
 def test_mid_size_tiles_vs_oracle(dtype, N, cuda_device):
     """Launches of 1,025..4,096 tiles take the one-client-per-step tile
     configuration (MidCfg); every element checked against the oracle,
@@ -301,6 +303,23 @@ def test_bf16_fp32_accumulate_tolerance(cuda_device):
     ref_chain = ao.FedMLAggOperator.agg(type("A", (), {"federated_optimizer": "FedAvg"})(),
                                         _to_device(raw, cuda_device))["h"].float().cpu().double()
     assert float((ref_chain - exact).abs().mean()) > float(err.mean())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K,N", [(3, 1023), (48, 70_001), (600, 40_001), (600, 300_001), (9, 1_000_001)])
+def test_fp32_accumulate_narrow_packs_vs_oracle(K, N, dtype, cuda_device):
+    """fp32-accumulate mode on the narrow-pack tiles (16-bit rows below 8M
+    elements), bit for bit against the oracle's fp32 chain with one final RNE,
+    aligned and at a one-element offset."""
+    g = torch.Generator(device=cuda_device).manual_seed(K + N)
+    rows = (torch.randn((K, N + 1), generator=g, device=cuda_device) * 0.05).to(dtype)
+    ns = [5 + 3 * i for i in range(K)]
+    w = [n / sum(ns) for n in ns]
+    for group in ([rows[i, :N] for i in range(K)], [rows[i, 1:] for i in range(K)]):
+        out = torch.empty(N, device=cuda_device, dtype=dtype)
+        kn.wsum_tensors(group, w, out, kn.ACC_FP32)
+        exp = orc.wsum_acc32([t.cpu() for t in group], w)
+        gu.assert_same(out.cpu(), exp, f"acc32 K={K} N={N} {dtype}")
 
 
 def test_fedavg_seq_inplace_on_device(cuda_device):
@@ -500,22 +519,25 @@ def test_next_update_does_not_overtake_a_pending_reduction(cuda_device):
     gu.assert_same(outs2[torch.float32][:N].cpu(), exp_new, "next round")
 
 
-@pytest.mark.parametrize("K", [2, 17, 48, 100])
-@pytest.mark.parametrize("N", [1, 3, 5, 63, 65, 255, 257, 1023, 4_097, 70_001])
-def test_tight_tensors_every_tile_config(K, N, cuda_device):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K", [2, 17, 48, 100, 600])
+@pytest.mark.parametrize("N", [1, 3, 5, 63, 65, 255, 257, 1023, 4_097, 40_001, 70_001])
+def test_tight_tensors_every_tile_config(K, N, dtype, cuda_device):
     """Separately allocated client tensors of exactly N elements (no padding
     to read into), aligned and at an odd element offset, across the tile
-    configs (tiny many-client, small, shipped) and their ragged edge paths."""
+    configs (narrow many-client packs, tiny, small, shipped) and their ragged
+    edge paths; 16-bit rows on the reference chain."""
     g = torch.Generator(device=cuda_device).manual_seed(K * 100_003 + N)
-    ts = [torch.randn(N, generator=g, device=cuda_device) * 0.05 for _ in range(K)]
-    views = [torch.randn(N + 1, generator=g, device=cuda_device)[1:] for _ in range(K)]  # 4-byte offset
+    ts = [(torch.randn(N, generator=g, device=cuda_device) * 0.05).to(dtype) for _ in range(K)]
+    views = [(torch.randn(N + 1, generator=g, device=cuda_device) * 0.05).to(dtype)[1:]
+             for _ in range(K)]  # one-element offset: not 16-byte aligned
     ns = [3 + 7 * i for i in range(K)]
     w = [n / sum(ns) for n in ns]
     for group in (ts, views):
-        out = torch.empty(N, device=cuda_device)
+        out = torch.empty(N, device=cuda_device, dtype=dtype)
         kn.wsum_tensors(group, w, out)
         exp = orc.wsum([t.cpu() for t in group], w)
-        gu.assert_same(out.cpu(), exp, f"K={K} N={N}")
+        gu.assert_same(out.cpu(), exp, f"K={K} N={N} {dtype}")
 
 
 def test_put_interleaved_host_and_device_keys(cuda_device):
