@@ -1005,8 +1005,10 @@ int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t
     if (sizeof(typename OP::in_t) == 2 ? N < kNarrow16BelowElems : (N < kNarrow32BelowElems && K >= kTinyFromClients))
       return launch_narrow_policy<OP, WS>(s, w, K, N, o, al, st, name);
   }
-  if (N < kTinyBelowElems && K >= kTinyFromClients)
-    return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
+  if constexpr (!narrow_ok<OP>()) {  // 2- and 4-byte rows never reach it (narrow packs above)
+    if (N < kTinyBelowElems && K >= kTinyFromClients)
+      return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
+  }
   if (blocks < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);
   if (blocks < kMid2BelowBlocks)
