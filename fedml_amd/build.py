@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "fedagg.hip")
 # every translation unit of libfedagg.so: compiled to objects separately (an
 # unchanged unit is not recompiled), then linked
-SRCS = [SRC, os.path.join(HERE, "csrc", "robust.hip")]
+SRCS = [SRC, os.path.join(HERE, "csrc", "robust.hip"), os.path.join(HERE, "csrc", "median.hip")]
 OUT_DIR = os.path.join(HERE, "lib")
 OBJ_DIR = os.path.join(OUT_DIR, "obj")
 OUT = os.path.join(OUT_DIR, "libfedagg.so")
@@ -93,17 +93,21 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_rebuild():
         return OUT
     os.makedirs(OBJ_DIR, exist_ok=True)
-    objs = []
-    for src in SRCS:
-        obj = _obj(src)
+    objs = [_obj(src) for src in SRCS]
+    # the translation units compile side by side (one hipcc each)
+    jobs = []
+    for src, obj in zip(SRCS, objs):
         if force or _stale(obj, [src, HEADER, __file__]):
             tmp = obj + ".tmp.o"
             cmd = [hipcc(), *HIPCC_FLAGS, "-c", "-o", tmp, src]
             if verbose:
                 print(" ".join(cmd))
-            subprocess.run(cmd, check=True)
-            os.replace(tmp, obj)
-        objs.append(obj)
+            jobs.append((subprocess.Popen(cmd), cmd, tmp, obj))
+    failed = [cmd for p, cmd, _, _ in jobs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    for _, _, tmp, obj in jobs:
+        os.replace(tmp, obj)
     tmp = OUT + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:

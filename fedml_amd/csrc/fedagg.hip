@@ -1180,896 +1180,6 @@ const TinyVariant kTinyVariants[] = {
 constexpr int kNumTinyVariants = sizeof(kTinyVariants) / sizeof(kTinyVariants[0]);
 
 // ---------------------------------------------------------------------------
-// Coordinate-wise median (the reference's "wise_median" defense:
-// core/security/defense/coordinate_wise_median_defense.py:24-32, i.e.
-// torch.median(stack, dim=-1).values: the LOWER median, element (K-1)/2 of the
-// sorted column; any NaN in the column makes the result that NaN).
-//
-// One lane per parameter element holds the column's K values in registers
-// (KMAX >= K slots).  The column is padded with -inf / +inf so that its lower
-// median always lands at the network's fixed middle slot (KMAX-1)/2; a
-// pairwise sorting network is then fully unrolled at compile time, and since
-// only that one output slot is used, the compiler deletes every comparator
-// that does not feed it.  Loads are 4 B per lane (256 B per wave
-// instruction), all K of them independent and in flight together.  K == KMAX
-// (e.g. 128 clients) gets a kernel with no padding logic at all.
-//
-// VALU per element at K = 128 (gfx950 ISA): 2,017 v_min/v_max (+61 fused
-// min3/max3), 128 NaN compares; ~3,470 with the earlier Batcher network,
-// per-client 64-bit addressing and in-line first-NaN tracking.
-
-__device__ __forceinline__ void cmpx(float& a, float& b) {
-  const float lo = fminf(a, b), hi = fmaxf(a, b);
-  a = lo;
-  b = hi;
-}
-
-// Parberry's pairwise sorting network on N slots, generated at compile time.
-// Pruned to the one output slot the median needs, it keeps 2,011 min/max at
-// N = 128 where Batcher's odd-even merge sort keeps 2,299 (same 1,471
-// comparators before pruning; the pairwise network's last stages feed fewer
-// slots).
-struct CmpPair {
-  int a, b;
-};
-template <int N>
-struct PairwiseNet {
-  // emit(a, b) for every comparator in network order; returns the count
-  template <class F>
-  static constexpr int walk(F emit) {
-    int m = 0;
-    int a = 1;
-    for (; a < N; a *= 2) {
-      int b = a, c = 0;
-      while (b < N) {
-        emit(m++, b - a, b);
-        ++b;
-        c = (c + 1) % a;
-        if (c == 0) b += a;
-      }
-    }
-    a /= 4;
-    for (int e = 1; a > 0; a /= 2, e = e * 2 + 1) {
-      for (int d = e; d > 0; d /= 2) {
-        int b = (d + 1) * a, c = 0;
-        while (b < N) {
-          emit(m++, b - d * a, b);
-          ++b;
-          c = (c + 1) % a;
-          if (c == 0) b += a;
-        }
-      }
-    }
-    return m;
-  }
-  static constexpr int M = walk([](int, int, int) {});
-  struct Table {
-    CmpPair p[M > 0 ? M : 1];
-  };
-  static constexpr Table make() {
-    Table t{};
-    walk([&t](int m, int x, int y) { t.p[m] = CmpPair{x, y}; });
-    return t;
-  }
-  static constexpr Table table = make();
-};
-
-// two 16-bit order keys per register: one v_pk_min_i16 + one v_pk_max_i16
-typedef short short2_t __attribute__((ext_vector_type(2)));
-typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void cmpx(short2_t& a, short2_t& b) {
-  const short2_t lo = __builtin_elementwise_min(a, b), hi = __builtin_elementwise_max(a, b);
-  a = lo;
-  b = hi;
-}
-
-template <int N, int I, class T>
-__device__ __forceinline__ void net_cmp(T (&v)[N]) {
-  constexpr int A = PairwiseNet<N>::table.p[I].a, B = PairwiseNet<N>::table.p[I].b;
-  cmpx(v[A], v[B]);
-}
-template <int N, class T, int... I>
-__device__ __forceinline__ void net_apply(T (&v)[N], std::integer_sequence<int, I...>) {
-  (net_cmp<N, I>(v), ...);
-}
-template <int N, class T>
-__device__ __forceinline__ void pairwise_sort(T (&v)[N]) {
-  net_apply<N, T>(v, std::make_integer_sequence<int, PairwiseNet<N>::M>{});
-}
-
-// Element types of the median kernels.  Every column value becomes an fp32
-// "selection value" whose float order is the element's order, the networks
-// select on those, and the selected value maps back to the input's bits
-// exactly (it is one of the inputs).  fp32 and bf16 widen exactly (bf16 is
-// the top half of an fp32).  f16 maps to an order-preserving 16-bit key
-// placed in the mantissa of [1, 2): x ^ 0x8000 for positive, ~x for negative
-// values, so -inf < -finite < -0 < +0 < +finite < +inf as keys, all normal
-// floats, and the ±inf pads stay below / above every key.  (Widening f16 to
-// fp32 with v_cvt kept both forms live and took the K = 128 kernel to 256
-// VGPRs, occupancy 1.)  nan() tests a selection value for NaN.
-struct MedF32 {
-  using S = float;
-  static __device__ __forceinline__ float widen(S x) { return x; }
-  static __device__ __forceinline__ S narrow(float v) { return v; }
-  static __device__ __forceinline__ bool nan(float v) { return __builtin_isnan(v); }
-  static __device__ __forceinline__ bool raw_nan(S x) { return __builtin_isnan(x); }
-  static constexpr bool kReloadNan = false;
-  // running "any NaN so far" over the column's selection values
-  using NanAcc = bool;
-  static __device__ __forceinline__ void nan_add(NanAcc& a, float v) { a |= __builtin_isnan(v); }
-  static __device__ __forceinline__ bool nan_any(NanAcc a) { return a; }
-  static constexpr uint32_t kNegInf = 0xff800000u, kPosInf = 0x7f800000u;
-};
-struct IsNanAcc {
-  using NanAcc = bool;
-  static __device__ __forceinline__ void nan_add(NanAcc& a, float v) { a |= __builtin_isnan(v); }
-  static __device__ __forceinline__ bool nan_any(NanAcc a) { return a; }
-};
-struct MedBF16 : IsNanAcc {
-  using S = uint16_t;
-  static __device__ __forceinline__ bool raw_nan(S x) { return (x & 0x7fffu) > 0x7f80u; }
-  static constexpr bool kReloadNan = true;
-  static __device__ __forceinline__ float widen(S x) { return __uint_as_float(uint32_t(x) << 16); }
-  static __device__ __forceinline__ S narrow(float v) { return S(__float_as_uint(v) >> 16); }
-  static __device__ __forceinline__ bool nan(float v) { return __builtin_isnan(v); }
-  static constexpr uint32_t kNegInf = 0xff80u, kPosInf = 0x7f80u;
-};
-struct MedF16 {
-  using S = uint16_t;
-  static __device__ __forceinline__ bool raw_nan(S x) { return (x & 0x7fffu) > 0x7c00u; }
-  static constexpr bool kReloadNan = true;
-  // The value arrives in the high half (as bf16 does: a d16_hi load), its
-  // order key is built there (x ^ 0x8000 for positive, ~x for negative values)
-  // and shifted down two bits: a positive float below 2.0 whose float order
-  // is the key order (normal for every non-NaN key: -inf's key 0x03ff gives
-  // 0x00ffc000).
-  static __device__ __forceinline__ float widen(S x) {
-    const uint32_t u = uint32_t(x) << 16;
-    const uint32_t neg = uint32_t(int32_t(u) >> 31);
-    return __uint_as_float((u ^ (0x80000000u | (neg & 0x7fff0000u))) >> 2);
-  }
-  static __device__ __forceinline__ S narrow(float v) {
-    const uint32_t k = (__float_as_uint(v) << 2) >> 16;  // the 16-bit key
-    const uint32_t neg = ~uint32_t(int32_t(k << 16) >> 31);  // key below 0x8000: a negative value
-    return S(k ^ ((neg & 0x7fffu) | 0x8000u));
-  }
-  static __device__ __forceinline__ uint32_t key(float v) { return (__float_as_uint(v) << 2) >> 16; }
-  // NaN keys: +NaN 0x7c01..0x7fff -> 0xfc01..0xffff, -NaN 0xfc01..0xffff -> 0x0000..0x03fe
-  static __device__ __forceinline__ bool nan(float v) {
-    const uint32_t k = key(v);
-    return __float_as_uint(v) < 0x40000000u && (k > 0xfc00u || k < 0x03ffu);
-  }
-  // rotated key (k - 0x3ff) mod 2^16: NaN keys land above 0xf801, every other
-  // key at or below it, so one unsigned compare per value
-  using NanAcc = bool;
-  static __device__ __forceinline__ void nan_add(NanAcc& a, float v) { a |= ((key(v) - 0x3ffu) & 0xffffu) > 0xf801u; }
-  static __device__ __forceinline__ bool nan_any(NanAcc a) { return a; }
-  static constexpr uint32_t kNegInf = 0xfc00u, kPosInf = 0x7c00u;
-};
-
-// -inf / +inf in each element type: what a padded slot's load returns
-template <class E>
-__device__ typename E::S g_median_pad[2] = {__builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
-                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kNegInf)),
-                                            __builtin_bit_cast(typename E::S, static_cast<std::conditional_t<
-                                                sizeof(typename E::S) == 4, uint32_t, uint16_t>>(E::kPosInf))};
-
-// Row base of client row p for a launch starting at column col0 (> 0 only
-// past 2^30 columns): an opaque SGPR pair, so the loads keep the
-// SGPR-base + 32-bit VGPR-offset form (left visible, the compiler folds col0
-// into a per-lane 64-bit address: 2.2x slower at K = 128).
-template <class T>
-__device__ __forceinline__ const char __attribute__((address_space(1)))* row_base(const T* p, int64_t col0) {
-  uint64_t b = reinterpret_cast<uint64_t>(p) + uint64_t(col0) * sizeof(T);
-  asm("" : "+s"(b));
-  return reinterpret_cast<const char __attribute__((address_space(1)))*>(b);
-}
-
-// Columns [col0, col0 + N) of the rows; out points at column col0's slot.
-// Launches cover at most 2^30 columns (kMedianChunk) so that a lane's byte
-// offset from the (wave-uniform) row base + col0 fits in 32 bits.
-template <int KMAX, bool FULL, int BS, bool PRIO = false, class E = MedF32, bool OFF = false>
-__global__ __launch_bounds__(BS) void median_kernel(const typename E::S* const* __restrict__ src, int K, int64_t N,
-                                                    typename E::S* __restrict__ out, int64_t col0 = 0) {
-  const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;
-  if constexpr (FULL) K = KMAX;  // K == KMAX: no padding, no per-client conditions
-  const int below = (KMAX - 1) / 2 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
-  // K < KMAX: the KMAX slot pointers (pads point at a ±inf constant) staged
-  // in LDS once per block.  Read per slot at a wave-uniform address and moved
-  // to SGPRs, they keep the loads in the SGPR-base form and batched; reading
-  // src[min(c, K - 1)] instead issued one s_load per client and waited for
-  // each (2.3x the K == KMAX time at K = 100).
-  __shared__ const typename E::S* tab[FULL ? 1 : KMAX];
-  if constexpr (!FULL) {
-    for (int i = threadIdx.x; i < KMAX; i += BS) tab[i] = i < K ? src[i] : &g_median_pad<E>[i - K < below ? 0 : 1];
-    __syncthreads();
-  }
-  if (e >= N) return;
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // issue this wave's loads ahead of others' sorting
-  // The host guarantees N * 4 < 2^32: a 32-bit byte offset on each
-  // wave-uniform row base lets every load use the SGPR-base + VGPR-offset
-  // form, with no per-client 64-bit address arithmetic on the VALU.
-  const uint32_t boff = uint32_t(e) * uint32_t(sizeof(typename E::S));
-  float v[KMAX];
-  typename E::NanAcc nacc{};
-#pragma unroll
-  for (int c = 0; c < KMAX; ++c) {
-    // Keep at most 16 row pointers live in SGPRs: without the barrier the
-    // scheduler hoists all K pointer loads to the top and spills them.
-    if (c % 16 == 0 && c) __builtin_amdgcn_sched_barrier(0);
-    // A padded slot (c >= K) reads a ±inf constant: its row pointer is the
-    // pad and its lane offset is 0, so the load itself yields the pad.
-    // Nothing per slot waits for a load here: all KMAX loads are in flight
-    // before the first value is used.
-    const bool live = FULL || c < K;
-    const typename E::S* p;
-    if constexpr (FULL) {
-      p = src[c];
-    } else {
-      // readfirstlane returns int: go through uint32_t, or a low word with
-      // its top bit set sign-extends over the high word
-      const uint64_t t = reinterpret_cast<uint64_t>(tab[c]);
-      const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(t >> 32))));
-      const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(t))));
-      p = reinterpret_cast<const typename E::S*>((uint64_t(hi) << 32) | uint64_t(lo));
-    }
-    const char __attribute__((address_space(1)))* row;
-    if constexpr (OFF)
-      row = live ? row_base(p, col0) : reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(p));
-    else
-      row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(p));
-    v[c] = E::widen(__builtin_nontemporal_load(
-        reinterpret_cast<const typename E::S __attribute__((address_space(1)))*>(row + (live ? boff : 0u))));
-    if constexpr (sizeof(typename E::S) == 2) E::nan_add(nacc, v[c]);
-  }
-  // torch returns the first NaN of the column (client order) if there is
-  // one; the common case pays one test per client.  fp32 tests after every
-  // load is in flight (testing inside the load loop waited for each pair of
-  // loads); 16-bit rows test as they widen (with all loads in flight first,
-  // the raw and widened values are both live: 259 VGPRs; this kernel is
-  // their unaligned-row path, the packed kernel takes aligned rows).
-  // Pads are ±inf, never NaN.
-  if constexpr (sizeof(typename E::S) == 4) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < KMAX; ++c) E::nan_add(nacc, v[c]);
-  }
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-  // Only a lane holding a NaN column searches.  fp32 tests the registers (one
-  // unordered compare); for 16-bit rows that search got speculated above the
-  // branch and kept both the loaded and the widened values live (259-267
-  // VGPRs), so they re-read the column in client order (cache hits).
-  typename E::S nan_raw{};
-  const bool has_nan = E::nan_any(nacc);
-  if (has_nan) {
-    if constexpr (E::kReloadNan) {
-#pragma unroll 1
-      for (int c = 0; c < K; ++c) {
-        const auto row = row_base(src[c], col0);
-        const typename E::S r = *reinterpret_cast<const typename E::S __attribute__((address_space(1)))*>(row + boff);
-        if (E::raw_nan(r)) {
-          nan_raw = r;
-          break;
-        }
-      }
-    } else {
-      float nan_v = 0.f;
-      bool found = false;
-#pragma unroll
-      for (int c = 0; c < KMAX; ++c) {
-        const bool n = (FULL || c < K) && !found && E::nan(v[c]);
-        nan_v = n ? v[c] : nan_v;
-        found = found || n;
-      }
-      nan_raw = E::narrow(nan_v);
-    }
-  }
-  pairwise_sort<KMAX>(v);
-  out[e] = has_nan ? nan_raw : E::narrow(v[(KMAX - 1) / 2]);
-}
-
-constexpr int64_t kMedianChunk = int64_t(1) << 30;  // columns per launch of the 32-bit-offset kernels
-
-template <int KMAX, class E = MedF32>
-int launch_median(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
-  constexpr int BS = 64;  // 3 % faster than 256 at config 3 (tools/median_probe.py, two boxes)
-  for (int64_t c0 = 0; c0 < N; c0 += kMedianChunk) {
-    const int64_t n = N - c0 < kMedianChunk ? N - c0 : kMedianChunk;
-    const int64_t grid = (n + BS - 1) / BS;
-    if (K == KMAX && c0 == 0)
-      hipLaunchKernelGGL((median_kernel<KMAX, true, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
-                         out, c0);
-    else if (c0 == 0)
-      hipLaunchKernelGGL((median_kernel<KMAX, false, BS, false, E>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
-                         out, c0);
-    else  // past 2^30 columns: the padded kernel (correct for K == KMAX too) with the row offset
-      hipLaunchKernelGGL((median_kernel<KMAX, false, BS, false, E, true>), dim3(unsigned(grid)), dim3(BS), 0, st, src,
-                         K, n, out + c0, c0);
-  }
-  return check_launch("fedagg_median");
-}
-
-// 16-bit rows, K <= 128, two columns per lane: a 32-bit load brings columns
-// 2e and 2e+1 of a client as one register, each half is turned into an
-// order-preserving int16 key (x ^ 0x7fff for negative values, so signed
-// compares follow the float order, -0 just below +0), and the same pruned
-// network runs on v_pk_min_i16 / v_pk_max_i16: half the VALU per column of the
-// widening kernel, which is VALU-bound on 16-bit rows.  Keys map back to the
-// input bits by the same transform.  Pads are the int16 extremes, below / above
-// every non-NaN key; a NaN column returns its first NaN, as everywhere.  Needs
-// 4-byte aligned rows and output (the FEDAGG_ALIGNED16 flag); an odd last
-// column is loaded and stored as 16 bits by its lane.
-__device__ __forceinline__ short2_t pk16_key(uint32_t x) {
-  const short2_t v = __builtin_bit_cast(short2_t, x);
-  return v ^ ((v >> short(15)) & short(0x7fff));
-}
-__device__ __forceinline__ uint32_t pk16_bits(short2_t k) {
-  return __builtin_bit_cast(uint32_t, k ^ ((k >> short(15)) & short(0x7fff)));
-}
-
-template <int KMAX, bool FULL, class E, bool TAIL, bool OFF>
-__device__ __forceinline__ void median_pk16_pair(const uint16_t* const* __restrict__ src, int K, int64_t e,
-                                                 uint16_t* __restrict__ out, int64_t col0) {
-  if constexpr (FULL) K = KMAX;
-  const uint32_t boff = uint32_t(e) * 4u;
-  const int below = (KMAX - 1) / 2 - (K - 1) / 2;
-  uint32_t raw[KMAX];
-  uint32_t nanacc = 0;  // per half, max of |x| bits
-#pragma unroll
-  for (int c = 0; c < KMAX; ++c) {
-    if (c % 16 == 0 && c) __builtin_amdgcn_sched_barrier(0);
-    const int ci = (FULL || c < K) ? c : K - 1;
-    const char __attribute__((address_space(1)))* row;
-    if constexpr (OFF)
-      row = row_base(src[ci], col0);
-    else
-      row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
-    uint32_t x;
-    if constexpr (!TAIL)
-      x = __builtin_nontemporal_load(reinterpret_cast<const uint32_t __attribute__((address_space(1)))*>(row + boff));
-    else  // the odd last column alone, duplicated into both halves
-      x = *reinterpret_cast<const uint16_t __attribute__((address_space(1)))*>(row + boff) * 0x10001u;
-    raw[c] = x;
-  }
-  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test (see median_kernel)
-#pragma unroll
-  for (int c = 0; c < KMAX; ++c) {
-    const uint32_t mag = raw[c] & 0x7fff7fffu;
-    nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
-                                                                     __builtin_bit_cast(ushort2_t, mag)));
-  }
-  const bool nan_lo = (nanacc & 0xffffu) > E::kPosInf, nan_hi = (nanacc >> 16) > E::kPosInf;
-  uint32_t nan_bits = 0;
-  if (nan_lo || nan_hi) {  // first NaN per half, in client order (only columns holding one)
-    bool f_lo = false, f_hi = false;
-#pragma unroll
-    for (int c = 0; c < KMAX; ++c) {
-      // predicated, not `break`: a data-dependent exit stops the full unroll
-      // and puts raw[] in scratch (272-528 B/lane before)
-      const bool live = FULL || c < K;
-      const uint32_t x = raw[c];
-      const bool n_lo = live && !f_lo && (x & 0x7fffu) > E::kPosInf;
-      const bool n_hi = live && !f_hi && ((x >> 16) & 0x7fffu) > E::kPosInf;
-      if (n_lo) nan_bits = (nan_bits & 0xffff0000u) | (x & 0xffffu);
-      if (n_hi) nan_bits = (nan_bits & 0xffffu) | (x & 0xffff0000u);
-      f_lo = f_lo || n_lo;
-      f_hi = f_hi || n_hi;
-    }
-  }
-  short2_t v[KMAX];
-#pragma unroll
-  for (int c = 0; c < KMAX; ++c) {
-    if constexpr (FULL)
-      v[c] = pk16_key(raw[c]);
-    else
-      v[c] = (c < K) ? pk16_key(raw[c]) : ((c - K < below) ? short2_t(short(-32768)) : short2_t(short(32767)));
-  }
-  pairwise_sort<KMAX>(v);
-  uint32_t m = pk16_bits(v[(KMAX - 1) / 2]);
-  if (nan_lo) m = (m & 0xffff0000u) | (nan_bits & 0xffffu);
-  if (nan_hi) m = (m & 0xffffu) | (nan_bits & 0xffff0000u);
-  if constexpr (!TAIL)
-    *reinterpret_cast<uint32_t*>(out + 2 * e) = m;
-  else
-    out[2 * e] = uint16_t(m);
-}
-
-template <int KMAX, bool FULL, class E, int BS = 256, bool OFF = false>
-__global__ __launch_bounds__(BS) void median_pk16_kernel(const uint16_t* const* __restrict__ src, int K, int64_t N,
-                                                         uint16_t* __restrict__ out, int64_t col0) {
-  static_assert(sizeof(typename E::S) == 2, "16-bit rows");
-  const int64_t e = int64_t(blockIdx.x) * BS + threadIdx.x;  // column pair
-  const int64_t pairs = (N + 1) / 2;
-  if (e >= pairs) return;
-  if ((N & 1) && e == pairs - 1)
-    median_pk16_pair<KMAX, FULL, E, true, OFF>(src, K, e, out, col0);
-  else
-    median_pk16_pair<KMAX, FULL, E, false, OFF>(src, K, e, out, col0);
-}
-
-template <int KMAX, class E>
-int launch_median_pk16(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
-  constexpr int BS = 64;
-  for (int64_t c0 = 0; c0 < N; c0 += kMedianChunk) {  // even chunk starts: 4-byte pairs stay aligned
-    const int64_t n = N - c0 < kMedianChunk ? N - c0 : kMedianChunk;
-    const int64_t grid = ((n + 1) / 2 + BS - 1) / BS;
-    if (K == KMAX && c0 == 0)
-      hipLaunchKernelGGL((median_pk16_kernel<KMAX, true, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
-                         out, c0);
-    else if (c0 == 0)
-      hipLaunchKernelGGL((median_pk16_kernel<KMAX, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, n,
-                         out, c0);
-    else
-      hipLaunchKernelGGL((median_pk16_kernel<KMAX, false, E, BS, true>), dim3(unsigned(grid)), dim3(BS), 0, st, src,
-                         K, n, out + c0, c0);
-  }
-  return check_launch("fedagg_median");
-}
-
-// More than 128 clients, in registers: P adjacent lanes share one column,
-// each holding R of its KMAX = P·R (±inf-padded) values, slot s = sub·R + j =
-// client s (shipped: P = 4, R = 64 up to 256 clients, then R = 128 with P = 4,
-// 8, 16 or 32, i.e. up to 4096 clients).  Every lane sorts its R values with the pairwise network (all outputs
-// used, so nothing is pruned); the sorted runs are then merged across lanes as
-// in a bitonic merge sort:
-//   - "reverse pairing" of two sorted runs A, B of length L held by lane
-//     groups g and g ^ (G-1): element i of A meets element L-1-i of B, the
-//     lower group keeps the min (the L smallest, a bitonic sequence), the
-//     upper the max.  Partner lane = sub ^ (G-1), partner register = R-1-i;
-//   - a half-cleaner cascade sorts each bitonic half: stages whose slot
-//     distance is a multiple of R pair lane sub with sub ^ m at the same
-//     register, the rest run inside the lane.
-// Cross-lane moves are single DPP movs (xor 1 / 2 / 3 quad permutes, xor 7 =
-// row_half_mirror, xor 15 = row_mirror), the min-or-max choice one v_med3
-// against ±inf.  The last level needs no merge: after its reverse pairing the
-// lower half holds exactly the KMAX/2 smallest values, whose maximum sits at
-// the padded median slot KMAX/2 - 1, i.e. it is the column's lower median.
-// VALU per column ≈ 8k (P·R = 4·64), 20k (4·128), 49k (8·128) lane-ops,
-// against 2k for K <= 128.
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
-}
-template <int M>
-constexpr int dpp_xor_ctrl() {
-  static_assert(M == 1 || M == 2 || M == 3 || M == 7 || M == 15, "lane xor pattern without a single DPP mov");
-  // quad_perm [1,0,3,2], [2,3,0,1], [3,2,1,0]; row_half_mirror; row_mirror
-  return M == 1 ? 0xB1 : M == 2 ? 0x4E : M == 3 ? 0x1B : M == 7 ? 0x141 : 0x140;
-}
-
-// The value of lane ^ M: one DPP mov where a pattern exists (xor 1, 2, 3,
-// 7, 15), two for xor 4 (xor 7 then xor 3), else ds_bpermute (xor 31: the
-// last level of the 32-lane groups above 2,048 clients).
-template <int M>
-constexpr bool dpp_xor_ok() { return M == 1 || M == 2 || M == 3 || M == 7 || M == 15; }
-template <int M>
-__device__ __forceinline__ float xor_mov(float x) {
-  if constexpr (dpp_xor_ok<M>()) return dpp_mov<dpp_xor_ctrl<M>()>(x);
-  else if constexpr (M == 4) return dpp_mov<dpp_xor_ctrl<3>()>(dpp_mov<dpp_xor_ctrl<7>()>(x));  // (i ^ 7) ^ 3
-  else return __int_as_float(__shfl_xor(__float_as_int(x), M, 64));
-}
-
-// min (lower lanes, sel = -inf) or max (upper lanes, sel = +inf) of own
-// register i and the partner lane's register R-1-i, for every i
-template <int M, int R>
-__device__ __forceinline__ void lanes_reverse_pair(float (&v)[R], float sel) {
-  // opaque to the compiler: knowing sel is ±inf it splits every v_med3 into
-  // min, max and a select (three ops and twice the live registers)
-  asm volatile("" : "+v"(sel));
-#pragma unroll
-  for (int i = 0; i < R / 2; ++i) {
-    const float a = xor_mov<M>(v[R - 1 - i]);
-    const float b = xor_mov<M>(v[i]);
-    v[i] = __builtin_amdgcn_fmed3f(v[i], a, sel);
-    v[R - 1 - i] = __builtin_amdgcn_fmed3f(v[R - 1 - i], b, sel);
-  }
-}
-
-// half-cleaner stage between lanes sub and sub ^ M, same register
-template <int M, int R>
-__device__ __forceinline__ void lanes_cross_stage(float (&v)[R], int sub) {
-  float sel = (sub & M) ? __builtin_huge_valf() : -__builtin_huge_valf();
-  asm volatile("" : "+v"(sel));
-#pragma unroll
-  for (int i = 0; i < R; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], xor_mov<M>(v[i]), sel);
-}
-
-// in-lane half-cleaner cascade: a bitonic register array -> ascending
-template <int R>
-__device__ __forceinline__ void lane_bitonic_merge(float (&v)[R]) {
-#pragma unroll
-  for (int d = R / 2; d > 0; d /= 2) {
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-      if ((i & d) == 0) cmpx(v[i], v[i + d]);
-  }
-}
-
-// merge levels G = 2, 4, 8 (< P): afterwards every group of G lanes holds its
-// G·R values sorted ascending over slots (sub % G)·R + j
-template <int G, int P, int R>
-__device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
-  if constexpr (G < P) {
-    static_assert(G <= 16, "lane groups of at most 32");
-    lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) ? __builtin_huge_valf() : -__builtin_huge_valf());
-    if constexpr (G == 16) lanes_cross_stage<4>(v, sub);  // slot distance 4R
-    if constexpr (G >= 8) lanes_cross_stage<2>(v, sub);  // slot distance 2R
-    if constexpr (G >= 4) lanes_cross_stage<1>(v, sub);  // slot distance R
-    lane_bitonic_merge(v);
-    lanes_merge_levels<G * 2, P, R>(v, sub);
-  }
-}
-
-template <int P, int R, bool FULL, class E = MedF32, int BS = 256>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_lanes_kernel(
-    const typename E::S* const* __restrict__ src, int K, int64_t N, typename E::S* __restrict__ out) {
-  using S = typename E::S;
-  static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column");
-  static_assert(R == 64 || R == 128, "64 or 128 values per lane");
-  constexpr int KMAX = P * R, PAD = 2;
-  // Row pointer of every slot, skewed by PAD entries per lane group so the P
-  // lanes of a column read different LDS banks.  A padded slot (K < KMAX)
-  // points at a ±inf constant and its column offset is masked to 0, so the
-  // load itself yields the pad: no per-slot, per-lane select.
-  __shared__ const S* rows[KMAX + PAD * P];
-  __shared__ uint64_t offmask[FULL ? 1 : KMAX + PAD * P];
-  const int t = threadIdx.x, sub = t & (P - 1);
-  if constexpr (FULL) K = KMAX;
-  const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
-  for (int i = t; i < KMAX; i += BS) {
-    const int q = i + PAD * (i / R);
-    if (FULL || i < K) {
-      rows[q] = src[i];
-      if constexpr (!FULL) offmask[q] = ~uint64_t(0);
-    } else {
-      rows[q] = &g_median_pad<E>[i - K < below ? 0 : 1];
-      offmask[q] = 0;
-    }
-  }
-  __syncthreads();
-  // every lane stays active through the DPP exchanges; a column past the end
-  // recomputes the last one and does not store
-  const int64_t e = (int64_t(blockIdx.x) * BS + t) / P;
-  const uint64_t boff = uint64_t(e < N ? e : N - 1) * sizeof(S);
-  float v[R];
-  typename E::NanAcc nacc{};
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if (j % 16 == 0 && j) __builtin_amdgcn_sched_barrier(0);
-    const int q = sub * (R + PAD) + j;
-    const uint64_t off = FULL ? boff : (boff & offmask[q]);
-    const auto row = reinterpret_cast<const char*>(rows[q]);
-    v[j] = E::widen(__builtin_nontemporal_load(as_global(reinterpret_cast<const S*>(row + off))));
-  }
-  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test (see median_kernel)
-#pragma unroll
-  for (int j = 0; j < R; ++j) E::nan_add(nacc, v[j]);
-  const bool has_nan = E::nan_any(nacc);
-  // first NaN of the column in client (= slot) order, only in waves holding
-  // one (pads are ±inf, never NaN)
-  int nan_slot = KMAX;
-  S nan_raw{};
-  if (__ballot(has_nan)) {
-    // re-read this lane's slots in client order (cache hits; see median_kernel)
-#pragma unroll 1
-    for (int j = 0; j < R; ++j) {
-      const int q = sub * (R + PAD) + j;
-      const uint64_t off = FULL ? boff : (boff & offmask[q]);
-      const S r = *as_global(reinterpret_cast<const S*>(reinterpret_cast<const char*>(rows[q]) + off));
-      if (E::raw_nan(r)) {
-        nan_slot = sub * R + j;
-        nan_raw = r;
-        break;
-      }
-    }
-#pragma unroll
-    for (int m = 1; m < P; m <<= 1) {
-      const int os = __shfl_xor(nan_slot, m, 64);
-      using U = std::conditional_t<sizeof(S) == 4, uint32_t, uint16_t>;  // move the bits, not the value
-      const S ov = __builtin_bit_cast(
-          S, U(__shfl_xor(int(uint32_t(__builtin_bit_cast(U, nan_raw))), m, 64)));
-      if (os < nan_slot) {
-        nan_slot = os;
-        nan_raw = ov;
-      }
-    }
-  }
-  pairwise_sort<R>(v);
-  lanes_merge_levels<2, P, R>(v, sub);
-  // last level: after the reverse pairing against sub ^ (P-1) the lower P/2
-  // lanes hold the KMAX/2 smallest values; their max is the median
-  lanes_reverse_pair<P - 1>(v, (sub & (P / 2)) ? __builtin_huge_valf() : -__builtin_huge_valf());
-  float m = v[0];
-#pragma unroll
-  for (int i = 1; i < R; ++i) m = fmaxf(m, v[i]);
-  if constexpr (P >= 4) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
-  if constexpr (P >= 8) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
-  if constexpr (P >= 16) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima across the two quads
-  if constexpr (P >= 32) m = fmaxf(m, dpp_mov<dpp_xor_ctrl<15>()>(m));  // the two 8-lane halves of a row
-  if (sub == 0 && e < N) out[e] = nan_slot < KMAX ? nan_raw : E::narrow(m);
-}
-
-template <int P, int R, class E = MedF32, int BS = 256>
-int launch_median_lanes(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
-  const int64_t grid = (N * P + BS - 1) / BS;
-  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
-  if (K == P * R)
-    hipLaunchKernelGGL((median_lanes_kernel<P, R, true, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
-                       out);
-  else
-    hipLaunchKernelGGL((median_lanes_kernel<P, R, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st, src, K, N,
-                       out);
-  return check_launch("fedagg_median");
-}
-
-// 16-bit rows with more than 128 clients, two columns per register: the lane
-// group layout above on the packed int16 order keys of median_pk16_pair.  One
-// 32-bit load brings columns 2e and 2e+1 of a client; the in-lane sorts and
-// half-cleaners are v_pk_min_i16 / v_pk_max_i16 (one op per comparator side
-// for TWO columns), so the per-column VALU is about half of the widening
-// kernel's, which is what bounds this range.  The cross-lane min-or-max has no
-// packed med3: both sides and one v_cndmask on a lane mask.  Pads are packed
-// ±inf (their keys sit below / above every non-NaN key); a NaN column returns
-// its first NaN in client order, per half.  An odd last column runs as the
-// TAIL instantiation: one block whose every column group recomputes the
-// duplicated lone column, and lane 0 stores it.
-template <int CTRL>
-__device__ __forceinline__ short2_t dpp_mov(short2_t x) {
-  return __builtin_bit_cast(short2_t, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
-}
-template <int M>
-__device__ __forceinline__ short2_t xor_mov(short2_t x) {
-  if constexpr (dpp_xor_ok<M>()) return dpp_mov<dpp_xor_ctrl<M>()>(x);
-  else if constexpr (M == 4) return dpp_mov<dpp_xor_ctrl<3>()>(dpp_mov<dpp_xor_ctrl<7>()>(x));
-  else return __builtin_bit_cast(short2_t, __shfl_xor(__builtin_bit_cast(int, x), M, 64));
-}
-__device__ __forceinline__ short2_t pk_pick(short2_t a, short2_t b, bool up) {
-  const short2_t lo = __builtin_elementwise_min(a, b), hi = __builtin_elementwise_max(a, b);
-  return up ? hi : lo;
-}
-template <int M, int R>
-__device__ __forceinline__ void pk_lanes_reverse_pair(short2_t (&v)[R], bool up) {
-#pragma unroll
-  for (int i = 0; i < R / 2; ++i) {
-    const short2_t a = xor_mov<M>(v[R - 1 - i]);
-    const short2_t b = xor_mov<M>(v[i]);
-    v[i] = pk_pick(v[i], a, up);
-    v[R - 1 - i] = pk_pick(v[R - 1 - i], b, up);
-  }
-}
-template <int M, int R>
-__device__ __forceinline__ void pk_lanes_cross_stage(short2_t (&v)[R], int sub) {
-  const bool up = (sub & M) != 0;
-#pragma unroll
-  for (int i = 0; i < R; ++i) v[i] = pk_pick(v[i], xor_mov<M>(v[i]), up);
-}
-template <int R>
-__device__ __forceinline__ void pk_lane_bitonic_merge(short2_t (&v)[R]) {
-#pragma unroll
-  for (int d = R / 2; d > 0; d /= 2) {
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-      if ((i & d) == 0) cmpx(v[i], v[i + d]);
-  }
-}
-template <int G, int P, int R>
-__device__ __forceinline__ void pk_lanes_merge_levels(short2_t (&v)[R], int sub) {
-  if constexpr (G < P) {
-    static_assert(G <= 16, "lane groups of at most 32");
-    pk_lanes_reverse_pair<G - 1>(v, (sub & (G / 2)) != 0);
-    if constexpr (G == 16) pk_lanes_cross_stage<4>(v, sub);
-    if constexpr (G >= 8) pk_lanes_cross_stage<2>(v, sub);
-    if constexpr (G >= 4) pk_lanes_cross_stage<1>(v, sub);
-    pk_lane_bitonic_merge(v);
-    pk_lanes_merge_levels<G * 2, P, R>(v, sub);
-  }
-}
-
-// packed ±inf pair in each 16-bit element type: a padded slot's 32-bit load
-template <class E>
-__device__ uint32_t g_median_pad2[2] = {E::kNegInf * 0x10001u, E::kPosInf * 0x10001u};
-
-template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
-    const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out) {
-  static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column pair");
-  static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
-  constexpr int KMAX = P * R, PAD = 2;
-  __shared__ const uint16_t* rows[KMAX + PAD * P];
-  __shared__ uint64_t offmask[FULL ? 1 : KMAX + PAD * P];
-  const int t = threadIdx.x, sub = t & (P - 1);
-  if constexpr (FULL) K = KMAX;
-  const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
-  for (int i = t; i < KMAX; i += BS) {
-    const int q = i + PAD * (i / R);
-    if (FULL || i < K) {
-      rows[q] = src[i];
-      if constexpr (!FULL) offmask[q] = ~uint64_t(0);
-    } else {
-      rows[q] = reinterpret_cast<const uint16_t*>(&g_median_pad2<E>[i - K < below ? 0 : 1]);
-      offmask[q] = 0;
-    }
-  }
-  __syncthreads();
-  // TAIL: `pairs` is the index of the pair holding the lone last column.
-  // Otherwise a column group past the end recomputes the last pair and does
-  // not store (every lane stays active through the DPP exchanges).
-  const int64_t e = TAIL ? pairs : (int64_t(blockIdx.x) * BS + t) / P;
-  const uint64_t boff = uint64_t(TAIL || e < pairs ? e : pairs - 1) * 4u;
-  uint32_t raw[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if (j % 16 == 0 && j) __builtin_amdgcn_sched_barrier(0);
-    const int q = sub * (R + PAD) + j;
-    const uint64_t off = FULL ? boff : (boff & offmask[q]);
-    const auto row = reinterpret_cast<const char*>(rows[q]);
-    if constexpr (TAIL)
-      raw[j] = uint32_t(*as_global(reinterpret_cast<const uint16_t*>(row + off))) * 0x10001u;
-    else
-      raw[j] = __builtin_nontemporal_load(as_global(reinterpret_cast<const uint32_t*>(row + off)));
-  }
-  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test
-  uint32_t nanacc = 0;  // per half, max of |x| bits
-#pragma unroll
-  for (int j = 0; j < R; ++j)
-    nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
-                                                                     __builtin_bit_cast(ushort2_t, raw[j] & 0x7fff7fffu)));
-  // first NaN per half in client (= slot) order as (slot << 16 | bits), only
-  // in waves holding a NaN column; KMAX << 16: none
-  int first_lo = KMAX << 16, first_hi = KMAX << 16;
-  if (__ballot((nanacc & 0xffffu) > E::kPosInf || (nanacc >> 16) > E::kPosInf)) {
-#pragma unroll
-    for (int j = R - 1; j >= 0; --j) {  // predicated, walked backwards: the lowest slot wins
-      const uint32_t x = raw[j];
-      const int s = (sub * R + j) << 16;
-      if ((x & 0x7fffu) > E::kPosInf) first_lo = s | int(x & 0xffffu);
-      if (((x >> 16) & 0x7fffu) > E::kPosInf) first_hi = s | int(x >> 16);
-    }
-#pragma unroll
-    for (int m = 1; m < P; m <<= 1) {
-      first_lo = min(first_lo, __shfl_xor(first_lo, m, 64));
-      first_hi = min(first_hi, __shfl_xor(first_hi, m, 64));
-    }
-  }
-  short2_t v[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) v[j] = pk16_key(raw[j]);
-  pairwise_sort<R>(v);
-  pk_lanes_merge_levels<2, P, R>(v, sub);
-  // last level: the lower P/2 lanes keep the KMAX/2 smallest keys per half
-  pk_lanes_reverse_pair<P - 1>(v, (sub & (P / 2)) != 0);
-  short2_t m = v[0];
-#pragma unroll
-  for (int i = 1; i < R; ++i) m = __builtin_elementwise_max(m, v[i]);
-  if constexpr (P >= 4) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
-  if constexpr (P >= 8) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
-  if constexpr (P >= 16) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima
-  if constexpr (P >= 32) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<15>()>(m));  // row halves
-  uint32_t bits = pk16_bits(m);
-  if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
-  if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
-  if constexpr (TAIL) {
-    if (t == 0) out[2 * e] = uint16_t(bits);
-  } else if (sub == 0 && e < pairs) {
-    *reinterpret_cast<uint32_t*>(out + 2 * e) = bits;
-  }
-}
-
-template <int P, int R, class E, int BS = 256>
-int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
-  const int64_t pairs = N / 2;
-  const int64_t grid = (pairs * P + BS - 1) / BS;
-  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
-  if (pairs > 0) {
-    if (K == P * R)
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st,
-                         src, K, pairs, out);
-    else
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0,
-                         st, src, K, pairs, out);
-  }
-  if (N & 1)
-    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS>), dim3(1), dim3(BS), 0, st, src, K,
-                       pairs, out);
-  return check_launch("fedagg_median");
-}
-
-// Any number of clients (the path above 1024, where the lane-group sort runs
-// out of lanes per column): MSD radix select over 32-bit order keys, the
-// column tile streamed from memory once per 8-bit digit.  A block owns 64
-// consecutive columns; its 4 waves read rows q, q + 4, ... of all 64 (one
-// coalesced 64-column segment per wave instruction) and count the keys that
-// match the digits chosen so far into a per-column 256-bin LDS histogram;
-// then, per column, the bin holding the remaining rank gives the next digit.
-// Four passes fix all 32 bits.  Passes 2-4 re-read the tile (K x 256 B per
-// row group), mostly from L2 / MALL.  The NaN rule is the register kernels':
-// the column's first NaN in client order (an LDS atomic min on the row, pass
-// one).  Exact for every input; a ±0 tie at the median may return the other
-// zero than torch's nth_element, as everywhere.
-constexpr int kRsCols = 64;
-__device__ __forceinline__ uint32_t f32_order_key(uint32_t u) { return (u & 0x80000000u) ? ~u : (u | 0x80000000u); }
-__device__ __forceinline__ uint32_t f32_from_order_key(uint32_t k) { return (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k; }
-
-template <class E>
-__global__ __launch_bounds__(256) void median_radix_stream_kernel(const typename E::S* const* __restrict__ src, int K,
-                                                                  int64_t N, typename E::S* __restrict__ out) {
-  constexpr int HS = 257;  // bins per column + 1: column c starts c banks apart
-  __shared__ uint32_t hist[kRsCols * HS];
-  __shared__ uint32_t part[4][kRsCols];
-  __shared__ uint32_t s_prefix[kRsCols];
-  __shared__ int s_rank[kRsCols];
-  __shared__ int nan_row[kRsCols];
-  const int t = threadIdx.x, c = t & (kRsCols - 1), q = t >> 6;
-  const int64_t col = int64_t(blockIdx.x) * kRsCols + c;
-  const int64_t colc = col < N ? col : N - 1;  // columns past the end recompute the last one
-  if (q == 0) {
-    nan_row[c] = K;
-    s_prefix[c] = 0;
-    s_rank[c] = (K - 1) / 2;
-  }
-  uint32_t pmask = 0;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int i = t; i < kRsCols * HS; i += 256) hist[i] = 0;
-    __syncthreads();
-    const uint32_t prefix = s_prefix[c];
-    int first_nan = K;
-    int r = q;
-    for (; r + 12 < K; r += 16) {  // 4 rows in flight per lane
-      typename E::S x[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load(as_global(src[r + 4 * u]) + colc);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float v = E::widen(x[u]);
-        const uint32_t k = f32_order_key(__float_as_uint(v));
-        if (shift == 24 && E::raw_nan(x[u]) && first_nan == K) first_nan = r + 4 * u;
-        if ((k & pmask) == prefix) atomicAdd(&hist[c * HS + ((k >> shift) & 0xffu)], 1u);
-      }
-    }
-    for (; r < K; r += 4) {
-      const typename E::S x = __builtin_nontemporal_load(as_global(src[r]) + colc);
-      const uint32_t k = f32_order_key(__float_as_uint(E::widen(x)));
-      if (shift == 24 && E::raw_nan(x) && first_nan == K) first_nan = r;
-      if ((k & pmask) == prefix) atomicAdd(&hist[c * HS + ((k >> shift) & 0xffu)], 1u);
-    }
-    if (first_nan < K) atomicMin(&nan_row[c], first_nan);
-    __syncthreads();
-    // lane (c, q) owns bins [64q, 64q + 64) of column c
-    uint32_t own = 0;
-    for (int b = 0; b < 64; ++b) own += hist[c * HS + 64 * q + b];
-    part[q][c] = own;
-    __syncthreads();
-    const int rank = s_rank[c];
-    int below = 0;
-    for (int j = 0; j < q; ++j) below += int(part[j][c]);
-    if (below <= rank && rank < below + int(own)) {  // exactly one q per column
-      int b = 0;
-      for (; b < 63; ++b) {
-        const int h = int(hist[c * HS + 64 * q + b]);
-        if (below + h > rank) break;
-        below += h;
-      }
-      s_prefix[c] = prefix | (uint32_t(64 * q + b) << shift);
-      s_rank[c] = rank - below;
-    }
-    pmask |= 0xffu << shift;
-    __syncthreads();
-  }
-  if (q == 0 && col < N) {
-    const int nr = nan_row[c];
-    out[col] = nr < K ? as_global(src[nr])[col] : E::narrow(__uint_as_float(f32_from_order_key(s_prefix[c])));
-  }
-}
-
-template <class E>
-int launch_median_radix_stream(const typename E::S* const* src, int K, int64_t N, typename E::S* out, hipStream_t st) {
-  const int64_t grid = (N + kRsCols - 1) / kRsCols;
-  if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
-  hipLaunchKernelGGL((median_radix_stream_kernel<E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K, N, out);
-  return check_launch("fedagg_median");
-}
-
-// ---------------------------------------------------------------------------
 // fp32 -> bf16 / f16 rounding of a reduced shard (the client-axis multi-GPU
 // mode accumulates bf16 clients in fp32 and rounds once, after the exchange).
 
@@ -2366,50 +1476,6 @@ int launch_multi(const void* const* d_src, void* const* d_out, const int64_t* d_
 }
 }  // namespace
 
-namespace {
-
-template <class E>
-int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typename E::S* d_out, bool aligned,
-                    hipStream_t st) {
-  if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
-    if constexpr (sizeof(typename E::S) == 2) {
-      if (aligned && K <= 4096) {  // two columns per lane on packed int16 keys
-        if (K <= 256) return launch_median_pk16_lanes<4, 64, E>(d_src, K, N, d_out, st);
-        if (K <= 512) return launch_median_pk16_lanes<4, 128, E>(d_src, K, N, d_out, st);
-        if (K <= 1024) return launch_median_pk16_lanes<8, 128, E>(d_src, K, N, d_out, st);
-        if (K <= 2048) return launch_median_pk16_lanes<16, 128, E>(d_src, K, N, d_out, st);
-        return launch_median_pk16_lanes<32, 128, E>(d_src, K, N, d_out, st);
-      }
-    }
-    if (K <= 256) return launch_median_lanes<4, 64, E>(d_src, K, N, d_out, st);  // 1.1 ms vs 1.4 for <2, 128> (4M cols)
-    if (K <= 512) return launch_median_lanes<4, 128, E>(d_src, K, N, d_out, st);
-    if (K <= 1024) return launch_median_lanes<8, 128, E>(d_src, K, N, d_out, st);
-    if (K <= 2048) return launch_median_lanes<16, 128, E>(d_src, K, N, d_out, st);
-    // 32 lanes per column pay off against the radix select only well inside
-    // their range (1M columns: 18.9 vs 18.7 ms at K = 2,049, 22.9 vs 35.4 ms
-    // at 4,096 in fp32; the packed 16-bit kernels win at every K, above)
-    if (K > 2560 && K <= 4096) return launch_median_lanes<32, 128, E>(d_src, K, N, d_out, st);
-    return launch_median_radix_stream<E>(d_src, K, N, d_out, st);  // no bound on K
-  }
-  if constexpr (sizeof(typename E::S) == 2) {
-    if (aligned) {  // two columns per lane on packed int16 keys
-      if (K <= 32) return launch_median_pk16<32, E>(d_src, K, N, d_out, st);
-      if (K <= 64) return launch_median_pk16<64, E>(d_src, K, N, d_out, st);
-      if (K <= 96) return launch_median_pk16<96, E>(d_src, K, N, d_out, st);
-      return launch_median_pk16<128, E>(d_src, K, N, d_out, st);
-    }
-  }
-  if (K <= 8) return launch_median<8, E>(d_src, K, N, d_out, st);
-  if (K <= 16) return launch_median<16, E>(d_src, K, N, d_out, st);
-  if (K <= 24) return launch_median<24, E>(d_src, K, N, d_out, st);
-  if (K <= 32) return launch_median<32, E>(d_src, K, N, d_out, st);
-  if (K <= 48) return launch_median<48, E>(d_src, K, N, d_out, st);
-  if (K <= 64) return launch_median<64, E>(d_src, K, N, d_out, st);
-  if (K <= 96) return launch_median<96, E>(d_src, K, N, d_out, st);
-  return launch_median<128, E>(d_src, K, N, d_out, st);
-}
-
-}  // namespace
 
 extern "C" {
 
@@ -2729,32 +1795,6 @@ int fedagg_lsa_reconstruct_f32(const int64_t* const* d_src, int32_t K, int64_t N
                                   reinterpret_cast<hipStream_t>(stream), "fedagg_lsa_reconstruct_f32");
 }
 
-int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K, int64_t N, void* d_out, uint32_t flags,
-                  fedagg_stream_t stream) {
-  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
-  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, "fedagg_median: K must be >= 1 and N >= 0");
-  if (!d_src || !d_out) return set_error(FEDAGG_EINVAL, "fedagg_median: null pointer");
-  if (N == 0) return FEDAGG_OK;
-  auto st = reinterpret_cast<hipStream_t>(stream);
-  switch (dtype) {
-    case FEDAGG_DT_F32:
-      return median_dispatch<MedF32>(reinterpret_cast<const float* const*>(d_src), K, N,
-                                     static_cast<float*>(d_out), aligned, st);
-    case FEDAGG_DT_BF16:
-      return median_dispatch<MedBF16>(reinterpret_cast<const uint16_t* const*>(d_src), K, N,
-                                      static_cast<uint16_t*>(d_out), aligned, st);
-    case FEDAGG_DT_F16:
-      return median_dispatch<MedF16>(reinterpret_cast<const uint16_t* const*>(d_src), K, N,
-                                     static_cast<uint16_t*>(d_out), aligned, st);
-    default:
-      return set_error(FEDAGG_EINVAL, "fedagg_median: dtype must be FEDAGG_DT_F32, _BF16 or _F16");
-  }
-}
-
-int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N, float* d_out, uint32_t flags,
-                      fedagg_stream_t stream) {
-  return fedagg_median(FEDAGG_DT_F32, reinterpret_cast<const void* const*>(d_src), K, N, d_out, flags, stream);
-}
 
 int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs, const int64_t* nbytes, int32_t n,
                      int32_t threads) {
