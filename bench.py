@@ -59,6 +59,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # element; the fp32 MFMA (v_mfma_f32_16x16x4_f32, the centred-Gram kernel) has the same 157.3 TF peak
 # (MI355X_MICROARCH.md, chip-level parameters)
 VALU_PEAK_TFLOPS = 157.3
+SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4
+VALU_HALF_RATE_CYCLES = 4  # min/max/med3/DPP wave64 issue cost per SIMD (profiles/r03/median_rsel/valu_rate_probe*.txt)
 LSA_PRIME, LSA_QBITS = 2 ** 15 - 19, 10  # the reference's example LightSecAgg config (fedml_config.yaml:58-59)
 
 CONFIGS = {
@@ -199,6 +202,18 @@ def load_traffic(config: str, mode: str, world: int, variant: str = ""):
     key = f"{config}:{mode if world > 1 else 'single'}" + (f":{variant}" if variant else "")
     try:
         return json.load(open(path)).get(key, {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def load_median_valu(config: str, mode: str, world: int, variant: str):
+    """Executed VALU instructions per wave and waves per launch of the median
+    kernel at this shape, from the committed SQ pass (profiles/median_valu.json,
+    tools/median_valu.py), or None."""
+    path = os.path.join(ROOT, "profiles", "median_valu.json")
+    key = f"{config}:{mode if world > 1 else 'single'}:{variant}"
+    try:
+        return json.load(open(path)).get(key)
     except (OSError, ValueError):
         return None
 
@@ -574,6 +589,20 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if a.op == "median":
+        # the sorting networks are VALU-bound above ~128 clients: their min / max /
+        # med3 / DPP ops issue at 4 cycles per wave64 instruction per SIMD
+        # (tools/valu_rate_probe.hip), so this is the share of the SIMDs' issue
+        # capacity the kernel's executed VALU instructions take
+        vv = load_median_valu(a.config, mode, world, variant)
+        if vv:
+            issue_ms = vv["valu_instr_per_wave"] * vv["waves_per_launch"] * VALU_HALF_RATE_CYCLES / (
+                SIMDS * CLOCK_GHZ * 1e9) * 1e3
+            line["roofline"]["valu"] = {
+                "bound": "valu issue (half-rate ops, 4 cycles per wave64 instruction per SIMD)",
+                "instr_per_wave": vv["valu_instr_per_wave"], "waves_per_launch": vv["waves_per_launch"],
+                "issue_ms_at_peak": round(issue_ms, 4), "frac": round(issue_ms / kern_ms, 4),
+                "source": "profiles/median_valu.json (SQ_INSTS_VALU / SQ_WAVES)"}
     if world > 1:
         # whole-job HBM rate: every rank's algorithmic bytes over the step time
         line["roofline"]["aggregate_gbps"] = round(hbm_all, 1)

@@ -13,6 +13,16 @@
 
 #include "../../include/fedagg.h"
 
+// A/B knob for tools/median_ab.py: 1 keeps the mirrored-pair merge (a lane
+// select per cross-lane step) in the packed 4-lane kernels
+#ifndef FEDAGG_PK16_MIRROR
+#define FEDAGG_PK16_MIRROR 0
+#endif
+// reversed DPP reads issued per batch in lanes4_merge_median
+#ifndef FEDAGG_PK16_BATCH
+#define FEDAGG_PK16_BATCH 2
+#endif
+
 extern "C" int fedagg_set_error_internal(int code, const char* msg);
 
 namespace {
@@ -483,6 +493,10 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float x) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
 }
+template <int CTRL>
+__device__ __forceinline__ short2_t dpp_mov(short2_t x) {
+  return __builtin_bit_cast(short2_t, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
 template <int M>
 constexpr int dpp_xor_ctrl() {
   static_assert(M == 1 || M == 2 || M == 3 || M == 7 || M == 15, "lane xor pattern without a single DPP mov");
@@ -551,6 +565,55 @@ __device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
     lane_bitonic_merge(v);
     lanes_merge_levels<G * 2, P, R>(v, sub);
   }
+}
+
+// Four lanes per column (P = 4), odd lanes in the reversed order
+// (complemented int16 keys), every lane's run sorted ascending in its own
+// order.  Lanes 2q and 2q + 1 hold runs A (ascending) and B (descending
+// in the true order), so A and B form a bitonic sequence whose half-cleaner
+// pairs register i with register i: the even lane keeps min(a, b) and the odd
+// lane max(a, b), which in its reversed order is min(own, rev(partner)) too.
+// An in-lane half-cleaner cascade then sorts each lane.  Lanes 0 and 1 now
+// hold the sorted 2R-run X (lane 0 ascending, lane 1 descending), lanes 2
+// and 3 the run Y.  The 2R smallest of X and Y are min(X[i], Y[2R-1-i]),
+// i.e. lane 0's register i against lane 3's register i and lane 2's against
+// lane 1's: the lower median is the max of min(own, rev(partner ^ 3)) over
+// lanes 0 and 2 (lanes 1 and 3 compute the same expression, unused).
+// Per register: one v_not_b32_dpp and one v_pk_min_i16 per level, against a
+// DPP mov, v_pk_min, v_pk_max and a lane select before.  (fp32 keeps the
+// mirrored pairing: a negated DPP read cannot fuse into an IEEE min there,
+// and its min-or-max is already one v_med3 against ±inf.)
+__device__ __forceinline__ short2_t lanes_rev(short2_t x) { return ~x; }
+__device__ __forceinline__ short2_t lanes_min(short2_t a, short2_t b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ short2_t lanes_max(short2_t a, short2_t b) { return __builtin_elementwise_max(a, b); }
+
+template <class T, int R>
+__device__ __forceinline__ T lanes4_merge_median(T (&v)[R]) {
+  constexpr int B = FEDAGG_PK16_BATCH;  // reversed reads in batches: none right behind its register's write
+#pragma unroll
+  for (int i0 = 0; i0 < R; i0 += B) {
+    T t[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) t[k] = lanes_rev(dpp_mov<dpp_xor_ctrl<1>()>(v[i0 + k]));
+#pragma unroll
+    for (int k = 0; k < B; ++k) v[i0 + k] = lanes_min(v[i0 + k], t[k]);
+  }
+#pragma unroll
+  for (int d = R / 2; d > 0; d /= 2) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if ((i & d) == 0) cmpx(v[i], v[i + d]);
+  }
+  T m = lanes_min(v[0], lanes_rev(dpp_mov<dpp_xor_ctrl<3>()>(v[0])));
+#pragma unroll
+  for (int i0 = 0; i0 < R; i0 += B) {
+    T t[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) t[k] = lanes_rev(dpp_mov<dpp_xor_ctrl<3>()>(v[i0 + k]));
+#pragma unroll
+    for (int k = (i0 == 0); k < B; ++k) m = lanes_max(m, lanes_min(v[i0 + k], t[k]));
+  }
+  return lanes_max(m, dpp_mov<dpp_xor_ctrl<2>()>(m));  // lane 0: its max and lane 2's
 }
 
 template <int P, int R, bool FULL, class E = MedF32, int BS = 256>
@@ -666,10 +729,6 @@ int launch_median_lanes(const typename E::S* const* src, int K, int64_t N, typen
 // its first NaN in client order, per half.  An odd last column runs as the
 // TAIL instantiation: one block whose every column group recomputes the
 // duplicated lone column, and lane 0 stores it.
-template <int CTRL>
-__device__ __forceinline__ short2_t dpp_mov(short2_t x) {
-  return __builtin_bit_cast(short2_t, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
-}
 template <int M>
 __device__ __forceinline__ short2_t xor_mov(short2_t x) {
   if constexpr (dpp_xor_ok<M>()) return dpp_mov<dpp_xor_ctrl<M>()>(x);
@@ -787,17 +846,28 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   short2_t v[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) v[j] = pk16_key(raw[j]);
-  pairwise_sort<R>(v);
-  pk_lanes_merge_levels<2, P, R>(v, sub);
-  // last level: the lower P/2 lanes keep the KMAX/2 smallest keys per half
-  pk_lanes_reverse_pair<P - 1>(v, (sub & (P / 2)) != 0);
-  short2_t m = v[0];
+  short2_t m;
+  if constexpr (P == 4 && !FEDAGG_PK16_MIRROR) {
+    // odd lanes hold complemented keys (~k reverses the int16 order): every
+    // cross-lane step is min(own, ~partner) in every lane (lanes4_merge_median)
+    const short2_t flip = (sub & 1) ? short2_t(short(-1)) : short2_t(short(0));
 #pragma unroll
-  for (int i = 1; i < R; ++i) m = __builtin_elementwise_max(m, v[i]);
-  if constexpr (P >= 4) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
-  if constexpr (P >= 8) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
-  if constexpr (P >= 16) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima
-  if constexpr (P >= 32) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<15>()>(m));  // row halves
+    for (int j = 0; j < R; ++j) v[j] ^= flip;
+    pairwise_sort<R>(v);
+    m = lanes4_merge_median(v);
+  } else {
+    pairwise_sort<R>(v);
+    pk_lanes_merge_levels<2, P, R>(v, sub);
+    // last level: the lower P/2 lanes keep the KMAX/2 smallest keys per half
+    pk_lanes_reverse_pair<P - 1>(v, (sub & (P / 2)) != 0);
+    m = v[0];
+#pragma unroll
+    for (int i = 1; i < R; ++i) m = __builtin_elementwise_max(m, v[i]);
+    if constexpr (P >= 4) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<1>()>(m));
+    if constexpr (P >= 8) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<2>()>(m));
+    if constexpr (P >= 16) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima
+    if constexpr (P >= 32) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<15>()>(m));  // row halves
+  }
   uint32_t bits = pk16_bits(m);
   if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
   if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
