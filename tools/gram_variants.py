@@ -1,0 +1,108 @@
+"""A/B of compile-time variants of the centred-Gram Krum kernel (tool only).
+
+    python tools/gram_variants.py --build      # CPU container: tools/_build/robust_<tag>.so
+    python tools/gram_variants.py --rounds 9   # GPU box
+
+Each variant is csrc/robust.hip built standalone with its -D flags (plus a
+stub for the error hook it takes from fedagg.hip).  fedagg_pairgram2_f32 at
+config 3 (128 clients x ResNet-50's weights, base + 0.01 noise per client as
+bench.py), variants interleaved in one process, HIP events on the launch
+stream, outputs compared bit for bit.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tools", "_build")
+# tag -> -D flags of the knobs under test (none are left in robust.hip: the
+# round-3 probes of a swizzled 72-float LDS row and of block-pipelined
+# fragment reads were bit-identical and slower, 5.97 and 8.49 ms against
+# 5.79 ms; profiles/r03/dist/gram_variants.txt).  Extra variants: --variant
+# TAG=-DFLAG=V,-DFLAG2=V2
+VARIANTS = {"same": []}
+STUB = 'extern "C" int fedagg_set_error_internal(int code, const char*) { return code; }\n'
+
+
+def build() -> None:
+    from fedml_amd import build as fb
+
+    os.makedirs(OUT, exist_ok=True)
+    stub = os.path.join(OUT, "stub.cpp")
+    open(stub, "w").write(STUB)
+    src = os.path.join(ROOT, "fedml_amd", "csrc", "robust.hip")
+    procs = [subprocess.Popen([fb.hipcc(), *fb.HIPCC_FLAGS, *flags, "-shared", "-o",
+                               os.path.join(OUT, f"robust_{tag}.so"), src, stub]) for tag, flags in VARIANTS.items()]
+    assert all(p.wait() == 0 for p in procs)
+
+
+def bench(rounds: int, out_path: str) -> None:
+    import torch
+
+    from fedml_amd import _native as nat
+    from fedml_amd import defense as dfn
+    from fedml_amd import shapes
+    from fedml_amd.bucket import ClientBucket
+
+    dev = torch.device("cuda:0")
+    K = 128
+    b = ClientBucket(shapes.resnet50(), K, dev)
+    g = b.groups[torch.float32]
+    gen = torch.Generator(device=dev).manual_seed(0)
+    base = torch.randn(g.rows.shape[1], generator=gen, device=dev) * 0.05
+    for i in range(K):
+        g.rows[i].copy_(base + 0.01 * torch.randn(g.rows.shape[1], generator=gen, device=dev))
+    del base
+    chunks, n_chunks = dfn.weight_chunks(g, nat.DIST_CHUNK, dev)
+    work = dfn._work(nat.WORK_PAIRGRAM, K, n_chunks, dev)
+    st = nat.stream_handle()
+    libs = {"shipped": nat.lib()}
+    for tag in VARIANTS:
+        libs[tag] = ctypes.CDLL(os.path.join(OUT, f"robust_{tag}.so"))
+    outs = {t: torch.empty((K, K), dtype=torch.float64, device=dev) for t in libs}
+    times = {t: [] for t in libs}
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tags = list(libs)
+    for r in range(rounds + 1):
+        order = tags[r % len(tags):] + tags[:r % len(tags)]
+        for tag in order:
+            lib = libs[tag]
+            ev0.record()
+            rc = lib.fedagg_pairgram2_f32(ctypes.c_void_p(g.d_ptrs.data_ptr()), K, ctypes.c_void_p(chunks.data_ptr()),
+                                          ctypes.c_int64(n_chunks), ctypes.c_void_p(outs[tag].data_ptr()),
+                                          ctypes.c_void_p(work.data_ptr()), ctypes.c_int64(work.numel()),
+                                          ctypes.c_void_p(st))
+            ev1.record()
+            ev1.synchronize()
+            assert rc == 0, tag
+            if r:
+                times[tag].append(ev0.elapsed_time(ev1))
+    res = {"K": K, "n_chunks": int(n_chunks), "variants": VARIANTS}
+    for tag in tags:
+        res[tag] = {"ms": round(statistics.median(times[tag]), 4),
+                    "identical_to_shipped": bool(torch.equal(outs[tag], outs["shipped"]))}
+        print(tag, res[tag], flush=True)
+    json.dump(res, open(out_path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--rounds", type=int, default=9)
+    ap.add_argument("--out", default="gpurun_out/gram_variants.json")
+    ap.add_argument("--variant", action="append", default=[], help="TAG=-DFLAG=V[,-DFLAG2=V2]")
+    a = ap.parse_args()
+    for v in a.variant:
+        tag, flags = v.split("=", 1)
+        VARIANTS[tag] = flags.split(",")
+    if a.build:
+        build()
+    else:
+        bench(a.rounds, a.out)
