@@ -24,7 +24,8 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
 # round 3: FEDAGG_PK16_MIRROR / FEDAGG_PK16_BATCH (profiles/r03/median_rsel/median_ab_pk16_merge.json); a
 # 2-lanes-per-column split of 97..128 clients was 1.3-1.4x slower and was removed
-# (median_ab_split128.json); MEDIAN_AB_VARIANTS="tag=-DX=1,-DY=2;tag2=..." sets the variants
+# (median_ab_split128.json), so was sorting a K <= 128 column in two loaded-then-sorted halves
+# (median_ab_halves.json); MEDIAN_AB_VARIANTS="tag=-DX=1,-DY=2;tag2=..." sets the variants
 VARIANTS = {"new": ["-DFEDAGG_PK16_MIRROR=0"], "mirror": ["-DFEDAGG_PK16_MIRROR=1"]}
 if os.environ.get("MEDIAN_AB_VARIANTS"):
     VARIANTS = {t: f.split(",") if f else [] for t, f in
@@ -67,8 +68,7 @@ def main():
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}  # FEDAGG_DT_*
-    shapes = [(torch.float32, 128, 25_610_152), (torch.float32, 100, 25_610_152), (torch.bfloat16, 128, 86_567_656),
-              (torch.float16, 128, 4_000_036)]
+    shapes = [(torch.float32, 128, 25_610_152), (torch.float32, 100, 25_610_152), (torch.float32, 64, 25_610_152)]
     if os.environ.get("MEDIAN_AB_SHAPES") == "k512":
         shapes = [(torch.float16, 512, 4_000_036), (torch.bfloat16, 512, 4_000_036), (torch.bfloat16, 300, 4_000_036),
                   (torch.bfloat16, 256, 4_000_036), (torch.float16, 512, 4_000_036), (torch.bfloat16, 512, 86_567_656)]
