@@ -30,7 +30,10 @@ count (strong scaling, ``--clients-total``, default the config's K):
 Prints ONE JSON line on rank 0 (contract in the task statement); at N = 1 the
 cpu_baseline leg times the reference's own CPU loop (oracle/cpu_baseline.py)
 over the FULL workload (every key, every client) at the job's CPU quota and
-at one thread.
+at one thread.  `--op median` lines also carry roofline.valu: the median's
+sorting networks are bound by VALU issue above ~128 clients, so the executed
+VALU instructions of its kernel (profiles/median_valu.json, an SQ pass) at 4
+cycles per wave64 instruction per SIMD are set against the kernel time.
 """
 from __future__ import annotations
 
