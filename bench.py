@@ -184,7 +184,7 @@ def cpu_baseline(bucket, ns, reps: int) -> dict:
 
 def median_kernel_name(K: int, dt) -> str:
     """The kernel fedagg_median dispatches for K clients of aligned rows
-    (median_dispatch in csrc/fedagg.hip)."""
+    (median_dispatch in csrc/median.hip)."""
     name = str(dt).replace("torch.", "")
     packed = dt in (torch.bfloat16, torch.float16)
     if K <= 128:
