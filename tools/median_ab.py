@@ -68,7 +68,8 @@ def main():
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}  # FEDAGG_DT_*
-    shapes = [(torch.float32, 128, 25_610_152), (torch.float32, 100, 25_610_152), (torch.float32, 64, 25_610_152)]
+    shapes = [(torch.bfloat16, 512, 4_000_036), (torch.bfloat16, 300, 4_000_036), (torch.bfloat16, 256, 4_000_036),
+              (torch.float16, 512, 4_000_036), (torch.bfloat16, 512, 86_567_656)]
     if os.environ.get("MEDIAN_AB_SHAPES") == "k512":
         shapes = [(torch.float16, 512, 4_000_036), (torch.bfloat16, 512, 4_000_036), (torch.bfloat16, 300, 4_000_036),
                   (torch.bfloat16, 256, 4_000_036), (torch.float16, 512, 4_000_036), (torch.bfloat16, 512, 86_567_656)]
