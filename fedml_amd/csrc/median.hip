@@ -22,6 +22,14 @@
 #ifndef FEDAGG_PK16_BATCH
 #define FEDAGG_PK16_BATCH 2
 #endif
+// Loads of the lane-group kernels: a wave instruction reads 64 B of each of P
+// rows' 128-B lines and the block's next wave reads the other half, so plain
+// loads (0) keep the line in L2 for it; non-temporal ones (1) fetched 1.04-1.5x
+// the algorithmic bytes vs 1.00-1.03x, at the same time
+// (profiles/r03/lanes_nt/)
+#ifndef FEDAGG_LANES_NT
+#define FEDAGG_LANES_NT 0
+#endif
 
 extern "C" int fedagg_set_error_internal(int code, const char* msg);
 
@@ -40,6 +48,15 @@ int check_launch(const char* what) {
 template <class T>
 __device__ __forceinline__ const T __attribute__((address_space(1)))* as_global(const T* p) {
   return (const T __attribute__((address_space(1)))*)(p);
+}
+
+// loads of the lane-group kernels (FEDAGG_LANES_NT)
+template <class T>
+__device__ __forceinline__ T lanes_load(const T __attribute__((address_space(1)))* p) {
+  if constexpr (FEDAGG_LANES_NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
 }
 
 // ---------------------------------------------------------------------------
@@ -655,7 +672,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
     const int q = sub * (R + PAD) + j;
     const uint64_t off = FULL ? boff : (boff & offmask[q]);
     const auto row = reinterpret_cast<const char*>(rows[q]);
-    v[j] = E::widen(__builtin_nontemporal_load(as_global(reinterpret_cast<const S*>(row + off))));
+    v[j] = E::widen(lanes_load(as_global(reinterpret_cast<const S*>(row + off))));
   }
   __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test (see median_kernel)
 #pragma unroll
@@ -818,7 +835,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
     if constexpr (TAIL)
       raw[j] = uint32_t(*as_global(reinterpret_cast<const uint16_t*>(row + off))) * 0x10001u;
     else
-      raw[j] = __builtin_nontemporal_load(as_global(reinterpret_cast<const uint32_t*>(row + off)));
+      raw[j] = lanes_load(as_global(reinterpret_cast<const uint32_t*>(row + off)));
   }
   __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test
   uint32_t nanacc = 0;  // per half, max of |x| bits

@@ -73,6 +73,11 @@ def main():
     if os.environ.get("MEDIAN_AB_SHAPES") == "k512":
         shapes = [(torch.float16, 512, 4_000_036), (torch.bfloat16, 512, 4_000_036), (torch.bfloat16, 300, 4_000_036),
                   (torch.bfloat16, 256, 4_000_036), (torch.float16, 512, 4_000_036), (torch.bfloat16, 512, 86_567_656)]
+    if os.environ.get("MEDIAN_AB_SHAPES") == "lanes":  # both lane-group kernels (fp32 and packed 16-bit)
+        shapes = [(torch.float32, 512, 4_000_037), (torch.bfloat16, 512, 4_000_036), (torch.float32, 300, 4_000_037),
+                  (torch.bfloat16, 256, 4_000_036), (torch.bfloat16, 512, 86_567_656)]
+    shapes = [sh for sh in shapes if sh[2] <= int(os.environ.get("MEDIAN_AB_MAXN", "1000000000"))]
+    reps = int(os.environ.get("MEDIAN_AB_REPS", "22"))
     res = []
     for dtype, K, N in shapes:
         L = (N + 63) // 64 * 64
@@ -85,7 +90,7 @@ def main():
         tab = kn.upload_i64([rows[i].data_ptr() for i in range(K)], dev)
         outs = {t: torch.empty(L, dtype=dtype, device=dev) for t in libs}
         ts = {t: [] for t in libs}
-        for rep in range(22):
+        for rep in range(reps):
             order = list(libs.items())
             order = order[rep % len(order):] + order[:rep % len(order)]  # rotate who goes first
             for t, lib in order:
@@ -95,10 +100,11 @@ def main():
                 e1.record()
                 e1.synchronize()
                 assert rc == 0, (t, rc)
-                if rep >= 2:
+                if rep >= min(2, reps - 1):
                     ts[t].append(e0.elapsed_time(e1))
         tags = list(libs)
-        same = all(torch.equal(outs[tags[0]][:N].view(torch.int16), outs[t][:N].view(torch.int16)) for t in tags[1:])
+        iv = torch.int32 if dtype == torch.float32 else torch.int16
+        same = all(torch.equal(outs[tags[0]][:N].view(iv), outs[t][:N].view(iv)) for t in tags[1:])
         nbytes = (K + 1) * N * rows.element_size()
         r = {"dtype": str(dtype).replace("torch.", ""), "K": K, "N": N, "identical": bool(same)}
         for t in tags:
