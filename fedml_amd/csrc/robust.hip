@@ -42,6 +42,10 @@
 #ifndef FEDAGG_DIST2_REF_NT
 #define FEDAGG_DIST2_REF_NT false
 #endif
+// client rows of dist2: non-temporal (true) or plain loads
+#ifndef FEDAGG_DIST2_X_NT
+#define FEDAGG_DIST2_X_NT true
+#endif
 
 extern "C" int fedagg_set_error_internal(int code, const char* msg);
 
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(kBS) void dist2_kernel(const float* const* __restri
         const int i = cb + w + kWaves * j;
         if (i < K) {  // wave-uniform
           f32x4 x[kLaneCols / 4];
-          load_chunk(src[i] + start, len, lane, x);
+          load_chunk<FEDAGG_DIST2_X_NT>(src[i] + start, len, lane, x);
 #pragma unroll
           for (int u = 0; u < kLaneCols / 4; ++u) {
             acc[j] = sq_diff(x[u].x, r[u].x, acc[j]);

@@ -134,6 +134,26 @@ def test_weight_chunks_skip_buffers_and_split():
     assert (t[:, 1] <= 2048).all() and (t[:, 1] > 0).all()
 
 
+@pytest.mark.parametrize("chunk", [8, 64, 2048])
+def test_weight_chunks_absolute_cuts(chunk):
+    """dist2's table: the same columns, cut at multiples of `chunk` in the row
+    (only a run's first piece may start elsewhere), in order, none empty."""
+    layout = RowLayout([("a.weight", (3, 501), torch.float32), ("bn.weight", (7,), torch.float32),
+                        ("bn.running_mean", (7,), torch.float32), ("bn.num_batches_tracked", (), torch.int64),
+                        ("fc.weight", (4097,), torch.float32), ("fc.bias", (5,), torch.float32)], True)
+    g = layout.groups[torch.float32]
+    t = dfn.weight_chunks(g, chunk, torch.device("cpu"), absolute=True)[0].view(-1, 2).numpy()
+    cols = np.concatenate([np.arange(s, s + l) for s, l in t])
+    want = np.concatenate([np.arange(o, o + m) for k, o, m in zip(g.keys, g.offsets, g.numels)
+                           if dfn.is_weight_param(k)])
+    np.testing.assert_array_equal(cols, want)
+    assert (t[:, 1] > 0).all() and (t[:, 1] <= chunk).all()
+    run_first = np.r_[True, t[1:, 0] != t[:-1, 0] + t[:-1, 1]]
+    assert (t[~run_first, 0] % chunk == 0).all()
+    # a piece never crosses a multiple of chunk
+    assert ((t[:, 0] // chunk) == ((t[:, 0] + t[:, 1] - 1) // chunk)).all()
+
+
 def test_abi_argument_checks():
     fbuild = pytest.importorskip("fedml_amd.build")
     fbuild.build()

@@ -23,6 +23,9 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_build")
 VARIANTS = {"clip1": ["-DFEDAGG_CLIP_CLIENTS=1"], "clip4": ["-DFEDAGG_CLIP_CLIENTS=4"],
             "d16nt": ["-DFEDAGG_DIST2_REF_NT=true"], "d32": ["-DFEDAGG_DIST2_BATCH=32"]}
+if os.environ.get("ROBUST_VARIANTS"):  # "tag=-DX=1,-DY=2;tag2=..."
+    VARIANTS = {t: f.split(",") if f else [] for t, f in
+                (v.split("=", 1) for v in os.environ["ROBUST_VARIANTS"].split(";"))}
 STUB = 'extern "C" int fedagg_set_error_internal(int code, const char*) { return code; }\n'
 
 
@@ -60,7 +63,7 @@ def bench(rounds: int) -> None:
     d_dst = kn.upload_i64([out[i].data_ptr() for i in range(K)], dev)
     d_div = kn.upload_f32([1.0 + 0.01 * (i % 3) for i in range(K)], dev)
     st = nat.stream_handle()
-    libs = {"shipped": nat.lib()}
+    libs = {} if os.environ.get("ROBUST_NO_SHIPPED") else {"shipped": nat.lib()}
     for tag in VARIANTS:
         libs[tag] = ctypes.CDLL(os.path.join(OUT, f"robust_{tag}.so"))
     want = None
@@ -100,7 +103,7 @@ def bench(rounds: int) -> None:
     # dist2 (every client's distance to a reference row), all builds
     from fedml_amd import defense as dfn
 
-    chunks, n_chunks = dfn.weight_chunks(g, nat.DIST_CHUNK, dev)
+    chunks, n_chunks = dfn.weight_chunks(g, nat.DIST_CHUNK, dev, absolute=True)
     d_out = torch.empty(K, dtype=torch.float64, device=dev)
     work = dfn._work(nat.WORK_DIST2, K, n_chunks, dev)
     n_w = sum(n for k, n in zip(g.keys, g.numels) if dfn.is_weight_param(k))
