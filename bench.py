@@ -401,7 +401,7 @@ def main():
                 gd.d_ptrs.data_ptr(), K, chunks.data_ptr(), n_chunks, pd_out.data_ptr(), work.data_ptr(),
                 work.numel(), nat.stream_handle())
         elif a.op == "dist2":
-            chunks, n_chunks = dfn.weight_chunks(gd, nat.DIST_CHUNK, dev, absolute=True)
+            chunks, n_chunks = dfn.weight_chunks(gd, nat.DIST_CHUNK, dev)
             d_out = torch.empty(K, dtype=torch.float64, device=dev)
             work = dfn._work(nat.WORK_DIST2, K, n_chunks, dev)
             call = lambda: nat.lib().fedagg_dist2_f32(  # noqa: E731

@@ -188,15 +188,17 @@ def trimmed_mean_before_aggregation(raw_client_grad_list: Sequence, beta: float)
 
 # ---- distance-based defenses (csrc/robust.hip) ---------------------------------
 
-def weight_chunks(group, chunk: int, device, absolute: bool = False) -> Tuple[torch.Tensor, int]:
+def weight_chunks(group, chunk: int, device, absolute: bool = True) -> Tuple[torch.Tensor, int]:
     """Device (start, length) table of a row group's weight-key columns, runs
     of adjacent keys merged, split into pieces of at most `chunk` columns.
 
-    absolute: cut at multiples of `chunk` in the row (a run's first piece is
-    shorter), so pieces after the first start on whole cache lines.  dist2
-    hands consecutive pieces to blocks on different XCDs; runs cut from their
-    16-byte aligned start made every boundary line a fetch for both blocks
-    (1.036x the algorithmic bytes at config 3, 1/32 per misaligned run)."""
+    absolute (default): cut at multiples of `chunk` in the row (a run's first
+    piece is shorter), so pieces after the first start on whole cache lines.
+    The kernels hand consecutive pieces to blocks on different XCDs; runs cut
+    from their 16-byte aligned start made every boundary line a fetch for
+    both blocks: dist2 at 1.036x the algorithmic bytes (1.009x now), Krum's
+    Gram 5.58 ms (5.39 now) at config 3.  False: cuts from each run's start
+    (tools' A/B baseline)."""
     segs = []
     for key, off, n in zip(group.keys, group.offsets, group.numels):
         if n == 0 or not is_weight_param(key):
@@ -344,7 +346,7 @@ def norm_diff_clipping_before_aggregation(raw_client_grad_list: Sequence, global
         gb.put(0, {k: global_model[k] for k in wkeys}, 1)
         gb.sync_ingest()
         ref = gb.groups[torch.float32].rows[0]
-        chunks, n_chunks = weight_chunks(g, nat.DIST_CHUNK, dev, absolute=True)
+        chunks, n_chunks = weight_chunks(g, nat.DIST_CHUNK, dev)
         sq = dist2_rows(g.d_ptrs, K, ref, chunks, n_chunks, dev).cpu().numpy()
         divs = [max(1, fp32_norm(s) / norm_bound) for s in sq]  # _get_clipped_norm_diff
         d_div = kn.upload_f32(divs, dev)
@@ -480,7 +482,7 @@ def cclip_before_aggregation(raw_client_grad_list: Sequence, tau: float, bucket_
         guess_idx = np.random.randint(0, B)  # _compute_an_initial_guess (:61-62), the global numpy RNG
         guess = means[guess_idx]
         m_ptrs = kn.upload_i64([means[b].data_ptr() for b in range(B)], dev)
-        chunks, n_chunks = weight_chunks(g, nat.DIST_CHUNK, dev, absolute=True)
+        chunks, n_chunks = weight_chunks(g, nat.DIST_CHUNK, dev)
         sq = dist2_rows(m_ptrs, B, guess, chunks, n_chunks, dev).cpu().numpy()
         scores = [min(1, tau / (fp32_norm(v) + 1e-8)) for v in sq]  # _compute_cclip_score (:64-71)
         d_sc = kn.upload_f32([float(x) for x in scores], dev)

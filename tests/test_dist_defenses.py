@@ -124,7 +124,7 @@ def test_weight_chunks_skip_buffers_and_split():
                         ("bn.running_mean", (7,), torch.float32), ("bn.num_batches_tracked", (), torch.int64),
                         ("fc.weight", (4097,), torch.float32)], True)
     g = layout.groups[torch.float32]
-    tab, n = dfn.weight_chunks(g, 2048, torch.device("cpu"))
+    tab, n = dfn.weight_chunks(g, 2048, torch.device("cpu"), absolute=False)
     t = tab.view(-1, 2).numpy()
     assert n == len(t)
     cols = np.concatenate([np.arange(s, s + l) for s, l in t])
@@ -136,13 +136,13 @@ def test_weight_chunks_skip_buffers_and_split():
 
 @pytest.mark.parametrize("chunk", [8, 64, 2048])
 def test_weight_chunks_absolute_cuts(chunk):
-    """dist2's table: the same columns, cut at multiples of `chunk` in the row
+    """The default table: the same columns, cut at multiples of `chunk` in the row
     (only a run's first piece may start elsewhere), in order, none empty."""
     layout = RowLayout([("a.weight", (3, 501), torch.float32), ("bn.weight", (7,), torch.float32),
                         ("bn.running_mean", (7,), torch.float32), ("bn.num_batches_tracked", (), torch.int64),
                         ("fc.weight", (4097,), torch.float32), ("fc.bias", (5,), torch.float32)], True)
     g = layout.groups[torch.float32]
-    t = dfn.weight_chunks(g, chunk, torch.device("cpu"), absolute=True)[0].view(-1, 2).numpy()
+    t = dfn.weight_chunks(g, chunk, torch.device("cpu"))[0].view(-1, 2).numpy()
     cols = np.concatenate([np.arange(s, s + l) for s, l in t])
     want = np.concatenate([np.arange(o, o + m) for k, o, m in zip(g.keys, g.offsets, g.numels)
                            if dfn.is_weight_param(k)])

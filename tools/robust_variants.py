@@ -103,7 +103,7 @@ def bench(rounds: int) -> None:
     # dist2 (every client's distance to a reference row), all builds
     from fedml_amd import defense as dfn
 
-    chunks, n_chunks = dfn.weight_chunks(g, nat.DIST_CHUNK, dev, absolute=True)
+    chunks, n_chunks = dfn.weight_chunks(g, nat.DIST_CHUNK, dev)
     d_out = torch.empty(K, dtype=torch.float64, device=dev)
     work = dfn._work(nat.WORK_DIST2, K, n_chunks, dev)
     n_w = sum(n for k, n in zip(g.keys, g.numels) if dfn.is_weight_param(k))
