@@ -30,6 +30,11 @@
 #ifndef FEDAGG_LANES_NT
 #define FEDAGG_LANES_NT 0
 #endif
+// Loads of the one-lane-per-column kernels (K <= 128; 256 B per wave
+// instruction): 1 non-temporal, 0 plain
+#ifndef FEDAGG_COLS_NT
+#define FEDAGG_COLS_NT 1
+#endif
 
 extern "C" int fedagg_set_error_internal(int code, const char* msg);
 
@@ -54,6 +59,14 @@ __device__ __forceinline__ const T __attribute__((address_space(1)))* as_global(
 template <class T>
 __device__ __forceinline__ T lanes_load(const T __attribute__((address_space(1)))* p) {
   if constexpr (FEDAGG_LANES_NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+// loads of the one-lane-per-column kernels (FEDAGG_COLS_NT)
+template <class T>
+__device__ __forceinline__ T cols_load(const T __attribute__((address_space(1)))* p) {
+  if constexpr (FEDAGG_COLS_NT)
     return __builtin_nontemporal_load(p);
   else
     return *p;
@@ -298,7 +311,7 @@ __global__ __launch_bounds__(BS) void median_kernel(const typename E::S* const* 
       row = live ? row_base(p, col0) : reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(p));
     else
       row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(p));
-    v[c] = E::widen(__builtin_nontemporal_load(
+    v[c] = E::widen(cols_load(
         reinterpret_cast<const typename E::S __attribute__((address_space(1)))*>(row + (live ? boff : 0u))));
     if constexpr (sizeof(typename E::S) == 2) E::nan_add(nacc, v[c]);
   }
@@ -406,7 +419,7 @@ __device__ __forceinline__ void median_pk16_pair(const uint16_t* const* __restri
       row = reinterpret_cast<const char __attribute__((address_space(1)))*>(as_global(src[ci]));
     uint32_t x;
     if constexpr (!TAIL)
-      x = __builtin_nontemporal_load(reinterpret_cast<const uint32_t __attribute__((address_space(1)))*>(row + boff));
+      x = cols_load(reinterpret_cast<const uint32_t __attribute__((address_space(1)))*>(row + boff));
     else  // the odd last column alone, duplicated into both halves
       x = *reinterpret_cast<const uint16_t __attribute__((address_space(1)))*>(row + boff) * 0x10001u;
     raw[c] = x;

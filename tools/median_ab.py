@@ -76,6 +76,9 @@ def main():
     if os.environ.get("MEDIAN_AB_SHAPES") == "lanes":  # both lane-group kernels (fp32 and packed 16-bit)
         shapes = [(torch.float32, 512, 4_000_037), (torch.bfloat16, 512, 4_000_036), (torch.float32, 300, 4_000_037),
                   (torch.bfloat16, 256, 4_000_036), (torch.bfloat16, 512, 86_567_656)]
+    if os.environ.get("MEDIAN_AB_SHAPES") == "cols":  # the one-lane-per-column kernels (K <= 128)
+        shapes = [(torch.float32, 128, 25_610_152), (torch.bfloat16, 128, 86_567_656), (torch.float32, 100, 25_610_152),
+                  (torch.bfloat16, 64, 86_567_656)]
     shapes = [sh for sh in shapes if sh[2] <= int(os.environ.get("MEDIAN_AB_MAXN", "1000000000"))]
     reps = int(os.environ.get("MEDIAN_AB_REPS", "22"))
     res = []
