@@ -9,14 +9,18 @@ Default workload = BASELINE.json config 3: 128 clients x ResNet-50 state dict
 (25,610,152 fp32 + 53 int64 elements per client), synthetic data generated
 in HBM.
 
-With --gpus N (one process per GPU) the round keeps the config's client
-count (strong scaling, ``--clients-total``, default the config's K):
+Every config keeps BASELINE.json's client count (4 / 32 / 128 / 512 / 64;
+`plan_clients`).  With --gpus N (one process per GPU) the round keeps it too
+(strong scaling, ``--clients-total``, default the config's K):
 
   --mode param (default)  every rank holds ITS KEYS of every client (whole
                           keys dealt to ranks by bytes, the same partition as
                           the in-process fedml_amd.multidev bucket) and
                           reduces them in the reference order: no exchange,
-                          bit-exact with one GPU.
+                          bit-exact with one GPU.  The same run then measures
+                          the client axis below on the same clients and nests
+                          it under "exchange" (north_star's RCCL
+                          reduce-scatter over xGMI; --no-exchange skips it).
   --mode client           every rank holds its K/N clients' whole updates,
                           computes an fp32 partial and joins one chunked RCCL
                           reduce-scatter (timed separately on the comm stream).
@@ -72,12 +76,12 @@ CONFIGS = {
     "cfg2": dict(model="cnn_web", K=32, desc="FedAvg 32 clients x LeNet CNN_WEB (62,006 params) fp32"),
     "cfg3": dict(model="resnet50", K=128,
                  desc="FedAvg 128 clients x ResNet-50 state dict (25,610,152 fp32 + 53 int64) fp32"),
-    "cfg4": dict(model="vit_b16", K=128, desc="FedAvg 128 clients/GPU x ViT-B/16 (86,567,656) bf16"),
+    "cfg4": dict(model="vit_b16", K=512, desc="FedAvg 512 clients x ViT-B/16 (86,567,656) bf16"),
     "cfg5": dict(model="llama2_7b_lora", K=64, desc="FedAvg 64 clients x Llama-2-7B LoRA r=8 q/v fp32"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -111,8 +115,41 @@ def parse():
                     help="1 GPU: clients per GPU instead of the config's (e.g. config 4's median over all 512 "
                          "clients: the median does not split along the client axis)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exchange", action="store_true",
+                    help="multi-GPU --mode param: skip the nested client-axis (RCCL reduce-scatter) measurement")
     ap.add_argument("--cpu-reps", type=int, default=5, help="cpu_baseline: timed runs after one warm-up")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def plan_clients(config: str, world: int, rank: int, mode: str, clients_total=None, weak: bool = False,
+                 clients=None):
+    """(K_total, K_loc, first): the round's clients over all ranks, this
+    rank's count and the index of its first client.  mode is "single" at one
+    GPU, else "param" (every rank holds its keys of ALL clients) or "client"
+    (clients dealt to ranks, the first K_total % world ranks one more)."""
+    K = CONFIGS[config]["K"]
+    if clients is not None:
+        if world > 1 or clients < 1:
+            raise SystemExit("--clients is a 1-GPU override (>= 1)")
+        K = clients
+    weak = weak and world > 1
+    if world > 1 and not weak:
+        K_total = clients_total if clients_total is not None else K
+        if K_total < 1:
+            raise SystemExit("--clients-total must be >= 1")
+    else:
+        K_total = K * world
+    if mode == "client" and not weak:
+        base_k, extra = divmod(K_total, world)
+        K_loc = base_k + (1 if rank < extra else 0)
+        first = rank * base_k + min(rank, extra)
+    elif mode == "client" or weak:
+        K_loc, first = K, rank * K
+    else:
+        K_loc, first = K_total, 0
+    if K_loc < 1:
+        raise SystemExit(f"rank {rank} would hold no clients: --clients-total {K_total} < --gpus {world}")
+    return K_total, K_loc, first
 
 
 def fill_rows(rows: torch.Tensor, length: int, seed: int, round_idx: int = 0) -> None:
@@ -133,14 +170,18 @@ def fill_rows(rows: torch.Tensor, length: int, seed: int, round_idx: int = 0) ->
     del base, eps
 
 
-def host_round(bucket) -> list:
+CPU_SAMPLE_BYTES = 13_400_000_000  # cpu_baseline: client bytes copied to the host (config 3 = 13.2 GB, all of it)
+
+
+def host_round(bucket, clients=None) -> list:
     """The bench's round as the reference's CPU server holds it: K pageable
     per-key host tensors per client (contiguous slices of one host copy of
-    each client's row; integer keys as int64 tensors), copied from HBM."""
+    each client's row; integer keys as int64 tensors), copied from HBM.
+    clients: the first this many slots (default all)."""
     from collections import OrderedDict
 
     raw = []
-    for i in range(bucket.capacity):
+    for i in range(bucket.capacity if clients is None else clients):
         d = OrderedDict()
         rows = {dt: g.rows[i, :g.length].cpu() for dt, g in bucket.groups.items()}
         for key, shape, dt in bucket.entries:
@@ -153,12 +194,18 @@ def host_round(bucket) -> list:
 
 def cpu_baseline(bucket, ns, reps: int) -> dict:
     """The reference's own CPU loop (agg_operator.py:35-44 in torch eager,
-    oracle/cpu_baseline.py) on the FULL workload: every key of the state dict,
-    all K clients, the same values as the HBM rows.  Median of `reps` runs
-    after one warm-up, at every CPU this job may use and at one thread."""
+    oracle/cpu_baseline.py) on every key of the state dict and the same values
+    as the HBM rows: all K clients while they fit CPU_SAMPLE_BYTES (config 3:
+    the FULL workload), else the first K' clients that do (config 4's 512 x
+    173 MB: a bounded sample; the unit is a rate, client-params/s).  Median of
+    `reps` runs after one warm-up, at every CPU this job may use and at one
+    thread."""
     from oracle import cpu_baseline as cb
 
-    raw = host_round(bucket)
+    row_bytes = sum(g.length * g.rows.element_size() for g in bucket.groups.values())
+    k_all = bucket.capacity
+    k_s = max(1, min(k_all, CPU_SAMPLE_BYTES // max(1, row_bytes)))
+    raw = host_round(bucket, k_s)
     raw = [(n, d) for n, (_, d) in zip(ns, raw)]
     cpus = cb.host_cpus()
     full = cb.time_fedavg(raw, reps=reps, threads=cpus["usable"])
@@ -168,7 +215,8 @@ def cpu_baseline(bucket, ns, reps: int) -> dict:
     del raw
     return {"value": K * n_elems / full["median_s"], "unit": "client-params/s", "cores": full["threads"],
             "kind": "port",
-            "sample": f"full workload: all {len(bucket.entries)} state-dict keys x {K} clients "
+            "sample": ("full workload" if K == k_all else f"bounded sample: the first {K} of {k_all} clients") +
+                      f": all {len(bucket.entries)} state-dict keys x {K} clients "
                       f"({n_elems:,} elements/client), torch-eager restatement of agg_operator.py:35-44, "
                       f"median of {reps} after 1 warm-up: {full['median_s'] * 1e3:.1f} ms/aggregation at "
                       f"{full['threads']} threads, {one['median_s'] * 1e3:.1f} ms at 1 thread",
@@ -197,28 +245,146 @@ def median_kernel_name(K: int, dt) -> str:
     return f"median_{'pk16_' if packed else ''}lanes_kernel<{p}, {r}> ({name})"
 
 
-def load_traffic(config: str, mode: str, world: int, variant: str = ""):
+def table_key(config: str, mode: str, world: int, variant: str, clients: int) -> str:
+    """Key of a measurement table entry: config, partitioning, variant and the
+    clients per GPU it was measured at, e.g. "cfg4:single@K512",
+    "cfg3:single:median@K128"."""
+    return f"{config}:{mode if world > 1 else 'single'}" + (f":{variant}" if variant else "") + f"@K{clients}"
+
+
+def load_traffic(config: str, mode: str, world: int, variant: str = "", clients: int = 128):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None.
     variant: "" for FedAvg, else the fused server step or the robust op."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    key = f"{config}:{mode if world > 1 else 'single'}" + (f":{variant}" if variant else "")
+    key = table_key(config, mode, world, variant, clients)
     try:
         return json.load(open(path)).get(key, {}).get("bytes_per_launch")
     except (OSError, ValueError):
         return None
 
 
-def load_median_valu(config: str, mode: str, world: int, variant: str):
+def load_median_valu(config: str, mode: str, world: int, variant: str, clients: int):
     """Executed VALU instructions per wave and waves per launch of the median
     kernel at this shape, from the committed SQ pass (profiles/median_valu.json,
     tools/median_valu.py), or None."""
     path = os.path.join(ROOT, "profiles", "median_valu.json")
-    key = f"{config}:{mode if world > 1 else 'single'}:{variant}"
+    key = table_key(config, mode, world, variant, clients)
     try:
         return json.load(open(path)).get(key)
     except (OSError, ValueError):
         return None
+
+
+def client_axis_step(bucket, dom_dt, w_local, chunks: int, world: int):
+    """The client-axis step over this rank's bucket: per dtype group the fp32
+    partial of its clients (global weights) and the chunked reduce-scatter,
+    16-bit models rounded once after the exchange.  Returns (step, launches
+    per step of the dominant group, its algorithmic bytes, xGMI bytes per rank)."""
+    aggs = {dt: ClientAxisAggregator(g.rows, g.length, chunks=chunks if dt == dom_dt else 1)
+            for dt, g in bucket.groups.items()}
+
+    def step(ev=None, cev=None):
+        for dt, agg in aggs.items():
+            agg.aggregate(w_local, events=ev if dt == dom_dt else None,
+                          comm_events=cev if dt == dom_dt else None)
+            if dt in (torch.bfloat16, torch.float16):
+                agg.shard_in_model_dtype()  # the one rounding of a 16-bit model, after the exchange
+
+    gd = bucket.groups[dom_dt]
+    dom_bytes = gd.rows.shape[0] * gd.length * gd.rows.element_size() + gd.length * 4  # rows in, fp32 partial out
+    xgmi_bytes = (world - 1) * aggs[dom_dt].piece * len(aggs[dom_dt].bounds) * 4
+    return step, len(aggs[dom_dt].bounds), dom_bytes, xgmi_bytes
+
+
+def run_timed(step, n_launch: int, steps: int, warmup: int, world: int, per_chunk: bool, timed_comm: bool):
+    """W untimed steps, then K timed steps between barrier + synchronize on
+    both sides.  Returns (elapsed s, MAX over ranks; kernel ms per step from
+    the HIP events on the launch stream; comm-stream ms per step or None)."""
+    def new_events(n):
+        return [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(n)]
+
+    for _ in range(warmup):
+        step()
+    evs = [new_events(n_launch) for _ in range(steps)]
+    cevs = [new_events(n_launch) for _ in range(steps)] if timed_comm else [None] * steps
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        # the client-axis steps take one (start, end) pair per chunk; the rest one pair
+        step(evs[s] if per_chunk else evs[s][0], cevs[s])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=torch.cuda.current_device(), dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(e0.elapsed_time(e1) for ev in evs for e0, e1 in ev) / steps  # per step
+    comm_ms = sum(e0.elapsed_time(e1) for ev in cevs for e0, e1 in ev) / steps if timed_comm else None
+    return elapsed, kern_ms, comm_ms
+
+
+def reduce_rates(achieved: float, hbm_all: float, comm_ms, world: int, dev):
+    """Over ranks: the slowest rank's kernel rate, the sum of the ranks' HBM
+    rates and the mean comm-stream time."""
+    t = torch.tensor([achieved], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)  # slowest rank's kernel
+    achieved = float(t.item())
+    t = torch.tensor([hbm_all, comm_ms or 0.0], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    hbm_all = float(t[0].item())
+    if comm_ms is not None:
+        comm_ms = float(t[1].item()) / world
+    return achieved, hbm_all, comm_ms
+
+
+def measure_client_axis(a, entries, n_elems: int, K_total: int, world: int, rank: int, dev) -> dict:
+    """north_star's client-axis mode on the same round (the same K_total
+    clients and sample counts): this rank's K_total/world clients' whole
+    updates, the fp32 partial and the chunked RCCL reduce-scatter over xGMI.
+    Runs after the headline in the same processes; returns the "exchange"
+    object of the JSON line."""
+    from fedml_amd.synth import sample_nums
+
+    if K_total < world:
+        return {"mode": "client", "skipped": f"{K_total} clients cannot cover {world} ranks on the client axis"}
+    _, K_c, first_c = plan_clients(a.config, world, rank, "client", K_total)
+    ns_all = sample_nums(K_total, seed=1)
+    total_n = sum(ns_all)
+    w = [n / total_n for n in ns_all[first_c:first_c + K_c]]
+    bucket = ClientBucket(entries, K_c, dev, low_precision_acc=a.acc)
+    for gi, (dt, g) in enumerate(bucket.groups.items()):
+        fill_rows(g.rows, g.length, seed=1000 * rank + gi, round_idx=3)
+    torch.cuda.synchronize()
+    dom_dt = max(bucket.groups.items(), key=lambda kv: kv[1].length * kv[1].rows.element_size())[0]
+    step, n_launch, dom_bytes, xgmi_bytes = client_axis_step(bucket, dom_dt, w, a.chunks, world)
+    backend = dist.get_backend()
+    timed_comm = backend == "nccl"
+    elapsed, kern_ms, comm_ms = run_timed(step, n_launch, a.steps, a.warmup, world, True, timed_comm)
+    achieved = dom_bytes / (kern_ms / 1e3) / 1e9
+    hbm_all = dom_bytes / (elapsed / a.steps) / 1e9
+    achieved, hbm_all, comm_ms = reduce_rates(achieved, hbm_all, comm_ms, world, dev)
+    ms = elapsed / a.steps * 1e3
+    out = {"mode": "client", "backend": backend, "world_size": world,
+           "collective": "reduce_scatter_tensor (RCCL over xGMI)" if backend == "nccl" else
+           "reduce_scatter_tensor (gloo, host-staged: a rehearsal, not a measurement)",
+           "clients_total": K_total, "clients_per_gpu": K_c, "chunks": n_launch,
+           "value": K_total * n_elems / (elapsed / a.steps), "unit": "client-params/s",
+           "ms_per_step": ms, "kernel_ms_per_step": round(kern_ms, 4),
+           "kernel_gbps_slowest_rank": round(achieved, 1), "aggregate_gbps": round(hbm_all, 1),
+           "xgmi_bytes_per_rank_per_step": xgmi_bytes,
+           "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
+           "parity": "fp32 partials summed across GPUs: |d| <= 2(K + log2 G + 1) 2^-24 sum|w_i p_i| vs one GPU "
+                     "(ClientAxisAggregator.tolerance; tests/test_sharded_gloo.py)",
+           "note": "same clients as the headline; comm_ms: mean over ranks of the chunks' reduce-scatter time on "
+                   "the comm stream (overlapping the next chunk's reduction)"}
+    del step, bucket
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -241,30 +407,11 @@ def main():
     entries = shapes.MODELS[cfg["model"]]()
     full_layout = RowLayout(entries)
     n_elems = sum(sum(g.numels) for g in full_layout.groups.values())  # per client, the whole model
-    K = cfg["K"]
-    if a.clients is not None:
-        if world > 1 or a.clients < 1:
-            raise SystemExit("--clients is a 1-GPU override (>= 1)")
-        K = a.clients
     mode = a.mode if world > 1 else "single"
     weak = a.weak and world > 1
-    if world > 1 and not weak:
-        K_total = a.clients_total if a.clients_total is not None else cfg["K"]
-        if K_total < 1:
-            raise SystemExit("--clients-total must be >= 1")
-    else:
-        K_total = K * world
     # this rank's clients: all of them (single / param axis) or its share (client axis)
-    if mode == "client" and not weak:
-        base_k, extra = divmod(K_total, world)
-        K_loc = base_k + (1 if rank < extra else 0)
-        first = rank * base_k + min(rank, extra)
-    elif mode == "client" or weak:
-        K_loc, first = K, rank * K
-    else:
-        K_loc, first = K_total, 0
-    if K_loc < 1:
-        raise SystemExit(f"rank {rank} would hold no clients: --clients-total {K_total} < --gpus {world}")
+    K_total, K_loc, first = plan_clients(a.config, world, rank, mode, a.clients_total, a.weak, a.clients)
+    K = K_loc
     # the keys this rank reduces: all of them, or its whole-key shard (param axis)
     my_entries = entries
     if mode == "param":
@@ -313,7 +460,6 @@ def main():
 
     groups = list(bucket.groups.items())
     dom_dt = max(groups, key=lambda kv: kv[1].length * kv[1].rows.element_size())[0]
-    comm_evs = None  # client axis: (start, end) per chunk on the comm stream
     xgmi_bytes = 0
 
     # per-step work -------------------------------------------------------------
@@ -469,63 +615,22 @@ def main():
         dom_bytes = K_loc * gd.length * gd.rows.element_size() + \
             gd.length * torch.empty((), dtype=gd.out_dtype).element_size()
     else:  # client axis: this rank's clients' partial + chunked RCCL reduce-scatter
-        aggs = {dt: ClientAxisAggregator(g.rows, g.length, chunks=a.chunks if dt == dom_dt else 1)
-                for dt, g in groups}
-
-        def step(ev=None, cev=None):
-            for dt, agg in aggs.items():
-                agg.aggregate(w_local, events=ev if dt == dom_dt else None,
-                              comm_events=cev if dt == dom_dt else None)
-                if dt in (torch.bfloat16, torch.float16):
-                    agg.shard_in_model_dtype()  # the one rounding of a 16-bit model, after the exchange
-
-        n_launch = len(aggs[dom_dt].bounds)
-        gd = bucket.groups[dom_dt]
-        dom_bytes = K_loc * gd.length * gd.rows.element_size() + gd.length * 4  # rows in, fp32 partial out
-        xgmi_bytes = (world - 1) * aggs[dom_dt].piece * len(aggs[dom_dt].bounds) * 4
-
-    def new_events(n):
-        return [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(n)]
+        step, n_launch, dom_bytes, xgmi_bytes = client_axis_step(bucket, dom_dt, w_local, a.chunks, world)
 
     timed_comm = mode == "client" and world > 1 and a.backend == "nccl"
-    for _ in range(a.warmup):
-        step()
-    evs = [new_events(n_launch) for _ in range(a.steps)]
-    cevs = [new_events(n_launch) for _ in range(a.steps)] if timed_comm else [None] * a.steps
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(a.steps):
-        # the client-axis steps take one (start, end) pair per chunk; the rest one pair
-        step(evs[s] if mode == "client" else evs[s][0], cevs[s])
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_ms = sum(e0.elapsed_time(e1) for ev in evs for e0, e1 in ev) / a.steps  # per step
-    comm_ms = sum(e0.elapsed_time(e1) for ev in cevs for e0, e1 in ev) / a.steps if timed_comm else None
+    elapsed, kern_ms, comm_ms = run_timed(step, n_launch, a.steps, a.warmup, world, mode == "client", timed_comm)
     achieved = dom_bytes / (kern_ms / 1e3) / 1e9  # GB/s (GFLOP/s for --op krum)
     hbm_all = dom_bytes / (elapsed / a.steps) / 1e9  # this rank's algorithmic bytes over the step time
     if world > 1:
-        t = torch.tensor([achieved], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)  # slowest rank's kernel
-        achieved = float(t.item())
-        t = torch.tensor([hbm_all, comm_ms or 0.0], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        hbm_all = float(t[0].item())
-        if comm_ms is not None:
-            comm_ms = float(t[1].item()) / world
+        achieved, hbm_all, comm_ms = reduce_rates(achieved, hbm_all, comm_ms, world, dev)
 
     ms_per_step = elapsed / a.steps * 1e3
     gram_op = a.op == "krum" and (a.pair_distance == "gram" or (a.pair_distance == "auto" and K <= 128))
     value = K_total * n_elems / (elapsed / a.steps)
-    variant = (a.fedopt or ("" if a.op == "fedavg" else a.op)) + (f"@K{K}" if a.clients is not None else "")
-    traffic = load_traffic(a.config, mode, world, variant)
+    variant = a.fedopt or ("" if a.op == "fedavg" else a.op)
+    if a.acc == "fp32" and dom_dt in (torch.bfloat16, torch.float16) and a.op == "fedavg":
+        variant = (variant + "+" if variant else "") + "acc32"  # the fp32-accumulate kernel's own PMC entry
+    traffic = load_traffic(a.config, mode, world, variant, K_loc)
     parallelism = {"single": "1 GPU",
                    "client": f"client-axis x{world}: {K_total} clients, ~{K_total // world} per GPU, fp32 partial + "
                              f"RCCL reduce-scatter, {a.chunks}-chunk pipeline",
@@ -597,7 +702,7 @@ def main():
         # med3 / DPP ops issue at 4 cycles per wave64 instruction per SIMD
         # (tools/valu_rate_probe.hip), so this is the share of the SIMDs' issue
         # capacity the kernel's executed VALU instructions take
-        vv = load_median_valu(a.config, mode, world, variant)
+        vv = load_median_valu(a.config, mode, world, variant, K_loc)
         if vv:
             issue_ms = vv["valu_instr_per_wave"] * vv["waves_per_launch"] * VALU_HALF_RATE_CYCLES / (
                 SIMDS * CLOCK_GHZ * 1e9) * 1e3
@@ -611,11 +716,18 @@ def main():
         line["roofline"]["aggregate_gbps"] = round(hbm_all, 1)
         line["roofline"]["aggregate_frac_of_n_peaks"] = round(hbm_all / (world * HBM_PEAK_GBPS), 4)
         if mode == "client":
-            line["exchange"] = {"collective": "reduce_scatter_tensor (RCCL)" if a.backend == "nccl" else "gloo (host)",
+            line["exchange"] = {"mode": "client", "backend": dist.get_backend(), "world_size": world,
+                                "collective": "reduce_scatter_tensor (RCCL)" if a.backend == "nccl" else "gloo (host)",
                                 "xgmi_bytes_per_rank_per_step": xgmi_bytes,
                                 "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
                                 "note": "comm_ms: mean over ranks of the chunks' reduce-scatter time on the comm "
                                         "stream (overlapping the next chunk's reduction)"}
+        elif mode == "param" and a.op == "fedavg" and not a.fedopt and not a.no_exchange:
+            # the headline is the exchange-free parameter axis; north_star's
+            # client axis + RCCL reduce-scatter runs next on the same clients
+            del step, outs, gd, groups, bucket  # free this rank's rows first
+            torch.cuda.empty_cache()
+            line["exchange"] = measure_client_axis(a, entries, n_elems, K_total, world, rank, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
         line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
     if rank == 0:

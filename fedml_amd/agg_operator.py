@@ -342,7 +342,7 @@ def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDic
     d0 = dicts[0]
     device = _host_device(args)
     layout = [(k, tuple(d0[k].shape), d0[k].dtype) for k in keys]
-    devices = multidev.devices_for_round(args, layout, K, device)
+    devices = _round_devices(args, layout, K, device, acc_mode)
     if len(devices) > 1:
         return _reduce_host_multi(layout, devices, tables, numels, codes, dicts, weights, acc_mode)
     with torch.cuda.device(device):
@@ -359,6 +359,40 @@ def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDic
 _MULTI: "OrderedDict[tuple, multidev.MultiDeviceBucket]" = OrderedDict()
 
 
+def _round_devices(args, layout, K: int, device: torch.device, acc_mode) -> list:
+    """Placement of a host round, decided once per (layout, K, accumulation):
+    a bucket already resident for it keeps its devices.  Asking the free HBM
+    again would not count that bucket's own rows as free, so a round that fit
+    one GPU in round 1 could flip to several GPUs in round 2 and hold its rows
+    twice (the cached one-device bucket plus the new shards)."""
+    if not _multi_requested(args):
+        lk = tuple((k, s, str(d)) for k, s, d in layout)
+        if (lk, K, str(device), _ACC_NAME[acc_mode]) in _BUCKETS:
+            return [device]
+        for key in _MULTI:
+            if key[0] == lk and key[1] == K and key[3] == acc_mode:
+                return [torch.device(d) for d in key[2]]
+    devices = multidev.devices_for_round(args, layout, K, device)
+    if len(devices) > 1:
+        # the round goes multi-device: a one-device bucket of the same layout
+        # (another K or accumulation) must not stay resident beside it
+        lk = tuple((k, s, str(d)) for k, s, d in layout)
+        for key in [k for k in _BUCKETS if k[0] == lk]:
+            del _BUCKETS[key]
+    return devices
+
+
+def _multi_bucket(layout, K: int, devices, acc_mode) -> "multidev.MultiDeviceBucket":
+    """The cached MultiDeviceBucket of this (layout, K, devices, accumulation)."""
+    key = (tuple((k, s, str(d)) for k, s, d in layout), K, tuple(str(d) for d in devices), acc_mode)
+    b = _MULTI.pop(key, None)
+    if b is None:
+        _MULTI.clear()  # one multi-device round resident at a time: they are the big ones
+        b = multidev.MultiDeviceBucket(layout, K, devices, low_precision_acc=_ACC_NAME[acc_mode])
+    _MULTI[key] = b
+    return b
+
+
 def _reduce_host_multi(layout, devices, tables, numels, codes, dicts, weights, acc_mode
                        ) -> "OrderedDict[str, torch.Tensor]":
     """A host round over several GPUs of this process (multidev): whole keys
@@ -367,12 +401,7 @@ def _reduce_host_multi(layout, devices, tables, numels, codes, dicts, weights, a
     exchange, bit-exact), results scattered back into per-key host tensors.
     The bucket is cached per (layout, K, devices) like the one-device one."""
     K = len(dicts)
-    key = (tuple((k, s, str(d)) for k, s, d in layout), K, tuple(str(d) for d in devices), acc_mode)
-    b = _MULTI.pop(key, None)
-    if b is None:
-        _MULTI.clear()  # one multi-device round resident at a time: they are the big ones
-        b = multidev.MultiDeviceBucket(layout, K, devices, low_precision_acc=_ACC_NAME[acc_mode])
-    _MULTI[key] = b
+    b = _multi_bucket(layout, K, devices, acc_mode)
     t2d = {c: np.frombuffer(t, dtype=np.int64).reshape(-1, K) for c, t in tables.items()}
     per_shard = b.split_tables(t2d)
     if K * sum(n * _ROW_ESZ[c] for n, c in zip(numels, codes)) <= _BATCH_MAX_BYTES:
@@ -417,12 +446,19 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
     # ---- host-resident inputs: pinned staging -> HBM rows, one launch per dtype --
     if host_keys:
         device = _host_device(args)
-        with torch.cuda.device(device):
-            layout = [(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in host_keys]
-            bucket = _cached_bucket(layout, K, device, _ACC_NAME[acc_mode])
+        layout = [(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in host_keys]
+        devices = _round_devices(args, layout, K, device, acc_mode)
+        if len(devices) > 1:  # the round spreads over GPUs (fedml_amd.multidev), as on the walked path
+            bucket = _multi_bucket(layout, K, devices, acc_mode)
             for i in range(K):
                 bucket.put(i, {k: per_key[k][i] for k in host_keys}, 1)
             results.update(bucket.reduce_to_host(weights))
+        else:
+            with torch.cuda.device(device):
+                bucket = _cached_bucket(layout, K, device, _ACC_NAME[acc_mode])
+                for i in range(K):
+                    bucket.put(i, {k: per_key[k][i] for k in host_keys}, 1)
+                results.update(bucket.reduce_to_host(weights))
 
     # ---- device-resident inputs: read in place --------------------------------
     if dev_keys:

@@ -102,10 +102,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
             cmd = [hipcc(), *HIPCC_FLAGS, "-c", "-o", tmp, src]
             if verbose:
                 print(" ".join(cmd))
-            jobs.append((subprocess.Popen(cmd), cmd, tmp, obj))
-    failed = [cmd for p, cmd, _, _ in jobs if p.wait() != 0]
+            # each unit's diagnostics are collected apart, so a failure prints
+            # one unit's errors instead of every hipcc's interleaved output
+            jobs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd, tmp, obj))
+    failed = []
+    for p, cmd, tmp, _ in jobs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            failed.append((cmd, out))
+        elif out and verbose:
+            sys.stdout.write(out.decode(errors="replace"))
     if failed:
-        raise subprocess.CalledProcessError(1, failed[0])
+        for _, _, tmp, _ in jobs:  # no half-built objects left behind
+            if os.path.exists(tmp):
+                os.remove(tmp)
+        cmd, out = failed[0]
+        sys.stderr.write(out.decode(errors="replace"))
+        raise subprocess.CalledProcessError(1, cmd, output=out)
     for _, _, tmp, obj in jobs:
         os.replace(tmp, obj)
     tmp = OUT + ".tmp"

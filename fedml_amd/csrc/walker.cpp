@@ -495,8 +495,28 @@ PyObject* group_by_device(PyObject*, PyObject* args) {
       Py_DECREF(out);
       return nullptr;
     }
-    for (size_t j = 0; j < sz.size(); ++j) PyList_SET_ITEM(idx, Py_ssize_t(j), PyLong_FromSsize_t(sz[j].second));
-    PyList_SET_ITEM(out, Py_ssize_t(g), Py_BuildValue("(iN)", dev_order[g], idx));
+    for (size_t j = 0; j < sz.size(); ++j) {
+      PyObject* v = PyLong_FromSsize_t(sz[j].second);
+      if (!v) {
+        Py_DECREF(idx);
+        Py_DECREF(out);
+        return nullptr;
+      }
+      PyList_SET_ITEM(idx, Py_ssize_t(j), v);
+    }
+    // (device, indices): built by hand so a failed allocation drops both
+    // references and raises, instead of leaving a NULL item in the list
+    PyObject* d = PyLong_FromLong(dev_order[g]);
+    PyObject* pair = d ? PyTuple_New(2) : nullptr;
+    if (!pair) {
+      Py_XDECREF(d);
+      Py_DECREF(idx);
+      Py_DECREF(out);
+      return nullptr;
+    }
+    PyTuple_SET_ITEM(pair, 0, d);
+    PyTuple_SET_ITEM(pair, 1, idx);
+    PyList_SET_ITEM(out, Py_ssize_t(g), pair);
   }
   return out;
 }

@@ -97,6 +97,19 @@ def is_weight_param(k: str) -> bool:
     return "running_mean" not in k and "running_var" not in k and "num_batches_tracked" not in k
 
 
+def _one_device(d0, wkeys, what: str) -> None:
+    """The defenses gather every client's weight keys into one bucket on one
+    GPU.  A round that a MultiDeviceBucket spread over several GPUs (because
+    it did not fit one) would be pulled back onto one device and fail with an
+    out-of-memory error deep inside; say what happened instead."""
+    devs = {d0[k].device for k in wkeys if isinstance(d0[k], torch.Tensor) and d0[k].is_cuda}
+    if len(devs) > 1:
+        raise NotImplementedError(
+            f"{what}: the clients' weight keys are spread over {len(devs)} GPUs "
+            f"({', '.join(sorted(str(d) for d in devs))}; a multi-device round, fedml_amd.multidev); the defense "
+            f"gathers every client onto one GPU, so run it on a round that fits one device")
+
+
 def median_f32(d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor) -> None:
     """Coordinate-wise lower median of K fp32 device rows (fedagg_median_f32)."""
     kn._require_cuda(out, "median_f32")
@@ -131,6 +144,7 @@ def coordinate_wise_median(raw_client_grad_list: List[Tuple[float, "OrderedDict"
     t0 = dicts[0][wkeys[0]] if wkeys else None
     if t0 is None:
         raise RuntimeError("torch.cat(): expected a non-empty list of Tensors")  # vectorize_weight on no keys
+    _one_device(dicts[0], wkeys, "wise_median")
     dev = t0.device if t0.is_cuda else (torch.device(device) if device is not None else
                                         torch.device("cuda", torch.cuda.current_device()))
     dts = {dicts[0][k].dtype for k in wkeys}
@@ -230,6 +244,33 @@ def _work(kind: int, K: int, n_chunks: int, device) -> torch.Tensor:
 
 
 GRAM_MAX_CLIENTS = 128  # fedagg_pairgram2_f32 holds up to 128 clients
+# "auto" keeps the Gram's distances only while (|c_i|^2 + |c_j|^2) / D_ij stays
+# at or below this for every pair (c = the rows centred on the client mean):
+# iid clients sit near 1; one update scaled far away inflates every honest
+# client's |c|^2 and triggers the exact kernel (gram_condition)
+GRAM_MAX_CONDITION = 8.0
+
+
+def gram_condition(D: np.ndarray) -> float:
+    """max over client pairs i != j of (|c_i|^2 + |c_j|^2) / D_ij, where c_i is
+    client i's row minus the mean of the K rows: the factor by which the
+    centred Gram's rounding error (~1e-7 (|c_i|^2 + |c_j|^2) per entry) exceeds
+    a relative error of D_ij itself.  The centred norms come from D alone
+    (double centring of a squared-distance matrix: |c_i|^2 = mean_j D_ij -
+    sum D / (2 K^2)).  inf when two distinct clients are at distance 0."""
+    K = D.shape[0]
+    if K < 2:
+        return 0.0
+    D = np.asarray(D, dtype=np.float64)
+    c2 = np.maximum(D.sum(axis=1) / K - D.sum() / (2.0 * K * K), 0.0)
+    num = c2[:, None] + c2[None, :]
+    off = ~np.eye(K, dtype=bool)
+    d, s = D[off], num[off]
+    if np.any((d <= 0) & (s > 0)):
+        return float("inf")
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r = np.where(d > 0, s / np.where(d > 0, d, 1.0), 0.0)
+    return float(r.max())
 
 
 def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks: int, device,
@@ -238,7 +279,11 @@ def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks:
     columns.  method "exact": the reference's fp32 differences, squared and
     summed on the VALU (fedagg_pairdist2_f32); "gram": the centred Gram on the
     fp32 matrix cores (fedagg_pairgram2_f32, K <= 128); "auto": gram when K
-    allows it (same Krum selections, ~3x faster at config 3)."""
+    allows it (same Krum selections, ~2x faster at config 3)
+    and the result is well conditioned (``gram_condition`` <=
+    GRAM_MAX_CONDITION), else the exact kernel: one far-away update (the case
+    Krum exists for) moves the client mean, and the honest clients' distances
+    would then carry the Gram's error scaled by that update's norm."""
     if method not in ("auto", "gram", "exact"):
         raise ValueError(f"pair distance method {method!r}: 'auto', 'gram' or 'exact'")
     gram = method == "gram" or (method == "auto" and K <= GRAM_MAX_CLIENTS)
@@ -249,6 +294,8 @@ def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks:
     fn = nat.lib().fedagg_pairgram2_f32 if gram else nat.lib().fedagg_pairdist2_f32
     nat.check(fn(d_ptrs.data_ptr(), K, chunks.data_ptr(), n_chunks, out.data_ptr(), work.data_ptr(), work.numel(),
                  nat.stream_handle()), "pairgram2" if gram else "pairdist2")
+    if gram and method == "auto" and gram_condition(out.cpu().numpy()) > GRAM_MAX_CONDITION:
+        return pairdist2_rows(d_ptrs, K, chunks, n_chunks, device, "exact")
     return out
 
 
@@ -281,6 +328,7 @@ def _weight_bucket(dicts: Sequence, what: str, device=None):
     dts = {dicts[0][k].dtype for k in wkeys}
     if dts != {torch.float32}:
         raise NotImplementedError(f"{what} on the GPU takes fp32 weight keys (got {sorted(map(str, dts))})")
+    _one_device(dicts[0], wkeys, what)
     t0 = dicts[0][wkeys[0]]
     dev = t0.device if t0.is_cuda else (torch.device(device) if device is not None else
                                         torch.device("cuda", torch.cuda.current_device()))

@@ -211,22 +211,37 @@ def round_bytes(layout, capacity: int, promote_ints: bool = True) -> int:
     return sum((capacity + 1) * _pad(n) * _ROW_ESZ.get(dt, 8) for dt, n in per_dt.items())
 
 
+def visible_devices() -> List[torch.device]:
+    """Every GPU this process sees (the devices an over-HBM round spreads to)."""
+    return [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+
+
+def free_bytes(device: torch.device) -> int:
+    """HBM a new round can take on ``device``: the driver's free memory plus
+    what torch's caching allocator holds reserved but unused (freed blocks it
+    would hand out again before asking the driver)."""
+    free, _ = torch.cuda.mem_get_info(device)
+    try:
+        free += max(0, torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device))
+    except (RuntimeError, AssertionError):
+        pass
+    return free
+
+
 def devices_for_round(args, layout, capacity: int, default: torch.device, promote_ints: bool = True
                       ) -> List[torch.device]:
     """Where a round's bucket goes: ``args.fedagg_devices`` when it lists
-    several devices; otherwise every visible GPU when the round does not fit
-    the default device's free HBM (with 10 % headroom) and more GPUs exist;
-    otherwise just the default device."""
+    devices; otherwise every visible GPU when the round does not fit the
+    default device's free HBM (``free_bytes``, with 10 % headroom) and more
+    GPUs exist; otherwise just the default device.  Callers decide once per
+    round layout (a resident bucket is not free memory any more; see
+    agg_operator._round_devices and the cross-silo mirror's first update)."""
     devs = parse_devices(getattr(args, "fedagg_devices", None)) if args is not None else []
-    if len(devs) > 1:
-        return devs
     if devs:
         return devs
-    n = torch.cuda.device_count()
-    if n > 1:
-        free, _ = torch.cuda.mem_get_info(default)
-        if round_bytes(layout, capacity, promote_ints) > 0.9 * free:
-            return [torch.device("cuda", i) for i in range(n)]
+    if torch.cuda.device_count() > 1:
+        if round_bytes(layout, capacity, promote_ints) > 0.9 * free_bytes(default):
+            return visible_devices()
     return [default]
 
 

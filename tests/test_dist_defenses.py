@@ -315,3 +315,65 @@ def test_robust_learning_rate_host_checks_before_device_work():
         dfn.robust_learning_rate([(1, OrderedDict(w=torch.ones(2, dtype=torch.bfloat16)))], 1)
     d = dfn.RobustLearningRateDefense(type("A", (), {"robust_threshold": 0})())
     assert d.run(raw, lambda lst: "base") == "base" and d.get_malicious_client_idxs() == []
+
+
+def test_gram_condition_from_distances():
+    """dfn.gram_condition recovers the client-mean-centred norms from D alone
+    (double centring) and reports max (|c_i|^2 + |c_j|^2) / D_ij: about 1 for
+    iid clients, large when one update sits far away, inf for two distinct
+    clients at distance 0; 0 below two clients."""
+    rng = np.random.default_rng(0)
+    X = 0.05 * rng.standard_normal(2000) + 0.01 * rng.standard_normal((30, 2000))
+
+    def D_of(X):
+        d = X[:, None, :] - X[None, :, :]
+        return (d * d).sum(-1)
+
+    C = X - X.mean(0)
+    c2 = (C * C).sum(1)
+    D = D_of(X)
+    off = ~np.eye(30, dtype=bool)
+    want = ((c2[:, None] + c2[None, :])[off] / D[off]).max()
+    assert abs(dfn.gram_condition(D) - want) < 1e-9 * want
+    assert 0.5 < dfn.gram_condition(D) < 2.0
+    X2 = X.copy()
+    X2[3] *= 1e3
+    assert dfn.gram_condition(D_of(X2)) > 1e3
+    X3 = X.copy()
+    X3[4] = X3[5]
+    assert dfn.gram_condition(D_of(X3)) == float("inf")
+    assert dfn.gram_condition(np.zeros((1, 1))) == 0.0
+    assert dfn.gram_condition(np.zeros((3, 3))) == 0.0  # all clients identical: nothing to lose
+
+
+class _OnDevice(torch.Tensor):
+    """A host tensor that reports a CUDA device (the placement check reads
+    only .is_cuda and .device)."""
+    _dev = None
+
+    @property
+    def is_cuda(self):
+        return True
+
+    @property
+    def device(self):
+        return self._dev
+
+
+def _on(t, i):
+    t = t.as_subclass(_OnDevice)
+    t._dev = torch.device("cuda", i)
+    return t
+
+
+def test_defenses_refuse_a_round_spread_over_gpus():
+    """A round whose weight keys sit on several GPUs (a MultiDeviceBucket's
+    views) gets a clear NotImplementedError from the gathering defenses
+    instead of an out-of-memory error inside the gather."""
+    d = OrderedDict([("a.weight", _on(torch.zeros(3), 0)), ("b.weight", _on(torch.zeros(2), 1)),
+                     ("bn.running_mean", _on(torch.zeros(2), 2))])
+    with pytest.raises(NotImplementedError, match="spread over 2 GPUs"):
+        dfn._one_device(d, ["a.weight", "b.weight"], "krum")
+    dfn._one_device(d, ["a.weight"], "krum")  # one device: fine
+    with pytest.raises(NotImplementedError, match="wise_median"):
+        dfn.coordinate_wise_median([(1, d), (1, d)])

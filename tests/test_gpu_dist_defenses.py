@@ -172,6 +172,37 @@ def test_pairgram2_vs_numpy(K, cuda_device):
     np.testing.assert_array_equal(D, D.T)
 
 
+@pytest.mark.parametrize("scale", [1.0, 3.0, 1e3])
+def test_auto_pair_distance_falls_back_for_a_far_outlier(scale, cuda_device):
+    """Krum's default ("auto"): one client scaled far from the rest (the
+    Byzantine update Krum exists for) moves the client mean, so the centred
+    Gram's error on the honest pairs grows with that update's norm.  auto
+    then returns the exact kernel's distances (bit for bit), and Krum selects
+    what the exact kernel selects; near the cluster (scale 1 or 3) it keeps the
+    Gram's distances."""
+    K, L = 40, 200_000
+    rows = _rows(K, L, cuda_device, 9)
+    rows[7] *= scale
+    segs = [(0, L)]
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    ch, n = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
+    Dg = dfn.pairdist2_rows(ptrs, K, ch, n, cuda_device, "gram").cpu().numpy()
+    De = dfn.pairdist2_rows(ptrs, K, ch, n, cuda_device, "exact").cpu().numpy()
+    Da = dfn.pairdist2_rows(ptrs, K, ch, n, cuda_device, "auto").cpu().numpy()
+    cond = dfn.gram_condition(Dg)
+    if scale >= 1e3:
+        assert cond > 100 * dfn.GRAM_MAX_CONDITION
+        np.testing.assert_array_equal(Da, De)
+    else:
+        assert cond < dfn.GRAM_MAX_CONDITION
+        np.testing.assert_array_equal(Da, Dg)
+    sa = torch.argsort(torch.Tensor(dfn.krum_scores(Da, 5))).tolist()
+    se = torch.argsort(torch.Tensor(dfn.krum_scores(De, 5))).tolist()
+    assert sa[:10] == se[:10]
+    if scale > 1.0:
+        assert 7 not in sa[:K - 5]
+
+
 def test_pairgram2_rejects_more_than_128_clients(cuda_device):
     rows = _rows(129, 64, cuda_device, 1)
     ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(129)], cuda_device)

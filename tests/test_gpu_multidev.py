@@ -174,3 +174,60 @@ def test_device_walk_groups_keys_by_device(cuda_device):
         gu.assert_same(res[k].cpu(), e, k)
     single = ClientBucket([(k, tuple(t.shape), t.dtype) for k, t in raw[0][1].items()], K, cuda_device)
     assert single.num_elements() == b.num_elements()
+
+
+def _over_hbm_node(monkeypatch, cuda_device, G: int = 4):
+    """A node of G GPUs (all mapped onto the box's one MI355X) whose default
+    device has 1 KB of HBM free: every round above that "exceeds one GPU"."""
+    from fedml_amd import multidev
+
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: G)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d=None: (1 << 10, 288 << 30))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda d=None: 0)
+    monkeypatch.setattr(multidev, "visible_devices", lambda: [cuda_device] * G)
+
+
+@pytest.mark.parametrize("name", ["ragged_f32_k128", "ragged_bf16_k32", "cfg2_cnn_web_k32"])
+def test_agg_spreads_an_over_hbm_round_unprompted(name, cuda_device, monkeypatch):
+    """north_star's trigger end to end: no fedagg_devices, but the round does
+    not fit the default GPU's free HBM, so FedMLAggOperator.agg builds a
+    MultiDeviceBucket over the visible GPUs by itself, and the result matches
+    the reference's golden vectors bit for bit.  A second round of the same
+    layout reuses that bucket (placement decided once)."""
+    _over_hbm_node(monkeypatch, cuda_device)
+    monkeypatch.setattr(ao, "_HOST_ROUND_MAX_BYTES", 0)  # small rounds would otherwise take the one-call path
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    ao._MULTI.clear()
+    ao._BUCKETS.clear()
+    res = ao.FedMLAggOperator.agg(cases.Args(spec), cases.build_inputs(spec))
+    gu.assert_groups(res, meta, arrays, name)
+    assert len(ao._MULTI) == 1 and not ao._BUCKETS
+    b = next(iter(ao._MULTI.values()))
+    assert isinstance(b, MultiDeviceBucket) and len(b.shards) >= 2
+    res = ao.FedMLAggOperator.agg(cases.Args(spec), cases.build_inputs(spec))
+    gu.assert_groups(res, meta, arrays, name + " (round 2)")
+    assert len(ao._MULTI) == 1 and next(iter(ao._MULTI.values())) is b
+    ao._MULTI.clear()
+
+
+def test_cross_silo_spreads_an_over_hbm_round_unprompted(cuda_device, monkeypatch):
+    """The cross-silo mirror's first update decides the placement: with the
+    round over the free HBM and 4 GPUs visible it builds a 4-shard
+    MultiDeviceBucket without fedagg_devices; aggregate() is bit-exact."""
+    _over_hbm_node(monkeypatch, cuda_device)
+    torch.manual_seed(1)
+    model = torch.nn.Sequential(torch.nn.Linear(37, 19), torch.nn.BatchNorm1d(19), torch.nn.Linear(19, 3)).to(cuda_device)
+    args = _Args()
+    K = 5
+    server = FedMLAggregator(None, None, 0, {}, {}, {}, K, cuda_device, args, MI355XServerAggregator(model, args))
+    entries = [(k, tuple(t.shape), t.dtype) for k, t in model.state_dict().items()]
+    raw = host_clients(entries, K, seed=77, round_idx=1)
+    exp = orc.agg(_Args(), copy.deepcopy(raw))
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    assert isinstance(server.bucket, MultiDeviceBucket) and len(server.bucket.shards) == 4
+    assert server.check_whether_all_receive()
+    averaged, _, _ = server.aggregate()
+    for k, e in exp.items():
+        gu.assert_same(averaged[k].cpu(), e, k)

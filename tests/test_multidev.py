@@ -133,3 +133,66 @@ def test_split_reduce_reassemble_matches_oracle(G):
         assert got[k].dtype == e.dtype and got[k].shape == e.shape, k
         assert torch.equal(got[k].view(torch.int16) if e.dtype == torch.bfloat16 else got[k].view(torch.int32),
                            e.view(torch.int16) if e.dtype == torch.bfloat16 else e.view(torch.int32)), k
+
+
+def _fake_node(monkeypatch, n: int, free: int, reserved_unused: int = 0):
+    """A node of n GPUs whose default device has `free` bytes of HBM free and
+    `reserved_unused` bytes held by torch's caching allocator but unused."""
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: n)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d=None: (free, 288 << 30))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda d=None: reserved_unused)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda d=None: 0)
+
+
+def test_over_hbm_trigger_spreads_the_round(monkeypatch):
+    """north_star's "shard when the model exceeds one GPU": with 4 GPUs visible
+    and 8 GB free, config 3 (128 x ResNet-50, 13.2 GB of rows) goes to all 4
+    devices unprompted; config 2 (32 x LeNet, 8 MB) stays on the default one;
+    a round that fits 90 % of the free HBM stays too, as does any round on a
+    one-GPU node."""
+    dev0 = torch.device("cuda", 0)
+    four = [torch.device("cuda", i) for i in range(4)]
+    _fake_node(monkeypatch, 4, 8 << 30)
+    assert md.devices_for_round(None, shapes.resnet50(), 128, dev0) == four
+    assert md.devices_for_round(SimpleNamespace(), shapes.resnet50(), 128, dev0) == four
+    assert md.devices_for_round(None, shapes.cnn_web(), 32, dev0) == [dev0]
+    rb = md.round_bytes(shapes.resnet50(), 128)
+    _fake_node(monkeypatch, 4, int(rb / 0.9) + (1 << 20))
+    assert md.devices_for_round(None, shapes.resnet50(), 128, dev0) == [dev0]
+    _fake_node(monkeypatch, 4, int(rb / 0.9) - (1 << 20))
+    assert md.devices_for_round(None, shapes.resnet50(), 128, dev0) == four
+    # torch's cached-but-unused blocks count as free
+    _fake_node(monkeypatch, 4, int(rb / 0.9) - (1 << 20), reserved_unused=2 << 20)
+    assert md.devices_for_round(None, shapes.resnet50(), 128, dev0) == [dev0]
+    _fake_node(monkeypatch, 1, 1 << 30)
+    assert md.devices_for_round(None, shapes.resnet50(), 128, dev0) == [dev0]
+    # an explicit list wins over the free-memory test
+    _fake_node(monkeypatch, 4, 8 << 30)
+    assert md.devices_for_round(SimpleNamespace(fedagg_devices="1"), shapes.resnet50(), 128, dev0) == \
+        [torch.device("cuda", 1)]
+
+
+def test_round_placement_is_decided_once_per_layout(monkeypatch):
+    """agg()'s placement (agg_operator._round_devices): a layout with a
+    resident one-device bucket keeps that device even when free HBM (which no
+    longer counts the bucket's own rows) now says "does not fit"; a resident
+    multi-device bucket keeps its devices; going multi-device evicts a
+    one-device bucket of the same layout."""
+    from fedml_amd import agg_operator as ao
+    from fedml_amd import kernels as kn
+
+    dev0 = torch.device("cuda", 0)
+    layout = shapes.resnet50()
+    lk = tuple((k, s, str(d)) for k, s, d in layout)
+    monkeypatch.setattr(ao, "_BUCKETS", type(ao._BUCKETS)())
+    monkeypatch.setattr(ao, "_MULTI", type(ao._MULTI)())
+    _fake_node(monkeypatch, 4, 1 << 30)
+    ao._BUCKETS[(lk, 128, str(dev0), "reference")] = object()
+    assert ao._round_devices(None, layout, 128, dev0, kn.ACC_REFERENCE) == [dev0]
+    # another client count of the same layout: asks again, goes multi, evicts the old bucket
+    got = ao._round_devices(None, layout, 64, dev0, kn.ACC_REFERENCE)
+    assert got == [torch.device("cuda", i) for i in range(4)]
+    assert not any(k[0] == lk for k in ao._BUCKETS)
+    ao._MULTI[(lk, 64, tuple(str(d) for d in got), kn.ACC_REFERENCE)] = object()
+    _fake_node(monkeypatch, 4, 1 << 40)  # plenty free now: the resident shards still decide
+    assert ao._round_devices(None, layout, 64, dev0, kn.ACC_REFERENCE) == got

@@ -25,9 +25,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 OUT_DIR = os.path.join(ROOT, "gpurun_out", "median_valu")
 SHAPES = {  # key (as bench.py's load_traffic) -> bench.py arguments
-    "cfg3:single:median": ["--config", "cfg3"],
-    "cfg4:single:median": ["--config", "cfg4"],
-    "cfg4:single:median@K512": ["--config", "cfg4", "--clients", "512"],
+    "cfg3:single:median@K128": ["--config", "cfg3"],
+    "cfg4:single:median@K128": ["--config", "cfg4", "--clients", "128"],
+    "cfg4:single:median@K512": ["--config", "cfg4"],
     "cfg3:single:median@K512": ["--config", "cfg3", "--clients", "512"],
 }
 

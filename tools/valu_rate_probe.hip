@@ -12,6 +12,7 @@
 // cost, at 2+ waves per SIMD the SIMD's own rate.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define R16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
@@ -63,7 +64,19 @@ __global__ __launch_bounds__(256) void probe(float* out, float seed) {
   if constexpr (KIND == 28) asm volatile("v_minimum3_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
   if constexpr (KIND == 29) asm volatile("v_min3_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
   if constexpr (KIND == 30) asm volatile("v_dot2_u32_u16 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
-  if constexpr (KIND == 31) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 15]));
+  if constexpr (KIND == 31) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 15])); \
+  if constexpr (KIND == 32) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
+  if constexpr (KIND == 33) asm volatile("v_sad_u16 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
+  if constexpr (KIND == 34) asm volatile("v_sad_hi_u8 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
+  if constexpr (KIND == 35) asm volatile("v_msad_u8 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
+  if constexpr (KIND == 36) asm volatile("v_pk_ashrrev_i16 %0, 15, %0" : "+v"(a[i])); \
+  if constexpr (KIND == 37) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 15])); \
+  if constexpr (KIND == 38) asm volatile("v_sad_u32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
+  if constexpr (KIND == 39) asm volatile("v_add_u32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a[i]) : "v"(a[(i + 8) & 15])); \
+  if constexpr (KIND == 40) asm volatile("v_lshl_or_b32 %0, %0, 8, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 15])); \
+  if constexpr (KIND == 41) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 15])); \
+  if constexpr (KIND == 42) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) & 15]), "v"(a[(i + 2) & 15])); \
+  if constexpr (KIND == 43) asm volatile("v_sub_u16 %0, %0, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 15]));
       R16(OP)
 #undef OP
     }
@@ -80,7 +93,7 @@ __global__ __launch_bounds__(256) void probe(float* out, float seed) {
 
 static const char* kNames[] = {"v_max_f32", "v_pk_max_i16", "v_med3_f32", "v_mov_b32_dpp", "v_fma_f32",
                                "v_pk_max_f16", "v_cndmask_b32", "v_pk_maximum3_f16", "v_max_i16_sdwa",
-                               "v_max3_f32", "v_xor_b32", "v_pk_min_i16 op_sel", "v_min_i32", "v_min_u32", "v_med3_i32", "v_min_i16", "v_sub_u32", "v_lshrrev_b32", "v_bfi_b32", "v_bitop3_b32", "v_cndmask_b32 sgpr", "v_cmp_lt_u32", "v_perm_b32", "v_permlane32_swap", "v_add_f32", "v_pk_fma_f32", "v_pk_add_u16", "v_max_u16", "v_minimum3_f32", "v_min3_u32", "v_dot2_u32_u16", "v_and_b32"};
+                               "v_max3_f32", "v_xor_b32", "v_pk_min_i16 op_sel", "v_min_i32", "v_min_u32", "v_med3_i32", "v_min_i16", "v_sub_u32", "v_lshrrev_b32", "v_bfi_b32", "v_bitop3_b32", "v_cndmask_b32 sgpr", "v_cmp_lt_u32", "v_perm_b32", "v_permlane32_swap", "v_add_f32", "v_pk_fma_f32", "v_pk_add_u16", "v_max_u16", "v_minimum3_f32", "v_min3_u32", "v_dot2_u32_u16", "v_and_b32", "v_sad_u8", "v_sad_u16", "v_sad_hi_u8", "v_msad_u8", "v_pk_ashrrev_i16", "v_pk_max_u16", "v_sad_u32", "v_add_u32_dpp", "v_lshl_or_b32", "v_bcnt_u32_b32", "v_add3_u32", "v_sub_u16"};
 
 template <int KIND>
 float run(int blocks, float* out) {
@@ -120,6 +133,26 @@ int main() {
   hipMalloc(&out, 4096);
   row<0>(out, cus, ghz);
   row<4>(out, cus, ghz);
+  if (getenv("VALU_PROBE_SAD")) {  // round 4: the counting-selection candidates only
+    for (int w = 0; w < 1; ++w) {
+      row<10>(out, cus, ghz);
+      row<22>(out, cus, ghz);
+      row<32>(out, cus, ghz);
+      row<33>(out, cus, ghz);
+      row<34>(out, cus, ghz);
+      row<35>(out, cus, ghz);
+      row<36>(out, cus, ghz);
+      row<37>(out, cus, ghz);
+      row<38>(out, cus, ghz);
+      row<39>(out, cus, ghz);
+      row<40>(out, cus, ghz);
+      row<41>(out, cus, ghz);
+      row<42>(out, cus, ghz);
+      row<43>(out, cus, ghz);
+    }
+    hipFree(out);
+    return 0;
+  }
   row<12>(out, cus, ghz);
   row<13>(out, cus, ghz);
   row<14>(out, cus, ghz);
