@@ -2,7 +2,8 @@
 
     python tools/median_ab.py [out.json]
 
-Builds tools/_build/libmedian_{a,b}.so from fedml_amd/csrc/median.hip with
+Builds tools/_build/libmedian_{a,b}.so (MEDIAN_AB_DIR: another directory,
+e.g. one that travels to the GPU box, built here beforehand with --build-only) from fedml_amd/csrc/median.hip with
 the -D flags in VARIANTS (plus a stub for the library's error hook), loads
 both, and times fedagg_median on the shapes below interleaved (2 warm-up, 9
 timed launches each, HIP events on the launch stream); outputs must agree bit
@@ -37,12 +38,13 @@ def build():
     from fedml_amd import build as fb
 
     src = os.path.join(ROOT, "fedml_amd", "csrc", "median.hip")
-    os.makedirs(os.path.join(HERE, "_build"), exist_ok=True)
-    stub = os.path.join(HERE, "_build", "median_ab_stub.cpp")
+    bdir = os.path.join(ROOT, os.environ.get("MEDIAN_AB_DIR", os.path.join("tools", "_build")))
+    os.makedirs(bdir, exist_ok=True)
+    stub = os.path.join(bdir, "median_ab_stub.cpp")
     open(stub, "w").write(STUB)
     procs, outs = [], {}
     for tag, flags in VARIANTS.items():
-        so = os.path.join(HERE, "_build", f"libmedian_{tag}.so")
+        so = os.path.join(bdir, f"libmedian_{tag}.so")
         outs[tag] = so
         if os.path.exists(so) and os.path.getmtime(so) > os.path.getmtime(src):
             continue
