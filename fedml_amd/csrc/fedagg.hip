@@ -1168,13 +1168,15 @@ int tiny_shipped_fn(const void* const* src, const float* w, int32_t K, int64_t N
 }
 #define FEDAGG_TINY_NARROW(U, EL) \
   { "EL" #EL "_U" #U, tiny_narrow_fn<OpF32, U, EL>, tiny_narrow_fn<OpBF16Ref, U, EL> }
+// (round 4: the entries that needed 258-266 VGPRs, wide_U32 and EL4_U64, one
+// wave per SIMD and slower everywhere in profiles/r03/tiny/, are no longer
+// instantiated)
 const TinyVariant kTinyVariants[] = {
     {"shipped", tiny_shipped_fn<OpF32>, tiny_shipped_fn<OpBF16Ref>},
     {"wide_U16", tiny_wide_fn<OpF32, 16>, tiny_wide_fn<OpBF16Ref, 16>},
-    {"wide_U32", tiny_wide_fn<OpF32, 32>, tiny_wide_fn<OpBF16Ref, 32>},
     FEDAGG_TINY_NARROW(16, 1), FEDAGG_TINY_NARROW(32, 1), FEDAGG_TINY_NARROW(64, 1),
     FEDAGG_TINY_NARROW(16, 2), FEDAGG_TINY_NARROW(32, 2), FEDAGG_TINY_NARROW(64, 2),
-    FEDAGG_TINY_NARROW(16, 4), FEDAGG_TINY_NARROW(32, 4), FEDAGG_TINY_NARROW(64, 4),
+    FEDAGG_TINY_NARROW(16, 4), FEDAGG_TINY_NARROW(32, 4),
 };
 #undef FEDAGG_TINY_NARROW
 constexpr int kNumTinyVariants = sizeof(kTinyVariants) / sizeof(kTinyVariants[0]);
@@ -1213,8 +1215,84 @@ __global__ __launch_bounds__(kBlock) void fedopt_sgd_kernel(float* __restrict__ 
 }  // namespace
 
 namespace {
+// Persistent workers for the host packs (fedagg_host_pack / _unpack).  Every
+// arriving client is one pack per dtype group, and a round spread over G GPUs
+// (fedml_amd.multidev) packs each device's keys from its own Python thread at
+// the same time: spawning 8 threads per call cost ~0.1-0.2 ms each time, and
+// one shared job slot would serialize the shards.  Callers queue a batch of
+// parts, work on it themselves, and idle workers join in; a batch leaves the
+// queue when its parts are all claimed, and its caller returns once every
+// part has run and no worker still holds it.
+class PackPool {
+ public:
+  static PackPool& get() {
+    static PackPool* p = new PackPool(15);  // + the caller: 16, the GPU box's CPU share
+    return *p;
+  }
+  void run(int parts, const std::function<void(int)>& fn) {
+    if (parts <= 1) {
+      if (parts == 1) fn(0);
+      return;
+    }
+    Batch b;
+    b.fn = &fn;
+    b.parts = parts;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(&b);
+    }
+    cv_.notify_all();
+    for (int part = b.next.fetch_add(1); part < parts; part = b.next.fetch_add(1)) {
+      fn(part);
+      b.done.fetch_add(1);
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    for (size_t i = 0; i < q_.size(); ++i)
+      if (q_[i] == &b) {
+        q_.erase(q_.begin() + std::ptrdiff_t(i));
+        break;
+      }
+    b.cv.wait(lk, [&] { return b.done.load() == parts && b.active == 0; });
+  }
+
+ private:
+  struct Batch {
+    const std::function<void(int)>* fn = nullptr;
+    int parts = 0;
+    int active = 0;  // workers holding this batch (guarded by mu_)
+    std::atomic<int> next{0}, done{0};
+    std::condition_variable cv;
+  };
+  explicit PackPool(int n) {
+    for (int i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return !q_.empty(); });
+      Batch* b = q_.front();
+      if (b->next.load() >= b->parts) {  // every part claimed: nothing left to join
+        q_.erase(q_.begin());
+        continue;
+      }
+      ++b->active;
+      lk.unlock();
+      for (int part = b->next.fetch_add(1); part < b->parts; part = b->next.fetch_add(1)) {
+        (*b->fn)(part);
+        b->done.fetch_add(1);
+      }
+      lk.lock();
+      if (--b->active == 0) b->cv.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Batch*> q_;
+};
+
 // Parallel copy of n byte ranges: range i goes from src_base[i] to dst_base[i]
-// (nbytes[i] bytes).  The total is cut into `threads` contiguous slices.
+// (nbytes[i] bytes).  The total is cut into `threads` contiguous slices, run
+// on the persistent PackPool.
 template <class SrcAt, class DstAt>
 void parallel_ranges(int32_t n, const int64_t* nbytes, int32_t threads, SrcAt src_at, DstAt dst_at) {
   int64_t total = 0;
@@ -1237,14 +1315,11 @@ void parallel_ranges(int32_t n, const int64_t* nbytes, int32_t threads, SrcAt sr
     return;
   }
   const int64_t per = ((total + T - 1) / T + 4095) & ~int64_t(4095);
-  std::vector<std::thread> pool;
-  pool.reserve(T);
-  for (int32_t t = 0; t < T; ++t) {
+  const int parts = int((total + per - 1) / per);
+  PackPool::get().run(parts, [&](int t) {
     const int64_t b0 = int64_t(t) * per, b1 = b0 + per < total ? b0 + per : total;
-    if (b0 >= total) break;
-    pool.emplace_back(work, b0, b1);
-  }
-  for (auto& th : pool) th.join();
+    work(b0, b1);
+  });
 }
 
 int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, const int64_t* nbytes,

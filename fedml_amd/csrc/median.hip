@@ -22,6 +22,26 @@
 #ifndef FEDAGG_PK16_BATCH
 #define FEDAGG_PK16_BATCH 2
 #endif
+// Packed 16-bit lane groups (128 < K <= 1024): 1 selects the median by
+// counting (median_pk16_count: byte-wise bisection with v_sad_u8), 0 by the
+// sorting networks and cross-lane merges (A/B knob for tools/median_ab.py)
+#ifndef FEDAGG_PK16_COUNT
+#define FEDAGG_PK16_COUNT 1
+#endif
+// values per lane of the counting kernels (P = KMAX / R lanes per column pair)
+#ifndef FEDAGG_PK16_COUNT_R
+#define FEDAGG_PK16_COUNT_R 128
+#endif
+// independent v_sad_u8 accumulator chains per sum
+#ifndef FEDAGG_SAD_CHAINS
+#define FEDAGG_SAD_CHAINS 2
+#endif
+// 1: the low bytes are gathered with the high bytes up front and clamped in
+// the byte domain (SWAR compares), so the 16-bit keys need not stay live
+// through the high phase: 128 instead of 192 registers of keys per lane
+#ifndef FEDAGG_PK16_COUNT_HL
+#define FEDAGG_PK16_COUNT_HL 0
+#endif
 // Loads of the lane-group kernels: a wave instruction reads 64 B of each of P
 // rows' 128-B lines and the block's next wave reads the other half, so plain
 // loads (0) keep the line in L2 for it; non-temporal ones (1) fetched 1.04-1.5x
@@ -613,9 +633,13 @@ __device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
 // DPP mov, v_pk_min, v_pk_max and a lane select before.  (fp32 keeps the
 // mirrored pairing: a negated DPP read cannot fuse into an IEEE min there,
 // and its min-or-max is already one v_med3 against ±inf.)
-__device__ __forceinline__ short2_t lanes_rev(short2_t x) { return ~x; }
-__device__ __forceinline__ short2_t lanes_min(short2_t a, short2_t b) { return __builtin_elementwise_min(a, b); }
-__device__ __forceinline__ short2_t lanes_max(short2_t a, short2_t b) { return __builtin_elementwise_max(a, b); }
+[[maybe_unused]] __device__ __forceinline__ short2_t lanes_rev(short2_t x) { return ~x; }
+[[maybe_unused]] __device__ __forceinline__ short2_t lanes_min(short2_t a, short2_t b) {
+  return __builtin_elementwise_min(a, b);
+}
+[[maybe_unused]] __device__ __forceinline__ short2_t lanes_max(short2_t a, short2_t b) {
+  return __builtin_elementwise_max(a, b);
+}
 
 template <class T, int R>
 __device__ __forceinline__ T lanes4_merge_median(T (&v)[R]) {
@@ -811,8 +835,170 @@ __device__ __forceinline__ void pk_lanes_merge_levels(short2_t (&v)[R], int sub)
 template <class E>
 __device__ uint32_t g_median_pad2[2] = {E::kNegInf * 0x10001u, E::kPosInf * 0x10001u};
 
-template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
+// ---------------------------------------------------------------------------
+// Selection by counting (FEDAGG_PK16_COUNT), for the packed lane groups: the
+// sorting networks above spend ~35 half-rate min/max per value at 512
+// clients (VALU-bound at 0.85 of the SIMDs' issue capacity).  Counting needs
+// far fewer operations per value:
+//   - every 16-bit float becomes its UNSIGNED order key (x ^ 0x8000 for a
+//     positive value, ~x for a negative one), so integer order = float order;
+//   - for integer keys x_i and a pivot p, S(p) = sum |x_i - p| is convex and
+//     S(p+1) - S(p) = #(x <= p) - #(x > p) = 2 c(p) - n, so the count c(p) of
+//     keys at or below p comes from two sums of absolute differences;
+//   - v_sad_u8 adds |a_b - p| over the 4 bytes b of a register into an
+//     accumulator: 4 keys per instruction.  So the keys are split into bytes
+//     and selected a byte at a time, most significant first: 8 bisection
+//     steps find the median's high byte h (the smallest h with #(hi <= h) at
+//     least the target rank + 1); then every key is clamped into
+//     [h << 8, h << 8 | 255] (a key below the range counts as low byte 0, one
+//     above as 255 and never counts for a pivot below 255, which is exactly
+//     its order relation to every candidate), and 8 more steps on the clamped
+//     low bytes find l.  The median's key is h << 8 | l, mapped back to the
+//     input's bits.
+// Padding stays the sorting kernels' (±inf slots that put the lower median at
+// slot KMAX/2 - 1 of KMAX), so the target count is KMAX/2 and the test per
+// step is D = S(p+1) - S(p) >= 0, summed over the column's P lanes (DPP adds).
+// Per lane at K = 512 (128 clients x 2 columns): 2 x 2 x 32 v_sad_u8 per step
+// x 16 steps = 2,048, plus 256 byte gathers (v_perm_b32), 256 clamps and the
+// key transform, against ~5,300 half-rate ops for the networks.
+[[maybe_unused]] __device__ __forceinline__ uint32_t pk16_ukey(uint32_t x) {
+  const uint32_t s = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, x) >> short(15));  // 0xffff: negative
+  return x ^ (s | 0x80008000u);
+}
+[[maybe_unused]] __device__ __forceinline__ uint32_t pk16_from_ukey(uint32_t k) {
+  const uint32_t s = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, k) >> short(15));  // 0xffff: positive
+  return k ^ (~s | 0x80008000u);
+}
+// sum of x over the P adjacent lanes of a column group (every lane gets it)
+template <int P>
+__device__ __forceinline__ int lanes_sum(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, dpp_xor_ctrl<1>(), 0xf, 0xf, false);
+  if constexpr (P >= 4) x += __builtin_amdgcn_update_dpp(0, x, dpp_xor_ctrl<2>(), 0xf, 0xf, false);
+  if constexpr (P >= 8) x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xf, 0xf, false);  // row_half_mirror: quads
+  if constexpr (P >= 16) x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xf, 0xf, false);  // row_mirror: halves
+  if constexpr (P >= 32) x += __shfl_xor(x, 16, 64);
+  return x;
+}
+// one byte of the two columns' medians: the smallest v in [0, 255] with
+// #(byte <= v) >= KMAX/2 over the column's P lanes, for column 0 (b0) and 1 (b1)
+template <int P, int NB>
+__device__ __forceinline__ void sad_bisect(const uint32_t (&b0)[NB], const uint32_t (&b1)[NB], uint32_t& v0,
+                                           uint32_t& v1) {
+  v0 = 0;
+  v1 = 0;
+#pragma unroll
+  for (int bit = 7; bit >= 0; --bit) {
+    const uint32_t p0 = (v0 + (1u << bit) - 1u) * 0x01010101u, p1 = (v1 + (1u << bit) - 1u) * 0x01010101u;
+    const uint32_t q0 = p0 + 0x01010101u, q1 = p1 + 0x01010101u;
+    constexpr int C = FEDAGG_SAD_CHAINS < NB ? FEDAGG_SAD_CHAINS : NB;
+    uint32_t s0[C], t0[C], s1[C], t1[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) s0[c] = t0[c] = s1[c] = t1[c] = 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      s0[j % C] = __builtin_amdgcn_sad_u8(b0[j], p0, s0[j % C]);
+      t0[j % C] = __builtin_amdgcn_sad_u8(b0[j], q0, t0[j % C]);
+      s1[j % C] = __builtin_amdgcn_sad_u8(b1[j], p1, s1[j % C]);
+      t1[j % C] = __builtin_amdgcn_sad_u8(b1[j], q1, t1[j % C]);
+    }
+#pragma unroll
+    for (int c = 1; c < C; ++c) {
+      s0[0] += s0[c];
+      t0[0] += t0[c];
+      s1[0] += s1[c];
+      t1[0] += t1[c];
+    }
+    const int d0 = lanes_sum<P>(int(t0[0]) - int(s0[0]));
+    const int d1 = lanes_sum<P>(int(t1[0]) - int(s1[0]));
+    if (d0 < 0) v0 += 1u << bit;  // fewer than KMAX/2 keys at or below the pivot: the median is above it
+    if (d1 < 0) v1 += 1u << bit;
+  }
+}
+// bytes `lo` and `lo + 2` (the two columns' byte of one key pair) of four
+// registers, gathered per column: c0 = {k0, k1, k2, k3}.byte lo, c1 = .byte lo+2
+template <int LO>
+__device__ __forceinline__ void gather_bytes(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t& c0,
+                                             uint32_t& c1) {
+  constexpr uint32_t sel = LO == 0 ? 0x06040200u : 0x07050301u;  // {S1.b, S1.b+2, S0.b, S0.b+2}
+  const uint32_t t01 = __builtin_amdgcn_perm(k1, k0, sel), t23 = __builtin_amdgcn_perm(k3, k2, sel);
+  c0 = __builtin_amdgcn_perm(t23, t01, 0x06040200u);
+  c1 = __builtin_amdgcn_perm(t23, t01, 0x07050301u);
+}
+// Per byte of four keys' high bytes H and low bytes L against the median's
+// high byte h: 0 where H < h, 255 where H > h, L where H == h.  Unsigned byte
+// compares without a borrow between bytes: a byte's low 7 bits compare as
+// (x | 0x80) - (y + 1), whose bit 7 is x > y; the top bits decide the rest
+// (bitop3: (x & ~y) | (~(x ^ y) & low)).  Bit 7 of every byte then widens to
+// the byte with v_perm_b32's sign-replicating selectors (8..11: bytes 1, 3,
+// 5, 7 of {S0, S1}; the flags shifted up a byte fill bytes 1 and 3 of S1).
+// hb = h * 0x01010101, y1 = (hb & 0x7f7f7f7f) + 0x01010101, yv = h >= 128 ? ~0 : 0.
+__device__ __forceinline__ uint32_t msb_bytes(uint32_t f) {
+  return __builtin_amdgcn_perm(f, f << 8, 0x0B090A08u);
+}
+__device__ __forceinline__ uint32_t clamp_bytes(uint32_t H, uint32_t L, uint32_t hb, uint32_t y1, uint32_t yv) {
+  const uint32_t t = (H | 0x80808080u) - y1;
+  const uint32_t gt = (H & ~yv) | (~(H ^ yv) & t);  // bit 7: H > h
+  const uint32_t t2 = (hb | 0x80808080u) - ((H & 0x7f7f7f7fu) + 0x01010101u);
+  const uint32_t lt = (hb & ~H) | (~(hb ^ H) & t2);  // bit 7: h > H
+  const uint32_t gm = msb_bytes(gt), lm = msb_bytes(lt);
+  return (L & ~(lm | gm)) | gm;
+}
+// the two columns' lower medians as packed order keys, from this lane's R
+// packed key registers (column 0 in the low halves)
+template <int P, int R>
+__device__ __forceinline__ uint32_t pk16_count_median(uint32_t (&k)[R]) {
+  constexpr int NB = R / 4;
+  uint32_t h0, h1, l0, l1;
+  if constexpr (FEDAGG_PK16_COUNT_HL) {
+    uint32_t b0[NB], b1[NB], c0[NB], c1[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      gather_bytes<1>(k[4 * j], k[4 * j + 1], k[4 * j + 2], k[4 * j + 3], b0[j], b1[j]);
+      gather_bytes<0>(k[4 * j], k[4 * j + 1], k[4 * j + 2], k[4 * j + 3], c0[j], c1[j]);
+    }
+    // the low bytes exist before the high phase, so the 16-bit keys die here
+    // (left alone, the scheduler sinks their gathers to the low phase)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) asm volatile("" : "+v"(c0[j]), "+v"(c1[j]));
+    sad_bisect<P, NB>(b0, b1, h0, h1);
+    const uint32_t hb0 = h0 * 0x01010101u, hb1 = h1 * 0x01010101u;
+    const uint32_t y10 = (hb0 & 0x7f7f7f7fu) + 0x01010101u, y11 = (hb1 & 0x7f7f7f7fu) + 0x01010101u;
+    const uint32_t yv0 = h0 >= 128u ? ~0u : 0u, yv1 = h1 >= 128u ? ~0u : 0u;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      c0[j] = clamp_bytes(b0[j], c0[j], hb0, y10, yv0);
+      c1[j] = clamp_bytes(b1[j], c1[j], hb1, y11, yv1);
+    }
+    sad_bisect<P, NB>(c0, c1, l0, l1);
+    return (h0 << 8) | (h1 << 24) | l0 | (l1 << 16);
+  }
+  {
+    uint32_t b0[NB], b1[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) gather_bytes<1>(k[4 * j], k[4 * j + 1], k[4 * j + 2], k[4 * j + 3], b0[j], b1[j]);
+    sad_bisect<P, NB>(b0, b1, h0, h1);
+  }
+  const uint32_t lo = (h0 << 8) | (h1 << 24), hi = lo | 0x00ff00ffu;
+  uint32_t b0[NB], b1[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    uint32_t c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const ushort2_t x = __builtin_bit_cast(ushort2_t, k[4 * j + u]);
+      c[u] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
+                                              __builtin_elementwise_max(x, __builtin_bit_cast(ushort2_t, lo)),
+                                              __builtin_bit_cast(ushort2_t, hi)));
+    }
+    gather_bytes<0>(c[0], c[1], c[2], c[3], b0[j], b1[j]);
+  }
+  sad_bisect<P, NB>(b0, b1, l0, l1);
+  return lo | l0 | (l1 << 16);
+}
+
+template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256, bool COUNT = false>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(COUNT && FEDAGG_PK16_COUNT_HL ? 3 : 2)))
+void median_pk16_lanes_kernel(
     const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out) {
   static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column pair");
   static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
@@ -873,6 +1059,12 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
       first_hi = min(first_hi, __shfl_xor(first_hi, m, 64));
     }
   }
+  uint32_t bits;
+  if constexpr (COUNT) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) raw[j] = pk16_ukey(raw[j]);
+    bits = pk16_from_ukey(pk16_count_median<P, R>(raw));
+  } else {
   short2_t v[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) v[j] = pk16_key(raw[j]);
@@ -898,7 +1090,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
     if constexpr (P >= 16) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<7>()>(m));  // quad maxima
     if constexpr (P >= 32) m = __builtin_elementwise_max(m, dpp_mov<dpp_xor_ctrl<15>()>(m));  // row halves
   }
-  uint32_t bits = pk16_bits(m);
+  bits = pk16_bits(m);
+  }
   if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
   if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
   if constexpr (TAIL) {
@@ -908,21 +1101,21 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   }
 }
 
-template <int P, int R, class E, int BS = 256>
+template <int P, int R, class E, int BS = 256, bool COUNT = false>
 int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
   const int64_t pairs = N / 2;
   const int64_t grid = (pairs * P + BS - 1) / BS;
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
   if (pairs > 0) {
     if (K == P * R)
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0, st,
-                         src, K, pairs, out);
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS, COUNT>), dim3(unsigned(grid)), dim3(BS),
+                         0, st, src, K, pairs, out);
     else
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS>), dim3(unsigned(grid)), dim3(BS), 0,
-                         st, src, K, pairs, out);
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS, COUNT>), dim3(unsigned(grid)), dim3(BS),
+                         0, st, src, K, pairs, out);
   }
   if (N & 1)
-    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS>), dim3(1), dim3(BS), 0, st, src, K,
+    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS, COUNT>), dim3(1), dim3(BS), 0, st, src, K,
                        pairs, out);
   return check_launch("fedagg_median");
 }
@@ -1029,6 +1222,12 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
     if constexpr (sizeof(typename E::S) == 2) {
       if (aligned && K <= 4096) {  // two columns per lane on packed int16 keys
+        if constexpr (FEDAGG_PK16_COUNT) {  // selection by counting: R values per lane, 256 / R .. 1024 / R lanes
+          constexpr int RC = FEDAGG_PK16_COUNT_R;
+          if (K <= 256) return launch_median_pk16_lanes<256 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
+          if (K <= 512) return launch_median_pk16_lanes<512 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
+          if (K <= 1024) return launch_median_pk16_lanes<1024 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
+        }
         if (K <= 256) return launch_median_pk16_lanes<4, 64, E>(d_src, K, N, d_out, st);
         if (K <= 512) return launch_median_pk16_lanes<4, 128, E>(d_src, K, N, d_out, st);
         if (K <= 1024) return launch_median_pk16_lanes<8, 128, E>(d_src, K, N, d_out, st);

@@ -635,6 +635,10 @@ __global__ __launch_bounds__(256) void tri_finish_kernel(const double* __restric
 // order as the reference's own fp32 torch.norm when the clients' spread is
 // of the order of their distances (tests/test_gpu_dist_defenses.py checks
 // the Krum selections and D against the exact-difference kernel).
+// 1: consecutive tiles of a wave share their A fragment's LDS reads
+#ifndef FEDAGG_GRAM_AREUSE
+#define FEDAGG_GRAM_AREUSE 1
+#endif
 constexpr int kGramMax = 128;          // clients the Gram kernel holds (8 groups of 16)
 constexpr int kGramBS = 256;           // 4 waves: one per SIMD
 constexpr int kGramRS = kStage + 4;    // LDS row stride in floats
@@ -780,6 +784,7 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
     // issue-stalled 42 % of their cycles, SQ_WAIT_INST_ANY)
     f32x4v acc[TPW];
     float A0[16], B0[16], A1[16], B1[16];
+    int held = -1;  // the client group whose A fragment A0 holds (FEDAGG_GRAM_AREUSE)
 #pragma unroll
     for (int j = 0; j < TPW; j += 2) {
       acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -788,10 +793,28 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
         const int2 ab0 = gram_tile(t0 + j, nb);
         const bool two = j + 1 < TPW && j + 1 < nmine;
         const int2 ab1 = two ? gram_tile(t0 + j + 1, nb) : ab0;
-        frag(buf, ab0.x, A0);
-        frag(buf, ab0.y, B0);
-        frag(buf, ab1.x, A1);
-        frag(buf, ab1.y, B1);
+        if constexpr (FEDAGG_GRAM_AREUSE) {
+          // a wave's tiles run along rows of the triangle, so consecutive tiles
+          // mostly share their A group: read it once (LDS reads are ~half the
+          // MFMA time here), and take tile j + 1's A from A0 when it matches
+          if (ab0.x != held) {
+            frag(buf, ab0.x, A0);
+            held = ab0.x;
+          }
+          frag(buf, ab0.y, B0);
+          if (ab1.x != ab0.x) {
+            frag(buf, ab1.x, A1);
+          } else {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) A1[m] = A0[m];
+          }
+          frag(buf, ab1.y, B1);
+        } else {
+          frag(buf, ab0.x, A0);
+          frag(buf, ab0.y, B0);
+          frag(buf, ab1.x, A1);
+          frag(buf, ab1.y, B1);
+        }
         if (two) {
 #pragma unroll
           for (int m = 0; m < 16; ++m) {
@@ -801,6 +824,13 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
         } else {
 #pragma unroll
           for (int m = 0; m < 16; ++m) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[m], B0[m], acc[j], 0, 0, 0);
+        }
+        if constexpr (FEDAGG_GRAM_AREUSE) {
+          if (two && ab1.x != held) {  // the next pair most likely continues tile j + 1's row
+#pragma unroll
+            for (int m = 0; m < 16; ++m) A0[m] = A1[m];
+            held = ab1.x;
+          }
         }
       }
     }

@@ -21,7 +21,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "tools", "_build")
+OUT = os.path.join(ROOT, os.environ.get("GRAM_AB_DIR", os.path.join("tools", "_build")))
 # tag -> -D flags of the knobs under test (none are left in robust.hip: the
 # round-3 probes of a swizzled 72-float LDS row and of block-pipelined
 # fragment reads were bit-identical and slower, 5.97 and 8.49 ms against

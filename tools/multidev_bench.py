@@ -45,6 +45,7 @@ def main() -> None:
     ap.add_argument("--clients", type=int, default=32)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--shards", type=int, nargs="*", default=[1, 2, 4])
+    ap.add_argument("--out", default="gpurun_out/r04/multidev_bench.json")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     entries = shapes.resnet50()
@@ -113,8 +114,8 @@ def main() -> None:
         print("device", G, res["device"][f"G{G}"], flush=True)
         del b, views, out
         torch.cuda.empty_cache()
-    os.makedirs("gpurun_out/r03", exist_ok=True)
-    json.dump(res, open("gpurun_out/r03/multidev_bench.json", "w"), indent=1)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    json.dump(res, open(a.out, "w"), indent=1)
 
 
 if __name__ == "__main__":
