@@ -1316,10 +1316,18 @@ void parallel_ranges(int32_t n, const int64_t* nbytes, int32_t threads, SrcAt sr
   }
   const int64_t per = ((total + T - 1) / T + 4095) & ~int64_t(4095);
   const int parts = int((total + per - 1) / per);
-  PackPool::get().run(parts, [&](int t) {
+  auto part = [&](int t) {
     const int64_t b0 = int64_t(t) * per, b1 = b0 + per < total ? b0 + per : total;
     work(b0, b1);
-  });
+  };
+  const char* sp = getenv("FEDAGG_PACK_SPAWN");  // "1": round 3's thread per part and call (A/B, read per call)
+  if (sp && sp[0] == '1') {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < parts; ++t) pool.emplace_back(part, t);
+    for (auto& th : pool) th.join();
+    return;
+  }
+  PackPool::get().run(parts, part);
 }
 
 int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, const int64_t* nbytes,

@@ -28,19 +28,16 @@
 #ifndef FEDAGG_PK16_COUNT
 #define FEDAGG_PK16_COUNT 1
 #endif
-// values per lane of the counting kernels (P = KMAX / R lanes per column pair)
+// values per lane of the counting kernels (P = KMAX / R lanes per column pair;
+// 64 and 32, i.e. 8 and 16 rows per wave instruction, ran config 4 in 32 and
+// 66 ms against 21 ms at 128: profiles/r04/c/median_ab_variants.json)
 #ifndef FEDAGG_PK16_COUNT_R
 #define FEDAGG_PK16_COUNT_R 128
 #endif
-// independent v_sad_u8 accumulator chains per sum
+// independent v_sad_u8 accumulator chains per sum (4: 21.3 vs 22.5 ms at
+// config 4's 512 clients, profiles/r04/c/)
 #ifndef FEDAGG_SAD_CHAINS
-#define FEDAGG_SAD_CHAINS 2
-#endif
-// 1: the low bytes are gathered with the high bytes up front and clamped in
-// the byte domain (SWAR compares), so the 16-bit keys need not stay live
-// through the high phase: 128 instead of 192 registers of keys per lane
-#ifndef FEDAGG_PK16_COUNT_HL
-#define FEDAGG_PK16_COUNT_HL 0
+#define FEDAGG_SAD_CHAINS 4
 #endif
 // Loads of the lane-group kernels: a wave instruction reads 64 B of each of P
 // rows' 128-B lines and the block's next wave reads the other half, so plain
@@ -924,54 +921,12 @@ __device__ __forceinline__ void gather_bytes(uint32_t k0, uint32_t k1, uint32_t 
   c0 = __builtin_amdgcn_perm(t23, t01, 0x06040200u);
   c1 = __builtin_amdgcn_perm(t23, t01, 0x07050301u);
 }
-// Per byte of four keys' high bytes H and low bytes L against the median's
-// high byte h: 0 where H < h, 255 where H > h, L where H == h.  Unsigned byte
-// compares without a borrow between bytes: a byte's low 7 bits compare as
-// (x | 0x80) - (y + 1), whose bit 7 is x > y; the top bits decide the rest
-// (bitop3: (x & ~y) | (~(x ^ y) & low)).  Bit 7 of every byte then widens to
-// the byte with v_perm_b32's sign-replicating selectors (8..11: bytes 1, 3,
-// 5, 7 of {S0, S1}; the flags shifted up a byte fill bytes 1 and 3 of S1).
-// hb = h * 0x01010101, y1 = (hb & 0x7f7f7f7f) + 0x01010101, yv = h >= 128 ? ~0 : 0.
-__device__ __forceinline__ uint32_t msb_bytes(uint32_t f) {
-  return __builtin_amdgcn_perm(f, f << 8, 0x0B090A08u);
-}
-__device__ __forceinline__ uint32_t clamp_bytes(uint32_t H, uint32_t L, uint32_t hb, uint32_t y1, uint32_t yv) {
-  const uint32_t t = (H | 0x80808080u) - y1;
-  const uint32_t gt = (H & ~yv) | (~(H ^ yv) & t);  // bit 7: H > h
-  const uint32_t t2 = (hb | 0x80808080u) - ((H & 0x7f7f7f7fu) + 0x01010101u);
-  const uint32_t lt = (hb & ~H) | (~(hb ^ H) & t2);  // bit 7: h > H
-  const uint32_t gm = msb_bytes(gt), lm = msb_bytes(lt);
-  return (L & ~(lm | gm)) | gm;
-}
 // the two columns' lower medians as packed order keys, from this lane's R
 // packed key registers (column 0 in the low halves)
 template <int P, int R>
 __device__ __forceinline__ uint32_t pk16_count_median(uint32_t (&k)[R]) {
   constexpr int NB = R / 4;
   uint32_t h0, h1, l0, l1;
-  if constexpr (FEDAGG_PK16_COUNT_HL) {
-    uint32_t b0[NB], b1[NB], c0[NB], c1[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      gather_bytes<1>(k[4 * j], k[4 * j + 1], k[4 * j + 2], k[4 * j + 3], b0[j], b1[j]);
-      gather_bytes<0>(k[4 * j], k[4 * j + 1], k[4 * j + 2], k[4 * j + 3], c0[j], c1[j]);
-    }
-    // the low bytes exist before the high phase, so the 16-bit keys die here
-    // (left alone, the scheduler sinks their gathers to the low phase)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) asm volatile("" : "+v"(c0[j]), "+v"(c1[j]));
-    sad_bisect<P, NB>(b0, b1, h0, h1);
-    const uint32_t hb0 = h0 * 0x01010101u, hb1 = h1 * 0x01010101u;
-    const uint32_t y10 = (hb0 & 0x7f7f7f7fu) + 0x01010101u, y11 = (hb1 & 0x7f7f7f7fu) + 0x01010101u;
-    const uint32_t yv0 = h0 >= 128u ? ~0u : 0u, yv1 = h1 >= 128u ? ~0u : 0u;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      c0[j] = clamp_bytes(b0[j], c0[j], hb0, y10, yv0);
-      c1[j] = clamp_bytes(b1[j], c1[j], hb1, y11, yv1);
-    }
-    sad_bisect<P, NB>(c0, c1, l0, l1);
-    return (h0 << 8) | (h1 << 24) | l0 | (l1 << 16);
-  }
   {
     uint32_t b0[NB], b1[NB];
 #pragma unroll
@@ -997,8 +952,7 @@ __device__ __forceinline__ uint32_t pk16_count_median(uint32_t (&k)[R]) {
 }
 
 template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256, bool COUNT = false>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(COUNT && FEDAGG_PK16_COUNT_HL ? 3 : 2)))
-void median_pk16_lanes_kernel(
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
     const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out) {
   static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column pair");
   static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");

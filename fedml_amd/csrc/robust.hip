@@ -635,9 +635,16 @@ __global__ __launch_bounds__(256) void tri_finish_kernel(const double* __restric
 // order as the reference's own fp32 torch.norm when the clients' spread is
 // of the order of their distances (tests/test_gpu_dist_defenses.py checks
 // the Krum selections and D against the exact-difference kernel).
-// 1: consecutive tiles of a wave share their A fragment's LDS reads
-#ifndef FEDAGG_GRAM_AREUSE
-#define FEDAGG_GRAM_AREUSE 1
+// stages (64 columns each) summed in fp32 by the MFMAs before one fp64 fold
+// (2 / 4: 5.19 / 5.09 against 5.44 ms at config 3, for a 2x / 4x longer fp32
+// chain per partial; profiles/r04/f/gram_map.json; kept at 1)
+#ifndef FEDAGG_GRAM_FOLD
+#define FEDAGG_GRAM_FOLD 1
+#endif
+// Diagnostics for tools/gram_variants.py (wrong results, timing only):
+// 1 skips the MFMA phase, 2 skips the staging of every stage after the first
+#ifndef FEDAGG_GRAM_DIAG
+#define FEDAGG_GRAM_DIAG 0
 #endif
 constexpr int kGramMax = 128;          // clients the Gram kernel holds (8 groups of 16)
 constexpr int kGramBS = 256;           // 4 waves: one per SIMD
@@ -730,6 +737,16 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
     }
     return true;
   };
+  auto fetch_skip = [&]() {  // FEDAGG_GRAM_DIAG == 2: advance the stage walk only
+    if (c >= n_chunks) return false;
+    const int len = int(chunks[2 * c + 1]);
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
   // Staging, in two halves around a barrier: stage_sums publishes this
   // wave's column sums of the loaded rows (still in registers), and once
   // every wave's sums are in, stage_centred writes the rows minus the column
@@ -777,44 +794,38 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
       F[4 * k + 3] = x.w;
     }
   };
+  // fp32 MFMA accumulators, folded into acc64 every FEDAGG_GRAM_FOLD stages
+  f32x4v acc[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  int unfolded = 0;
+  auto fold = [&]() {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      acc64[j][0] += double(acc[j].x);
+      acc64[j][1] += double(acc[j].y);
+      acc64[j][2] += double(acc[j].z);
+      acc64[j][3] += double(acc[j].w);
+      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+    unfolded = 0;
+  };
   auto compute = [&](int buf) {
     // tiles two at a time, their MFMAs interleaved: two independent
     // accumulation chains hide the 16x16x4 MFMA's dependent latency (40
     // cycles against a 32-cycle issue; one chain at a time left the waves
     // issue-stalled 42 % of their cycles, SQ_WAIT_INST_ANY)
-    f32x4v acc[TPW];
     float A0[16], B0[16], A1[16], B1[16];
-    int held = -1;  // the client group whose A fragment A0 holds (FEDAGG_GRAM_AREUSE)
 #pragma unroll
     for (int j = 0; j < TPW; j += 2) {
-      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      if (j + 1 < TPW) acc[j + 1] = f32x4v{0.f, 0.f, 0.f, 0.f};
       if (j < nmine) {
         const int2 ab0 = gram_tile(t0 + j, nb);
         const bool two = j + 1 < TPW && j + 1 < nmine;
         const int2 ab1 = two ? gram_tile(t0 + j + 1, nb) : ab0;
-        if constexpr (FEDAGG_GRAM_AREUSE) {
-          // a wave's tiles run along rows of the triangle, so consecutive tiles
-          // mostly share their A group: read it once (LDS reads are ~half the
-          // MFMA time here), and take tile j + 1's A from A0 when it matches
-          if (ab0.x != held) {
-            frag(buf, ab0.x, A0);
-            held = ab0.x;
-          }
-          frag(buf, ab0.y, B0);
-          if (ab1.x != ab0.x) {
-            frag(buf, ab1.x, A1);
-          } else {
-#pragma unroll
-            for (int m = 0; m < 16; ++m) A1[m] = A0[m];
-          }
-          frag(buf, ab1.y, B1);
-        } else {
-          frag(buf, ab0.x, A0);
-          frag(buf, ab0.y, B0);
-          frag(buf, ab1.x, A1);
-          frag(buf, ab1.y, B1);
-        }
+        frag(buf, ab0.x, A0);
+        frag(buf, ab0.y, B0);
+        frag(buf, ab1.x, A1);
+        frag(buf, ab1.y, B1);
         if (two) {
 #pragma unroll
           for (int m = 0; m < 16; ++m) {
@@ -825,22 +836,9 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 #pragma unroll
           for (int m = 0; m < 16; ++m) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[m], B0[m], acc[j], 0, 0, 0);
         }
-        if constexpr (FEDAGG_GRAM_AREUSE) {
-          if (two && ab1.x != held) {  // the next pair most likely continues tile j + 1's row
-#pragma unroll
-            for (int m = 0; m < 16; ++m) A0[m] = A1[m];
-            held = ab1.x;
-          }
-        }
       }
     }
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      acc64[j][0] += double(acc[j].x);
-      acc64[j][1] += double(acc[j].y);
-      acc64[j][2] += double(acc[j].z);
-      acc64[j][3] += double(acc[j].w);
-    }
+    if (++unfolded == FEDAGG_GRAM_FOLD) fold();
   };
   // stage s computes from buffer s & 1 while stage s + 1 is staged into the
   // other (sums, barrier, centred rows) and stage s + 2's loads are in
@@ -853,8 +851,12 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
     have = fetch();
     lds_barrier();
     for (int buf = 0;; buf ^= 1) {
-      compute(buf);
+      if constexpr (FEDAGG_GRAM_DIAG != 1) compute(buf);
       if (!have) break;
+      if constexpr (FEDAGG_GRAM_DIAG == 2) {  // same stage count, no loads, sums or barriers
+        have = fetch_skip();
+        continue;
+      }
       stage_sums(buf ^ 1);
       lds_barrier();
       stage_centred(buf ^ 1);
@@ -862,6 +864,7 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
       lds_barrier();
     }
   }
+  if (unfolded) fold();
   // C/D layout of the 16x16 MFMA: lane l holds row 4 * (l >> 4) + r, column l & 15
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {

@@ -46,6 +46,10 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--shards", type=int, nargs="*", default=[1, 2, 4])
     ap.add_argument("--out", default="gpurun_out/r04/multidev_bench.json")
+    ap.add_argument("--ingest", action="store_true",
+                    help="also time put() x K + reduce_to_host on resident buckets, the G values interleaved")
+    ap.add_argument("--ab-pack", action="store_true",
+                    help="host rounds: time the pack pool and round 3's threads per call, interleaved")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     entries = shapes.resnet50()
@@ -63,19 +67,28 @@ def main() -> None:
     nbytes = K * sum(t.numel() * t.element_size() for t in raw[0][1].values())
     res = {"clients": K, "model": "resnet50", "host_bytes_per_round": nbytes, "host": {}, "device": {}}
     ref_host = None
+    modes = ["pool", "spawn"] if a.ab_pack else ["pool"]
     for G in a.shards:
         args = Args()
         args.fedagg_devices = [dev] * G
         ts = []
+        tmode = {m: [] for m in modes}
         out = None
         for r in range(a.reps + 1):
-            lst = [(n, OrderedDict(d)) for n, d in raw]
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            out = ao.FedMLAggOperator.agg(args, lst)
-            torch.cuda.synchronize()
-            if r:
-                ts.append(time.perf_counter() - t0)
+            order = modes[r % len(modes):] + modes[:r % len(modes)]
+            for m in order:  # --ab-pack: the native pack's pool vs round 3's threads per call, interleaved
+                os.environ["FEDAGG_PACK_SPAWN"] = "1" if m == "spawn" else "0"
+                lst = [(n, OrderedDict(d)) for n, d in raw]
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                out = ao.FedMLAggOperator.agg(args, lst)
+                torch.cuda.synchronize()
+                if r:
+                    tmode[m].append(time.perf_counter() - t0)
+        os.environ["FEDAGG_PACK_SPAWN"] = "0"
+        ts = tmode["pool"]
+        if a.ab_pack:
+            res.setdefault("host_spawn_ms", {})[f"G{G}"] = round(statistics.median(tmode["spawn"]) * 1e3, 2)
         if ref_host is None:
             ref_host = out
         same = all(torch.equal(out[k].view(-1).view(torch.int32) if out[k].dtype == torch.float32 else out[k],
@@ -114,6 +127,37 @@ def main() -> None:
         print("device", G, res["device"][f"G{G}"], flush=True)
         del b, views, out
         torch.cuda.empty_cache()
+    if a.ingest:
+        # the cross-silo arrival path: every client put() into resident
+        # buckets (one per G, built once), then reduce_to_host; the G values
+        # interleaved per round in this one process, so host drift cancels
+        buckets = {G: MultiDeviceBucket([(k, s, dt) for k, s, dt in entries], K, [dev] * G) for G in a.shards}
+        ns = [n for n, _ in raw]
+        tin = {G: [] for G in a.shards}
+        outs = {}
+        for r in range(a.reps * 2 + 1):
+            order = a.shards[r % len(a.shards):] + a.shards[:r % len(a.shards)]
+            for G in order:
+                b = buckets[G]
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i, (n, d) in enumerate(raw):
+                    b.put(i, d, n)
+                outs[G] = b.reduce_to_host(b.weights(ns))
+                torch.cuda.synchronize()
+                if r:
+                    tin[G].append(time.perf_counter() - t0)
+        g0 = a.shards[0]
+        res["ingest"] = {}
+        for G in a.shards:
+            same = all(torch.equal(outs[G][k].view(-1).view(torch.int32) if outs[G][k].dtype == torch.float32 else
+                                   outs[G][k], outs[g0][k].view(-1).view(torch.int32)
+                                   if outs[g0][k].dtype == torch.float32 else outs[g0][k]) for k in outs[g0])
+            ms = statistics.median(tin[G]) * 1e3
+            res["ingest"][f"G{G}"] = {"ms": round(ms, 2), "GBps_host_in": round(nbytes / ms / 1e6, 1),
+                                      "vs_G1": round(ms / (statistics.median(tin[g0]) * 1e3), 4),
+                                      "bitwise_equal_to_G1": same}
+            print("ingest", G, res["ingest"][f"G{G}"], flush=True)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
 
