@@ -727,7 +727,10 @@ def main():
             # client axis + RCCL reduce-scatter runs next on the same clients
             del step, outs, gd, groups, bucket  # free this rank's rows first
             torch.cuda.empty_cache()
-            line["exchange"] = measure_client_axis(a, entries, n_elems, K_total, world, rank, dev)
+            try:
+                line["exchange"] = measure_client_axis(a, entries, n_elems, K_total, world, rank, dev)
+            except Exception as e:  # the headline above stands; report what the nested run hit
+                line["exchange"] = {"mode": "client", "error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
         line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
     if rank == 0:

@@ -60,6 +60,7 @@ SIGNATURES = {
     "fedagg_sum_mod_i64": (ctypes.c_int, [_P, _I32, _I64, _I64, _P, _U32, _P]),
     "fedagg_lsa_reconstruct_f32": (ctypes.c_int, [_P, _I32, _I64, _P, _I64, _I32, _F, _P, _U32, _P]),
     "fedagg_host_pack": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32]),
+    "fedagg_host_gather": (ctypes.c_int, [_P, _P, _P, _I32, _I32]),
     "fedagg_host_unpack": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32]),
     "fedagg_host_round_f32": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P]),
     "fedagg_robust_work_len": (_I64, [_I32, _I32, _I64]),

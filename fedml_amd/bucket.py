@@ -47,6 +47,23 @@ def _pad(n: int) -> int:
     return (n + _ROW_ALIGN - 1) // _ROW_ALIGN * _ROW_ALIGN
 
 
+def gather_jobs(jobs: Sequence[dict], threads: int = _PACK_THREADS) -> None:
+    """Pack the byte ranges of staging jobs (ClientBucket.put_prepare /
+    put_from_table_prepare, of one bucket or of every shard of a
+    MultiDeviceBucket) into their pinned rows in ONE native call
+    (fedagg_host_gather: one persistent thread pool, no GIL)."""
+    parts = [j for j in jobs if j.get("srcs") is not None and len(j["srcs"])]
+    if not parts:
+        return
+    srcs = np.ascontiguousarray(np.concatenate([np.asarray(j["srcs"]).astype(np.uint64, copy=False) for j in parts]))
+    dsts = np.ascontiguousarray(np.concatenate([np.asarray(j["dsts"]).astype(np.int64, copy=False) for j in parts]))
+    nb = np.ascontiguousarray(np.concatenate([np.asarray(j["nbytes"]).astype(np.int64, copy=False) for j in parts]))
+    nat.check(nat.lib().fedagg_host_gather(dsts.ctypes.data, srcs.ctypes.data, nb.ctypes.data, int(nb.size), threads),
+              "host_gather")
+    for j in parts:
+        j["keep"] = None  # converted sources are no longer needed
+
+
 class ClientBucket:
     """One round's client updates in HBM, laid out for the streaming reduction.
 
@@ -127,6 +144,18 @@ class ClientBucket:
         staging is double-buffered, so packing the next client overlaps this
         client's PCIe transfer.  The reduction waits for every pending H2D
         (``sync_ingest``, called by reduce_into)."""
+        jobs = self.put_prepare(slot, state_dict, sample_num)
+        gather_jobs(jobs)
+        self.put_issue(jobs)
+
+    def put_prepare(self, slot: int, state_dict, sample_num: float) -> list:
+        """put()'s first half: device tensors are copied D2D now; every dtype
+        group with host keys gets a staging job (a pinned row of its ring,
+        whose previous H2D has landed, and the byte ranges to gather into
+        it).  ``gather_jobs`` packs the jobs of one or several buckets in ONE
+        native call and ``put_issue`` sends them: a MultiDeviceBucket packs
+        every GPU's keys of an arriving client together and then issues the G
+        H2Ds back to back."""
         if not 0 <= slot < self.capacity:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
         host: Dict[torch.dtype, List[Tuple[int, int, int, torch.Tensor]]] = {}
@@ -146,9 +175,14 @@ class ClientBucket:
                 dev_seen[g.dtype] = dev_seen.get(g.dtype, 0) + 1
             else:
                 host.setdefault(g.dtype, []).append((dev_seen.get(g.dtype, 0), g.offsets[j], g.numels[j], t))
-        for dt, parts in host.items():
-            self._stage(dt, slot, parts)
+        jobs = [self._stage_prepare(dt, slot, parts) for dt, parts in host.items()]
         self.sample_nums[slot] = sample_num
+        return jobs
+
+    def put_issue(self, jobs: list) -> None:
+        """put()'s second half: the gathered staging rows' async H2Ds."""
+        for job in jobs:
+            self._stage_issue(job)
 
     def put_encoded(self, slot: int, message) -> None:
         """Ingest a FAGG wire message (fedml_amd.wire): its payload already IS
@@ -244,6 +278,15 @@ class ClientBucket:
         row of the ring plus ONE async H2D, with no per-key Python work apart
         from integer keys promoted into the fp32 rows (converted from
         state_dict)."""
+        jobs = self.put_from_table_prepare(slot, tables, state_dict, sample_num)
+        gather_jobs(jobs)
+        self.put_issue(jobs)
+
+    def put_from_table_prepare(self, slot: int, tables: Dict[int, "np.ndarray"], state_dict,
+                               sample_num: float) -> list:
+        """put_from_table()'s first half (as put_prepare): per dtype group a
+        staging job whose sources are the walker table's pointers of this
+        slot; promoted integer keys are converted into the staging row here."""
         code_dt = {nat.DT_F32: torch.float32, nat.DT_BF16: torch.bfloat16, nat.DT_F16: torch.float16,
                    nat.DT_F64: torch.float64, nat.DT_I64: torch.int64}
         if self._copy is None:
@@ -251,34 +294,36 @@ class ClientBucket:
             self._copy.wait_stream(torch.cuda.current_stream(self.device))
         plans = self._table_plans()
         by_dt = {code_dt[c]: t for c, t in tables.items()}
+        jobs = []
         for dt, g in self.groups.items():
             if g.length == 0:
                 continue
             native, offs, nb, ints = plans[dt]
-            st = self._staging.get(dt)
-            if st is None:
-                st = self._staging[dt] = {"bufs": [[torch.empty(g.length, dtype=dt).pin_memory(), None]
-                                                   for _ in range(_STAGES)], "next": 0}
-            b = st["bufs"][st["next"]]
-            st["next"] = (st["next"] + 1) % _STAGES
-            if b[1] is not None:
-                b[1].synchronize()
+            b = self._ring_row(dt, g)
             stage = b[0]
+            job = {"dt": dt, "slot": slot, "buf": b, "whole": True, "keep": None}
             if native.size:
-                srcs = np.ascontiguousarray(by_dt[dt][native, slot])
-                nat.check(nat.lib().fedagg_host_pack(stage.data_ptr(), srcs.ctypes.data, offs.ctypes.data,
-                                                     nb.ctypes.data, int(srcs.size), _PACK_THREADS), "host_pack")
+                job["srcs"] = np.ascontiguousarray(by_dt[dt][native, slot])
+                job["dsts"] = offs + stage.data_ptr()
+                job["nbytes"] = nb
             for key, lo, n in ints:
                 stage[lo:lo + n].copy_(state_dict[key].reshape(-1))
-            self._order_after_readers()
-            with torch.cuda.stream(self._copy):
-                g.rows[slot, :g.length].copy_(stage[:g.length], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self._copy)
-            b[1] = ev
-            self._pending = True
-            self._pending_other = True
+            jobs.append(job)
         self.sample_nums[slot] = sample_num
+        return jobs
+
+    def _ring_row(self, dt: torch.dtype, g) -> list:
+        """The next pinned staging row of dtype group g's ring, once its
+        previous H2D has landed: [row, event of its last H2D]."""
+        st = self._staging.get(dt)
+        if st is None:  # per dtype group: _STAGES pinned rows used round-robin
+            st = self._staging[dt] = {"bufs": [[torch.empty(g.length, dtype=dt).pin_memory(), None]
+                                               for _ in range(_STAGES)], "next": 0}
+        b = st["bufs"][st["next"]]
+        st["next"] = (st["next"] + 1) % _STAGES
+        if b[1] is not None:
+            b[1].synchronize()  # this staging row's previous H2D has landed
+        return b
 
     def _table_plans(self):
         """Per dtype group: the rows of the walker's table that feed it (keys of
@@ -305,19 +350,12 @@ class ClientBucket:
             self._tplans = plans
         return self._tplans
 
-    def _stage(self, dt: torch.dtype, slot: int, parts) -> None:
+    def _stage_prepare(self, dt: torch.dtype, slot: int, parts) -> dict:
         g = self.groups[dt]
         if self._copy is None:
             self._copy = torch.cuda.Stream(self.device)
             self._copy.wait_stream(torch.cuda.current_stream(self.device))  # rows were zero-filled there
-        st = self._staging.get(dt)
-        if st is None:  # per dtype group: _STAGES pinned rows used round-robin
-            st = self._staging[dt] = {"bufs": [[torch.empty(g.length, dtype=dt).pin_memory(), None]
-                                               for _ in range(_STAGES)], "next": 0}
-        b = st["bufs"][st["next"]]
-        st["next"] = (st["next"] + 1) % _STAGES
-        if b[1] is not None:
-            b[1].synchronize()  # this staging row's previous H2D has landed
+        b = self._ring_row(dt, g)
         stage = b[0]
         # parts: (run, element offset, count, tensor) in layout order; a run
         # is a stretch of host keys with no device key between them, and each
@@ -327,43 +365,52 @@ class ClientBucket:
         for run, off, n, _ in parts:
             r = runs.setdefault(run, [off, off + n])
             r[0], r[1] = min(r[0], off), max(r[1], off + n)
-        lo = min(r[0] for r in runs.values())
         esz = stage.element_size()
+        base = stage.data_ptr()
         keep = []
-        srcs, offs, nbytes = [], [], []
+        srcs, dsts, nbytes = [], [], []
         for _, off, n, t in parts:
             src = t.reshape(-1)
             if src.dtype != dt or not src.is_contiguous():
                 src = src.to(dt).contiguous()
                 keep.append(src)
             srcs.append(src.data_ptr())
-            offs.append((off - lo) * esz)
+            dsts.append(base + off * esz)
             nbytes.append(n * esz)
-        n = len(srcs)
-        nat.check(nat.lib().fedagg_host_pack(stage[lo:].data_ptr(), (ctypes.c_void_p * n)(*srcs),
-                                             (ctypes.c_int64 * n)(*offs), (ctypes.c_int64 * n)(*nbytes), n,
-                                             _PACK_THREADS), "host_pack")
-        del keep
+        return {"dt": dt, "slot": slot, "buf": b, "whole": False, "runs": sorted(runs.values()), "keep": keep,
+                "srcs": np.asarray(srcs, dtype=np.uint64), "dsts": np.asarray(dsts, dtype=np.int64),
+                "nbytes": np.asarray(nbytes, dtype=np.int64)}
+
+    def _stage_issue(self, job: dict) -> None:
+        """The H2D of a gathered staging job on the copy stream: a put() job
+        in pieces of _PIECE columns, each with an event (the pipelined round
+        end starts reducing a column range as soon as the last client's bytes
+        for it have landed); a walked-table job as one copy of the row."""
+        dt, slot, b = job["dt"], job["slot"], job["buf"]
+        g = self.groups[dt]
+        stage = b[0]
         self._order_after_readers()
         with torch.cuda.stream(self._copy):
-            # in pieces of _PIECE columns, each with an event: the pipelined
-            # round end (reduce_to_host) starts reducing a column range as soon
-            # as the last client's bytes for it have landed
-            last = self._piece_events.setdefault(dt, {})
-            for a, e in sorted(runs.values()):
-                while a < e:
-                    p = a // _PIECE
-                    z = min(e, (p + 1) * _PIECE)
-                    g.rows[slot, a:z].copy_(stage[a:z], non_blocking=True)
-                    pev = torch.cuda.Event()
-                    pev.record(self._copy)
-                    self._piece_seq += 1
-                    last[p] = (self._piece_seq, pev)
-                    a = z
+            if job["whole"]:
+                g.rows[slot, :g.length].copy_(stage[:g.length], non_blocking=True)
+            else:
+                last = self._piece_events.setdefault(dt, {})
+                for a, e in job["runs"]:
+                    while a < e:
+                        p = a // _PIECE
+                        z = min(e, (p + 1) * _PIECE)
+                        g.rows[slot, a:z].copy_(stage[a:z], non_blocking=True)
+                        pev = torch.cuda.Event()
+                        pev.record(self._copy)
+                        self._piece_seq += 1
+                        last[p] = (self._piece_seq, pev)
+                        a = z
             ev = torch.cuda.Event()
             ev.record(self._copy)
         b[1] = ev
         self._pending = True
+        if job["whole"]:
+            self._pending_other = True
 
     def _order_after_readers(self) -> None:
         """An H2D into the rows must not overtake work already enqueued on the

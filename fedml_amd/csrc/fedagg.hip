@@ -1888,6 +1888,18 @@ int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs
   return FEDAGG_OK;
 }
 
+int fedagg_host_gather(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int32_t n,
+                       int32_t threads) {
+  if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes))) return set_error(FEDAGG_EINVAL, "fedagg_host_gather: bad argument");
+  for (int32_t i = 0; i < n; ++i)
+    if (nbytes[i] < 0 || (nbytes[i] > 0 && (!dsts[i] || !srcs[i])))
+      return set_error(FEDAGG_EINVAL, "fedagg_host_gather: negative size or null pointer");
+  parallel_ranges(
+      n, nbytes, threads, [&](int32_t i) { return static_cast<const char*>(srcs[i]); },
+      [&](int32_t i) { return static_cast<char*>(dsts[i]); });
+  return FEDAGG_OK;
+}
+
 int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_offs, const int64_t* nbytes, int32_t n,
                        int32_t threads) {
   if (int rc = check_ranges(n, src, dsts, src_offs, nbytes, "fedagg_host_unpack")) return rc;

@@ -22,9 +22,9 @@ the PARAMETER axis inside the process:
   equal LoRA keys exact on 2, 4 and 8.
 * **Ingest.**  ``put`` sends each device its keys from the arriving dict: one
   pinned pack + one async H2D per device and dtype, on that device's own copy
-  stream and PCIe link.  The shards' packs and H2Ds are issued from one
-  thread per shard at the same time (the packs run natively without the GIL
-  on a shared persistent pool), so G links carry a client at once.
+  stream and PCIe link.  Every device's staging row of the arriving client is
+  packed in ONE native gather (fedagg_host_gather, a persistent thread pool),
+  then the G H2Ds are issued back to back, so G links carry a client at once.
 * **Reduction.**  Every device runs the single-GPU kernels over its keys in
   the reference's client order: no exchange and bit-exact with one GPU.
   ``reduce_to_host`` enqueues every device's reductions and D2H copies before
@@ -43,7 +43,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .bucket import ClientBucket, _pad
+from .bucket import ClientBucket, _pad, gather_jobs
 from .layout import INT_DTYPES, numel
 
 Entry = Tuple[str, Tuple[int, ...], torch.dtype]
@@ -267,38 +267,19 @@ class MultiDeviceBucket:
         self.owner: Dict[str, int] = {k: g for g, sub in enumerate(self.plan) for k, _, _ in sub}
         self.sample_nums: List[Optional[float]] = [None] * capacity
         self.int_keys = set().union(*(b.int_keys for b in self.shards))
-        self._pool = None  # ingest threads, one per shard (created at the first multi-shard put)
 
     # ---- ingest ---------------------------------------------------------------
 
-    def _each_shard(self, fn) -> None:
-        """fn(shard) for every shard, the shards concurrently: each shard's
-        pack (native, GIL released) and H2D run beside the others', so G
-        PCIe links are fed at once instead of one after another.  Every
-        worker runs on the caller's current stream of its shard's device (a
-        shard's copy stream orders itself after that stream's earlier work)."""
-        if len(self.shards) == 1:
-            fn(self.shards[0])
-            return
-        if self._pool is None:
-            from concurrent.futures import ThreadPoolExecutor
-
-            self._pool = ThreadPoolExecutor(max_workers=len(self.shards), thread_name_prefix="fedagg-shard")
-        streams = {b.device: torch.cuda.current_stream(b.device) for b in self.shards}
-
-        def run(b):
-            with torch.cuda.device(b.device), torch.cuda.stream(streams[b.device]):
-                fn(b)
-
-        futs = [self._pool.submit(run, b) for b in self.shards]
-        for f in futs:
-            f.result()  # the first shard's error, as a serial loop would raise it
-
     def put(self, slot: int, state_dict, sample_num: float) -> None:
-        """One client: every device takes its keys (one pack + one H2D per
-        dtype on its own copy stream; device tensors D2D), all devices at
-        once."""
-        self._each_shard(lambda b: b.put(slot, state_dict, sample_num))
+        """One client: every device takes its keys (device tensors D2D; host
+        keys packed into each device's pinned staging row, ALL devices' rows
+        in one native gather, then one H2D per device and dtype on its own
+        copy stream, issued back to back so the G links carry the client at
+        once)."""
+        jobs = [(b, b.put_prepare(slot, state_dict, sample_num)) for b in self.shards]
+        gather_jobs([j for _, js in jobs for j in js])
+        for b, js in jobs:
+            b.put_issue(js)
         self.sample_nums[slot] = sample_num
 
     def split_tables(self, tables: Dict[int, np.ndarray]) -> List[Dict[int, np.ndarray]]:
@@ -308,14 +289,16 @@ class MultiDeviceBucket:
                         sample_num: float) -> None:
         """put() for one client of a walked host round (``split_tables`` of
         the walker's tables, computed once per round)."""
-        tab = {id(b): t for b, t in zip(self.shards, shard_tables)}
-        self._each_shard(lambda b: b.put_from_table(slot, tab[id(b)], state_dict, sample_num))
+        jobs = [(b, b.put_from_table_prepare(slot, t, state_dict, sample_num))
+                for b, t in zip(self.shards, shard_tables)]
+        gather_jobs([j for _, js in jobs for j in js])
+        for b, js in jobs:
+            b.put_issue(js)
         self.sample_nums[slot] = sample_num
 
     def put_batch(self, shard_tables: Sequence[Dict[int, np.ndarray]], state_dicts, sample_nums) -> None:
-        tab = {id(b): t for b, t in zip(self.shards, shard_tables)}
-        self._each_shard(lambda b: b.put_batch({c: np.ascontiguousarray(a).ravel() for c, a in tab[id(b)].items()},
-                                               state_dicts, sample_nums))
+        for b, t in zip(self.shards, shard_tables):
+            b.put_batch({c: np.ascontiguousarray(a).ravel() for c, a in t.items()}, state_dicts, sample_nums)
         for i, n in enumerate(sample_nums):
             self.sample_nums[i] = n
 

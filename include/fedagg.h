@@ -370,6 +370,15 @@ int fedagg_host_pack(void* dst, const void* const* srcs, const int64_t* dst_offs
 int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_offs,
                        const int64_t* nbytes, int32_t n, int32_t threads);
 
+/* The general form for a client spread over several destinations: srcs[i]
+ * (nbytes[i] bytes) goes to dsts[i].  A round cut over G GPUs (whole keys per
+ * GPU, fedml_amd.multidev) packs every GPU's pinned staging row of an arriving
+ * client in ONE call, so the G per-GPU H2Ds can be issued together right
+ * after it (the packing half of add_local_trained_result's tensor moves,
+ * cross_silo/server/fedml_aggregator.py:58-67).  Synchronous; host memory only. */
+int fedagg_host_gather(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int32_t n,
+                       int32_t threads);
+
 /* ---- Small host-resident rounds ----------------------------------------- */
 
 /* One whole FedAvg round of HOST tensors, host to host, in one call: the

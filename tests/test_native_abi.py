@@ -174,6 +174,53 @@ def test_host_unpack_scatters_exactly(lib):
         assert np.array_equal(d, src[off:off + d.size])
 
 
+@pytest.mark.parametrize("threads", [1, 8, 16])
+def test_host_gather_to_many_destinations(lib, threads):
+    """fedagg_host_gather (the multi-device ingest's one pack for every GPU's
+    staging row): each source lands in its own destination buffer, bytes
+    around the destinations untouched, sizes above the threading threshold;
+    several callers at once (the pack pool serves concurrent batches)."""
+    import ctypes
+    import threading
+
+    import numpy as np
+
+    rng = np.random.default_rng(2)
+    sizes = [0, 9, 4_000_001, 3, 6_500_000, 1, 131_072]
+
+    def one(seed):
+        r = np.random.default_rng(seed)
+        srcs = [r.integers(0, 255, s, dtype=np.uint8) for s in sizes]
+        bufs = [np.full(s + 2, 0xCD, dtype=np.uint8) for s in sizes]  # one guard byte each side
+        n = len(sizes)
+        rc = lib.fedagg_host_gather((ctypes.c_void_p * n)(*[b.ctypes.data + 1 for b in bufs]),
+                                    (ctypes.c_void_p * n)(*[a.ctypes.data for a in srcs]),
+                                    (ctypes.c_int64 * n)(*sizes), n, threads)
+        assert rc == 0
+        for a, b in zip(srcs, bufs):
+            assert np.array_equal(b[1:1 + a.size], a) and b[0] == 0xCD and b[-1] == 0xCD
+
+    one(int(rng.integers(1 << 30)))
+    errs = []
+
+    def run(seed):
+        try:
+            one(seed)
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(s,)) for s in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errs
+    assert lib.fedagg_host_gather(None, None, None, -1, 1) == -1
+    one_byte = np.zeros(1, dtype=np.uint8)
+    assert lib.fedagg_host_gather((ctypes.c_void_p * 1)(None), (ctypes.c_void_p * 1)(one_byte.ctypes.data),
+                                  (ctypes.c_int64 * 1)(1), 1, 1) == -1
+
+
 def test_dict_walker_builds_and_declines_host_inputs():
     """The native dict walker (csrc/walker.cpp) only ever takes the all-device
     fast path; host tensors and missing keys return None so the Python walk
