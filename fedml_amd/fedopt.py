@@ -298,3 +298,141 @@ class FedOptServer:
                 tot += 2 * n * 4 + (2 * n * 4 if self.mom is not None and not self.first_step else
                                     (n * 4 if self.mom is not None else 0))
         return tot
+
+
+class MultiDeviceFedOptServer:
+    """FedOptServer over G GPUs of ONE server process (the reference's
+    FedOptAggregator is one process: FedOptAggregator.py:81-130).
+
+    The model's keys are dealt to the devices whole (multidev.shard_plan, the
+    partition MultiDeviceBucket uses) and every device runs an ordinary
+    FedOptServer over its keys: its own client rows, global vector and
+    optimizer state, its own fused FedAvg + server-step launches.  Every
+    element's FedAvg chain and optimizer step are the one-device ones, so the
+    result is bit-exact with FedOptServer, and nothing is exchanged.  Same
+    interface as FedOptServer."""
+
+    def __init__(self, global_state: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],
+                 worker_num: int, server_optimizer: str = "sgd", server_lr: float = 1.0,
+                 server_momentum: float = 0.0, devices: Sequence = (), server_weight_decay: Optional[float] = None):
+        from .multidev import shard_plan
+
+        devices = [torch.device(d) for d in devices]
+        if not devices:
+            raise ValueError("MultiDeviceFedOptServer needs at least one device")
+        self.entries = [(k, tuple(t.shape), t.dtype) for k, t in global_state.items()]
+        plan = shard_plan(self.entries, len(devices))
+        self.devices = devices[:len(plan)]
+        self.servers: List[FedOptServer] = []
+        for sub, dev in zip(plan, self.devices):
+            keys = [k for k, _, _ in sub]
+            mine = set(keys)
+            self.servers.append(FedOptServer(OrderedDict((k, global_state[k]) for k in keys),
+                                             [k for k in param_names if k in mine], worker_num,
+                                             server_optimizer, server_lr, server_momentum, dev, server_weight_decay))
+        self.owner = {k: i for i, s in enumerate(self.servers) for k, _, _ in s.bucket.entries}
+        self.worker_num = worker_num
+        self.optimizer = self.servers[0].optimizer
+        self.param_names = list(param_names)
+        self.sample_num_dict = _SharedDict(self.servers, "sample_num_dict")
+        self.flag_client_model_uploaded_dict = {i: False for i in range(worker_num)}
+        self._views: Optional["OrderedDict[str, torch.Tensor]"] = None
+
+    def add_local_trained_result(self, index: int, model_params, sample_num) -> None:
+        """:68-72: every device takes its keys of the update; the host keys of
+        all devices are packed in one native gather, then the G H2Ds go out
+        back to back (MultiDeviceBucket.put's ingest)."""
+        from .bucket import gather_jobs
+
+        jobs = [(s, s.bucket.put_prepare(index, model_params, sample_num)) for s in self.servers]
+        gather_jobs([j for _, js in jobs for j in js])
+        for s, js in jobs:
+            s.bucket.put_issue(js)
+            s.sample_num_dict[index] = sample_num
+            s.flag_client_model_uploaded_dict[index] = True
+        dict.__setitem__(self.sample_num_dict, index, sample_num)
+        self.flag_client_model_uploaded_dict[index] = True
+
+    def check_whether_all_receive(self) -> bool:
+        for idx in range(self.worker_num):
+            if not self.flag_client_model_uploaded_dict[idx]:
+                return False
+        for idx in range(self.worker_num):
+            self.flag_client_model_uploaded_dict[idx] = False
+        for s in self.servers:
+            for idx in range(self.worker_num):
+                s.flag_client_model_uploaded_dict[idx] = False
+        return True
+
+    def aggregate(self, events=None) -> "OrderedDict[str, torch.Tensor]":
+        """Every device's launches are enqueued on its own current stream
+        (events, if given, around the first device's fp32 launches)."""
+        for i, s in enumerate(self.servers):
+            s.aggregate(events=events if i == 0 else None)
+        return self.get_global_model_params()
+
+    def get_global_model_params(self) -> "OrderedDict[str, torch.Tensor]":
+        if self._views is None:
+            parts = [s.get_global_model_params() for s in self.servers]
+            self._views = OrderedDict((k, parts[self.owner[k]][k]) for k, _, _ in self.entries)
+        return self._views
+
+    @property
+    def step_count(self) -> int:
+        return self.servers[0].step_count
+
+    def optimizer_state(self) -> Dict[str, object]:
+        out: Dict[str, object] = {"step": self.step_count}
+        for s in self.servers:
+            for name, v in s.optimizer_state().items():
+                if name != "step":
+                    out.setdefault(name, OrderedDict()).update(v)
+        for name, v in list(out.items()):  # the model's parameter order
+            if name != "step":
+                out[name] = OrderedDict((k, v[k]) for k in self.param_names if k in v)
+        return out
+
+    def load_optimizer_state(self, state: Dict[str, object]) -> None:
+        for s in self.servers:
+            mine = {k for k, _, _ in s.bucket.entries}
+            s.load_optimizer_state({name: (v if name == "step" else
+                                           OrderedDict((k, t) for k, t in v.items() if k in mine))
+                                    for name, v in state.items()})
+
+    def algorithmic_bytes(self) -> int:
+        return sum(s.algorithmic_bytes() for s in self.servers)
+
+
+class _SharedDict(dict):
+    """sample_num_dict of a MultiDeviceFedOptServer: a write goes to every
+    device's server too (the reference sets it per client before aggregate)."""
+
+    def __init__(self, servers, attr):
+        super().__init__()
+        self._targets = [getattr(s, attr) for s in servers]
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        for t in self._targets:
+            t[k] = v
+
+
+def make_fedopt_server(global_state: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str], worker_num: int,
+                       server_optimizer: str = "sgd", server_lr: float = 1.0, server_momentum: float = 0.0,
+                       device=None, args=None, server_weight_decay: Optional[float] = None):
+    """The FedOpt server for this round's shape: one device, or several GPUs
+    of this process when ``args.fedagg_devices`` lists them or the round does
+    not fit the default device's free HBM (multidev.devices_for_round, the
+    rule FedMLAggOperator.agg and the cross-silo mirror use)."""
+    from .multidev import devices_for_round
+
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    entries = [(k, tuple(t.shape), t.dtype) for k, t in global_state.items()]
+    # the server also holds the global vector and the optimizer state: up to
+    # three more model-sized fp32 vectors besides the K + 1 rows
+    devs = devices_for_round(args, entries, worker_num + 3, dev)
+    if len(devs) > 1:
+        return MultiDeviceFedOptServer(global_state, param_names, worker_num, server_optimizer, server_lr,
+                                       server_momentum, devs, server_weight_decay)
+    return FedOptServer(global_state, param_names, worker_num, server_optimizer, server_lr, server_momentum,
+                        devs[0], server_weight_decay)
