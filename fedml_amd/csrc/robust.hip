@@ -802,6 +802,7 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
   auto fold = [&]() {
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
+      asm volatile("s_nop 15" : "+v"(acc[j]));  // MFMA -> VALU wait states (see pairgram_split_kernel)
       acc64[j][0] += double(acc[j].x);
       acc64[j][1] += double(acc[j].y);
       acc64[j][2] += double(acc[j].z);
@@ -876,6 +877,270 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same centred Gram on the bf16 matrix cores (FEDAGG_GRAM_SPLIT, default).
+//
+// Every centred value is split EXACTLY into three bf16 parts, c = h + m + l
+// (h = bf16(c) rounded to nearest, m = bf16(c - h), l = c - h - m: each
+// remainder is exact in fp32 and the last one has at most 8 significant bits,
+// so it IS a bf16), and
+//   c_i c_j = h_i h_j + h_i m_j + m_i h_j + m_i m_j + h_i l_j + l_i h_j + e,
+//   |e| <= (|m_i l_j| + |l_i m_j| + |l_i l_j|) < 2^-25 |c_i| |c_j|,
+// below the fp32 rounding of the product the f32 MFMA makes.  bf16 x bf16
+// products are exact in fp32 and the MFMA accumulates in fp32, so each Gram
+// entry is a sum of exact products at fp32 accumulation, as on the f32 MFMA.
+// Six v_mfma_f32_16x16x32_bf16 (16 cycles each) cover 32 columns of a tile
+// where the f32 form needs eight 16x16x4 (32 cycles each): 96 against 256
+// cycles, so the 3.0 ms matrix floor at config 3 drops to 1.1 ms, under the
+// 1.64 ms of reading the rows once.
+//
+// LDS: the three planes of one stage, [plane][client][64 columns] bf16, rows
+// of 144 B (the 16 rows of a ds_read_b128 lane group fall on 16 distinct
+// 16-byte bank groups); one buffer per block (57 KB), two blocks per CU.  The
+// split is done once per element when a stage is written, never per tile.
+// Fragments (16x16x32, lane i = l & 15, q = l >> 4): A[row i][k = 8q + j] and
+// B[k = 8q + j][col i] are both 16 bytes of row (16 g + i) at columns
+// 32 ks + 8q .. + 7.  A wave's tiles are a contiguous run in row-major order,
+// so consecutive tiles share their A group: its fragments are read once per run.
+#ifndef FEDAGG_GRAM_SPLIT
+#define FEDAGG_GRAM_SPLIT 1
+#endif
+#ifndef FEDAGG_GRAM_SPLIT_FOLD
+#define FEDAGG_GRAM_SPLIT_FOLD 4
+#endif
+constexpr int kSplitRB = 144;                  // bytes per plane row: 64 bf16 + 16 B
+
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+// two floats -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// The split kernel's tile schedule: wave w takes the two rows of tiles w and
+// NB - 1 - w of the group triangle (NB - w and w + 1 tiles: NB + 1 in all, the
+// same for every wave at even NB; an odd NB's middle row goes alone).  Both
+// rows' A fragments are read once per k-step, the B fragments ping-pong by
+// tile, so tile j + 1's reads overlap tile j's six MFMAs, and every wave runs
+// ONE code path (per-wave compile-time schedules spilled).
+template <int PLANE>
+__device__ __forceinline__ void split_frag(const unsigned char* fp, int grp, int ks, bf16x8v (&F)[3]) {
+  const unsigned char* p = fp + grp * (16 * kSplitRB) + 64 * ks;
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) F[pl] = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(p + pl * PLANE));
+}
+
+__device__ __forceinline__ f32x4v split_mfma6(const bf16x8v (&A)[3], const bf16x8v (&B)[3], f32x4v x) {
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[1], x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[0], x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[1], x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[2], x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2], B[0], x, 0, 0, 0);
+  return x;
+}
+
+// NB = the groups of 16 clients of THIS K (1..8): every wave's tiles, their
+// rows and columns are compile-time constants, so the fragment ping-pong and
+// the A reloads (only where a wave's run of tiles changes row) are static
+template <int NB>
+__global__ __launch_bounds__(kGramBS, 2) void pairgram_split_kernel(const float* const* __restrict__ src, int K,
+                                                                    const int64_t* __restrict__ chunks,
+                                                                    int64_t n_chunks, int G,
+                                                                    double* __restrict__ partial) {
+  constexpr int ROWS = NB * 16;
+  constexpr int NT = NB * (NB + 1) / 2;
+  constexpr int TPW = NB + 1;  // tiles per wave, at most (two rows)
+  constexpr int LPW = ROWS / 16;
+  constexpr int PLANE = ROWS * kSplitRB;
+  __shared__ __attribute__((aligned(16))) unsigned char sP[3 * PLANE];
+  __shared__ float sSum[2][4][kStage];
+  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int i16 = lane & 15, q = lane >> 4;
+  const float* rowp[LPW];
+  bool rlive[LPW];
+#pragma unroll
+  for (int u = 0; u < LPW; ++u) {
+    const int cl = wave * (ROWS / 4) + 4 * u + q;
+    rlive[u] = cl < K;
+    rowp[u] = src[cl < K ? cl : 0];
+  }
+  double acc64[TPW][4];
+  f32x4v acc[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc64[j][r] = 0.0;
+  }
+  const float invK = 1.0f / float(K);
+  int64_t c = g;
+  int s0 = 0;
+  f32x4 v[LPW];
+  auto fetch = [&]() {
+    if (c >= n_chunks) return false;
+    const int len = int(chunks[2 * c + 1]);
+    const int64_t col0 = chunks[2 * c] + s0;
+    const int w = len - s0 < kStage ? len - s0 : kStage;
+    const int c4 = 4 * i16;
+    if (w == kStage) {
+#pragma unroll
+      for (int u = 0; u < LPW; ++u) v[u] = ld4<true>(rowp[u] + col0 + c4);
+    } else {
+#pragma unroll
+      for (int u = 0; u < LPW; ++u) {
+        const float* p = rowp[u] + col0;
+        const bool ok = rlive[u];
+        v[u].x = ok && c4 < w ? p[c4] : 0.f;
+        v[u].y = ok && c4 + 1 < w ? p[c4 + 1] : 0.f;
+        v[u].z = ok && c4 + 2 < w ? p[c4 + 2] : 0.f;
+        v[u].w = ok && c4 + 3 < w ? p[c4 + 3] : 0.f;
+      }
+    }
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
+  auto fetch_skip = [&]() {
+    if (c >= n_chunks) return false;
+    const int len = int(chunks[2 * c + 1]);
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
+  auto masked = [&](int u) {
+    const uint32_t m = rlive[u] ? 0xffffffffu : 0u;
+    return f32x4{__uint_as_float(__float_as_uint(v[u].x) & m), __uint_as_float(__float_as_uint(v[u].y) & m),
+                 __uint_as_float(__float_as_uint(v[u].z) & m), __uint_as_float(__float_as_uint(v[u].w) & m)};
+  };
+  auto stage_sums = [&](int sb) {
+    f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < LPW; ++u) cs += masked(u);
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      cs.x += __shfl_xor(cs.x, m, 64);
+      cs.y += __shfl_xor(cs.y, m, 64);
+      cs.z += __shfl_xor(cs.z, m, 64);
+      cs.w += __shfl_xor(cs.w, m, 64);
+    }
+    if (q == 0) *reinterpret_cast<f32x4*>(&sSum[sb][wave][4 * i16]) = cs;
+  };
+  // the rows minus the column means, split into the three bf16 planes
+  auto stage_split = [&](int sb) {
+    const f32x4 s0v = *reinterpret_cast<const f32x4*>(&sSum[sb][0][4 * i16]);
+    const f32x4 s1v = *reinterpret_cast<const f32x4*>(&sSum[sb][1][4 * i16]);
+    const f32x4 s2v = *reinterpret_cast<const f32x4*>(&sSum[sb][2][4 * i16]);
+    const f32x4 s3v = *reinterpret_cast<const f32x4*>(&sSum[sb][3][4 * i16]);
+    const f32x4 r = ((s0v + s1v) + (s2v + s3v)) * invK;
+#pragma unroll
+    for (int u = 0; u < LPW; ++u) {
+      const f32x4 cc = masked(u) - r;
+      const uint32_t h01 = pk_bf16(cc.x, cc.y), h23 = pk_bf16(cc.z, cc.w);
+      const float r0 = cc.x - bf16_lo(h01), r1 = cc.y - bf16_hi(h01);
+      const float r2 = cc.z - bf16_lo(h23), r3 = cc.w - bf16_hi(h23);
+      const uint32_t m01 = pk_bf16(r0, r1), m23 = pk_bf16(r2, r3);
+      const uint32_t l01 = pk_bf16(r0 - bf16_lo(m01), r1 - bf16_hi(m01));
+      const uint32_t l23 = pk_bf16(r2 - bf16_lo(m23), r3 - bf16_hi(m23));
+      unsigned char* d = sP + (wave * (ROWS / 4) + 4 * u + q) * kSplitRB + 8 * i16;
+      *reinterpret_cast<u32x2v*>(d) = u32x2v{h01, h23};
+      *reinterpret_cast<u32x2v*>(d + PLANE) = u32x2v{m01, m23};
+      *reinterpret_cast<u32x2v*>(d + 2 * PLANE) = u32x2v{l01, l23};
+    }
+  };
+  int unfolded = 0;
+  auto fold = [&]() {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      // 16 wait states between the last MFMA writing acc[j] and this VALU
+      // read: the compiler left none when the fold follows the MFMA chain
+      // directly (NB = 1: wrong sums on the box)
+      asm volatile("s_nop 15" : "+v"(acc[j]));
+      acc64[j][0] += double(acc[j].x);
+      acc64[j][1] += double(acc[j].y);
+      acc64[j][2] += double(acc[j].z);
+      acc64[j][3] += double(acc[j].w);
+      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+    unfolded = 0;
+  };
+  // this wave's rows of tiles: r1 = wave (n1 tiles), r2 = NB - 1 - wave (n2)
+  const int r1 = wave, r2 = NB - 1 - wave;
+  const int n1 = wave < (NB + 1) / 2 ? NB - wave : 0;
+  const int n2 = r2 > r1 ? wave + 1 : 0;
+  const int nmine = n1 + n2;
+  const unsigned char* fp = sP + i16 * kSplitRB + 16 * q;
+  auto compute = [&]() {
+    if (nmine > 0) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8v A1[3], A2[3], B[2][3];
+        split_frag<PLANE>(fp, r1, ks, A1);
+        split_frag<PLANE>(fp, r1, ks, B[0]);  // tile 0 = (r1, r1)
+        if (n2) split_frag<PLANE>(fp, r2, ks, A2);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          if (j < nmine) {
+            if (j + 1 < nmine)  // tile j + 1's column group
+              split_frag<PLANE>(fp, j + 1 < n1 ? r1 + j + 1 : r2 + (j + 1 - n1), ks, B[(j + 1) & 1]);
+            acc[j] = j < n1 ? split_mfma6(A1, B[j & 1], acc[j]) : split_mfma6(A2, B[j & 1], acc[j]);
+          }
+        }
+      }
+    }
+    if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
+  };
+  // one plane buffer: compute(s), then stage s + 1's sums (its loads had the
+  // whole compute to land), barrier (every wave done reading the planes),
+  // split-write stage s + 1, issue stage s + 2's loads, barrier
+  bool have = fetch();
+  if (have) {
+    stage_sums(0);
+    lds_barrier();
+    stage_split(0);
+    have = fetch();
+    lds_barrier();
+    for (int sb = 1;; sb ^= 1) {
+      if constexpr (FEDAGG_GRAM_DIAG != 1) compute();
+      if (!have) break;
+      if constexpr (FEDAGG_GRAM_DIAG == 2) {  // same stage count, no loads, sums or barriers
+        have = fetch_skip();
+        continue;
+      }
+      stage_sums(sb);
+      lds_barrier();
+      stage_split(sb);
+      have = fetch();
+      lds_barrier();
+    }
+  }
+  if (unfolded) fold();
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    if (j < nmine) {
+      // row-major index of tile (a, b) in the triangle: the workspace layout
+      const int a = j < n1 ? r1 : r2, b = j < n1 ? r1 + j : r2 + (j - n1);
+      const int tt = a * NB - a * (a - 1) / 2 + (b - a);
+      double* out = partial + (int64_t(g) * NT + tt) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(4 * q + r) * 16 + i16] = acc64[j][r];
+    }
+  }
+}
+
 // M (K x K, fp64, both triangles) = the tiles' partials summed over the chunk
 // groups in four fixed-order quarters (as tri_finish_kernel)
 __global__ __launch_bounds__(256) void gram_sum_kernel(const double* __restrict__ partial, int G, int K,
@@ -911,7 +1176,10 @@ __global__ __launch_bounds__(256) void gram_dist_kernel(const double* __restrict
   const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (e >= int64_t(K) * K) return;
   const int i = int(e / K), j = int(e % K);
-  const double d = (M[int64_t(i) * K + i] + M[int64_t(j) * K + j]) - 2.0 * M[e];
+  // M_ij + M_ji: a diagonal tile of the split kernel computes the two in a
+  // different MFMA order (h_i m_j before m_i h_j), so they may differ in the
+  // last bits; the sum keeps D exactly symmetric (= 2 M_ij when M is)
+  const double d = (M[int64_t(i) * K + i] + M[int64_t(j) * K + j]) - (M[e] + M[int64_t(j) * K + i]);
   D[e] = i == j ? 0.0 : (d > 0.0 ? d : 0.0);
 }
 
@@ -1101,7 +1369,21 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: workspace too small (fedagg_robust_work_len)");
   const int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, work_len - mat, per);
   double* M = d_work + int64_t(G) * per;
-  if (K <= 64)
+  if (FEDAGG_GRAM_SPLIT) {
+    auto kern = pairgram_split_kernel<8>;
+    switch (gram_groups(K)) {
+      case 1: kern = pairgram_split_kernel<1>; break;
+      case 2: kern = pairgram_split_kernel<2>; break;
+      case 3: kern = pairgram_split_kernel<3>; break;
+      case 4: kern = pairgram_split_kernel<4>; break;
+      case 5: kern = pairgram_split_kernel<5>; break;
+      case 6: kern = pairgram_split_kernel<6>; break;
+      case 7: kern = pairgram_split_kernel<7>; break;
+      default: break;
+    }
+    hipLaunchKernelGGL(kern, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G, d_work);
+  }
+  else if (K <= 64)
     hipLaunchKernelGGL(pairgram_kernel<4>, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G,
                        d_work);
   else

@@ -84,10 +84,27 @@ def bench(rounds: int, out_path: str) -> None:
             assert rc == 0, tag
             if r:
                 times[tag].append(ev0.elapsed_time(ev1))
+    # the exact-difference kernel's D, and each variant's error against it in
+    # the units test_gpu_dist_defenses.py bounds (|c_i|^2 + |c_j|^2, the
+    # double-centred norms)
+    exact = torch.empty((K, K), dtype=torch.float64, device=dev)
+    wex = dfn._work(nat.WORK_PAIRDIST2, K, n_chunks, dev)
+    assert nat.lib().fedagg_pairdist2_f32(ctypes.c_void_p(g.d_ptrs.data_ptr()), K, ctypes.c_void_p(chunks.data_ptr()),
+                                          ctypes.c_int64(n_chunks), ctypes.c_void_p(exact.data_ptr()),
+                                          ctypes.c_void_p(wex.data_ptr()), ctypes.c_int64(wex.numel()),
+                                          ctypes.c_void_p(st)) == 0
+    torch.cuda.synchronize()
+    cn = exact.mean(1) - exact.sum() / (2 * K * K)
+    scale = cn[:, None] + cn[None, :]
+    off = ~torch.eye(K, dtype=torch.bool, device=dev)
     res = {"K": K, "n_chunks": int(n_chunks), "variants": VARIANTS}
     for tag in tags:
+        err = ((outs[tag] - exact).abs() / scale)[off]
         res[tag] = {"ms": round(statistics.median(times[tag]), 4),
-                    "identical_to_shipped": bool(torch.equal(outs[tag], outs["shipped"]))}
+                    "identical_to_shipped": bool(torch.equal(outs[tag], outs["shipped"])),
+                    "max_err_vs_exact": float(err.max()),
+                    "krum_order_same_as_exact": bool(torch.equal(outs[tag].sort(1).values[:, :64].sum(1).argsort(),
+                                                                 exact.sort(1).values[:, :64].sum(1).argsort()))}
         print(tag, res[tag], flush=True)
     json.dump(res, open(out_path, "w"), indent=1)
 
