@@ -562,11 +562,13 @@ def main():
                 nat.stream_handle())
         n_weight = sum(n for k, n in zip(gd.keys, gd.numels) if dfn.is_weight_param(k))
         gram = a.op == "krum" and (a.pair_distance == "gram" or (a.pair_distance == "auto" and K <= 128))
-        # krum: 3 flops (sub, mul, add) per client pair and weight element;
+        # krum, exact kernel: 3 flops (sub, mul, add) per client pair and weight element (VALU-bound);
+        # krum, centred Gram on the bf16 matrix cores: the K weight rows read once (HBM-bound: its
+        # six bf16 MFMAs per 32 columns need ~2/3 of the time the rows take to stream);
         # dist2: K rows + the reference row read once; clip: K rows in + K out + the reference row
-        # krum, gram: 2 flops (one FMA on the matrix cores) per client pair and weight element
-        dom_bytes = {"krum": (2 if a.op == "krum" and gram else 3) * K * (K - 1) // 2 * n_weight,
+        dom_bytes = {"krum": K * n_weight * 4 if a.op == "krum" and gram else 3 * K * (K - 1) // 2 * n_weight,
                      "dist2": (K + 1) * n_weight * 4, "clip": (2 * K + 1) * gd.length * 4}[a.op]
+        krum_pair_flops = 2 * K * (K - 1) // 2 * n_weight  # one multiply-add per client pair and element
 
         def step(ev=None, cev=None):
             if ev is not None:
@@ -619,7 +621,7 @@ def main():
 
     timed_comm = mode == "client" and world > 1 and a.backend == "nccl"
     elapsed, kern_ms, comm_ms = run_timed(step, n_launch, a.steps, a.warmup, world, mode == "client", timed_comm)
-    achieved = dom_bytes / (kern_ms / 1e3) / 1e9  # GB/s (GFLOP/s for --op krum)
+    achieved = dom_bytes / (kern_ms / 1e3) / 1e9  # GB/s (GFLOP/s for the exact-difference krum kernel)
     hbm_all = dom_bytes / (elapsed / a.steps) / 1e9  # this rank's algorithmic bytes over the step time
     if world > 1:
         achieved, hbm_all, comm_ms = reduce_rates(achieved, hbm_all, comm_ms, world, dev)
@@ -668,15 +670,16 @@ def main():
             "parallelism": parallelism,
         },
         "roofline": {
-            "bound": ("mfma" if gram_op else "valu") if a.op == "krum" else "hbm",
-            "achieved": round(achieved / 1e3, 2) if a.op == "krum" else round(achieved, 1),
-            "peak": VALU_PEAK_TFLOPS if a.op == "krum" else HBM_PEAK_GBPS,
-            "unit": "TFLOP/s" if a.op == "krum" else "GB/s",
-            "frac": round(achieved / 1e3 / VALU_PEAK_TFLOPS if a.op == "krum" else achieved / HBM_PEAK_GBPS, 4),
+            "bound": "valu" if a.op == "krum" and not gram_op else "hbm",
+            "achieved": round(achieved / 1e3, 2) if a.op == "krum" and not gram_op else round(achieved, 1),
+            "peak": VALU_PEAK_TFLOPS if a.op == "krum" and not gram_op else HBM_PEAK_GBPS,
+            "unit": "TFLOP/s" if a.op == "krum" and not gram_op else "GB/s",
+            "frac": round(achieved / 1e3 / VALU_PEAK_TFLOPS if a.op == "krum" and not gram_op
+                          else achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>",
-                        "krum": ((f"pairgram_kernel<{4 if K <= 64 else 8}> + gram_sum_kernel + gram_dist_kernel "
-                                  "(fp32 MFMA 16x16x4, centred Gram)") if a.pair_distance == "gram" or
+                        "krum": ((f"pairgram_split_kernel<{(K + 15) // 16}> + gram_sum_kernel + gram_dist_kernel "
+                                  "(centred Gram, exact 3-way bf16 split, 16x16x32 bf16 MFMA)") if a.pair_distance == "gram" or
                                  (a.pair_distance == "auto" and K <= 128) else
                                  ("pairtri_kernel<16> + tri_finish_kernel" if K <= 64 else
                                   "pairtri_kernel<32> + tri_finish_kernel" if K <= 128 else
@@ -694,6 +697,11 @@ def main():
                        f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step"),
             "alg_bytes_per_step": dom_bytes,
             "kernel_ms_per_step": round(kern_ms, 4),
+            **({"useful_tflops": round(krum_pair_flops / (kern_ms / 1e3) / 1e12, 2),
+                # NT 16x16 tiles x 12 MFMAs of 16 cycles per 64 columns, over 1024 SIMDs at 2.4 GHz
+                "bf16_mfma_floor_ms": round(((K + 15) // 16) * ((K + 15) // 16 + 1) // 2 * 12 * 16 * (n_weight / 64)
+                                            / (1024 * 2.4e9) * 1e3, 3)}
+               if gram_op else {}),
         },
         "cpu_baseline": None,
     }

@@ -27,6 +27,8 @@
 // are deterministic run to run.
 
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #include <string>
@@ -885,8 +887,9 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 // remainder is exact in fp32 and the last one has at most 8 significant bits,
 // so it IS a bf16), and
 //   c_i c_j = h_i h_j + h_i m_j + m_i h_j + m_i m_j + h_i l_j + l_i h_j + e,
-//   |e| <= (|m_i l_j| + |l_i m_j| + |l_i l_j|) < 2^-25 |c_i| |c_j|,
-// below the fp32 rounding of the product the f32 MFMA makes.  bf16 x bf16
+//   |e| <= |m_i l_j| + |l_i m_j| + |l_i l_j| <= 2^-23 |c_i| |c_j|
+// (|m| <= 2^-8 |c|, |l| <= 2^-8 |m|; tests/test_gram_split.py), the order of
+// the fp32 rounding of each product on the f32 MFMA (2^-24).  bf16 x bf16
 // products are exact in fp32 and the MFMA accumulates in fp32, so each Gram
 // entry is a sum of exact products at fp32 accumulation, as on the f32 MFMA.
 // Six v_mfma_f32_16x16x32_bf16 (16 cycles each) cover 32 columns of a tile
@@ -1141,6 +1144,221 @@ __global__ __launch_bounds__(kGramBS, 2) void pairgram_split_kernel(const float*
   }
 }
 
+// FEDAGG_GRAM_SPLIT == 2: the same split Gram with 8 waves per block and ONE
+// block per CU, so the planes can be double-buffered (2 x 55 KB) and a stage
+// needs one barrier, and each lane's raw rows are prefetched two stages
+// ahead (two register sets; 16 rows per wave).  Iteration k: split stage
+// k + 1 into the free plane buffer (its column sums were published before
+// the last barrier), issue stage k + 3's loads into the freed registers,
+// compute stage k, publish stage k + 2's column sums, barrier.  A stage's
+// loads have two iterations to land.  Tiles: the row pair p (rows p and
+// NB - 1 - p, as the 4-wave kernel) is shared by waves p and p + 4, which sit
+// on the same SIMD: wave p takes its first ceil(n / 2) tiles, wave p + 4 the
+// rest, so every SIMD runs one pair's MFMAs per stage.
+constexpr int kSplit8BS = 512;
+
+template <int NB>
+__global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const float* const* __restrict__ src, int K,
+                                                                     const int64_t* __restrict__ chunks,
+                                                                     int64_t n_chunks, int G,
+                                                                     double* __restrict__ partial) {
+  constexpr int ROWS = NB * 16;
+  constexpr int NT = NB * (NB + 1) / 2;
+  constexpr int TPW = (NB + 2) / 2;  // ceil((NB + 1) / 2) tiles per wave, at most
+  constexpr int RPW = ROWS / 8;      // staged rows per wave
+  constexpr int LPW = (RPW + 3) / 4; // 16-byte loads per lane and stage (4 rows per wave-load)
+  constexpr int PLANE = ROWS * kSplitRB;
+  __shared__ __attribute__((aligned(16))) unsigned char sP[2][3 * PLANE];
+  __shared__ float sSum[2][8][kStage];
+  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int i16 = lane & 15, q = lane >> 4;
+  const float* rowp[LPW];
+  bool rlive[LPW];
+#pragma unroll
+  for (int u = 0; u < LPW; ++u) {
+    const int lr = 4 * u + q;  // row within the wave's RPW (NB = 1, 2: RPW < 4, lanes past it idle)
+    const int cl = wave * RPW + lr;
+    rlive[u] = lr < RPW && cl < K;
+    rowp[u] = src[rlive[u] ? cl : 0];
+  }
+  // the row pair of this wave and its share of the pair's tiles
+  const int p = wave & 3;
+  const int pr1 = p, pr2 = NB - 1 - p;
+  const int len1 = p < (NB + 1) / 2 ? NB - p : 0;  // row pr1's tiles (b = pr1 .. NB - 1)
+  const int len2 = len1 && pr2 > pr1 ? p + 1 : 0;  // row pr2's tiles (b = pr2 .. NB - 1)
+  const int half = (len1 + len2 + 1) / 2;
+  const int first = wave < 4 ? 0 : half;                    // this wave's tiles: pair tiles first .. first + nmine - 1
+  const int nmine = wave < 4 ? half : len1 + len2 - half;
+  // as (row, first column group, count) runs: at most two
+  const int r1 = first < len1 ? pr1 : pr2;
+  const int b1 = first < len1 ? pr1 + first : pr2 + (first - len1);
+  const int n1 = first < len1 ? (len1 - first < nmine ? len1 - first : nmine) : nmine;
+  const int r2 = pr2, b2 = pr2 + (first + n1 - len1 > 0 ? first + n1 - len1 : 0);
+  const int n2 = nmine - n1;
+  double acc64[TPW][4];
+  f32x4v acc[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc64[j][r] = 0.0;
+  }
+  const float invK = 1.0f / float(K);
+  int64_t c = g;
+  int s0 = 0;
+  f32x4 v[2][LPW];
+  auto fetch = [&](f32x4 (&vv)[LPW]) {
+    if (c >= n_chunks) return false;
+    const int len = int(chunks[2 * c + 1]);
+    const int64_t col0 = chunks[2 * c] + s0;
+    const int w = len - s0 < kStage ? len - s0 : kStage;
+    const int c4 = 4 * i16;
+    if (w == kStage) {
+#pragma unroll
+      for (int u = 0; u < LPW; ++u) vv[u] = ld4<true>(rowp[u] + col0 + c4);
+    } else {
+#pragma unroll
+      for (int u = 0; u < LPW; ++u) {
+        const float* pp = rowp[u] + col0;
+        const bool ok = rlive[u];
+        vv[u].x = ok && c4 < w ? pp[c4] : 0.f;
+        vv[u].y = ok && c4 + 1 < w ? pp[c4 + 1] : 0.f;
+        vv[u].z = ok && c4 + 2 < w ? pp[c4 + 2] : 0.f;
+        vv[u].w = ok && c4 + 3 < w ? pp[c4 + 3] : 0.f;
+      }
+    }
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
+  auto masked = [&](const f32x4& x, int u) {
+    const uint32_t m = rlive[u] ? 0xffffffffu : 0u;
+    return f32x4{__uint_as_float(__float_as_uint(x.x) & m), __uint_as_float(__float_as_uint(x.y) & m),
+                 __uint_as_float(__float_as_uint(x.z) & m), __uint_as_float(__float_as_uint(x.w) & m)};
+  };
+  auto stage_sums = [&](const f32x4 (&vv)[LPW], int sb) {
+    f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < LPW; ++u) cs += masked(vv[u], u);
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      cs.x += __shfl_xor(cs.x, m, 64);
+      cs.y += __shfl_xor(cs.y, m, 64);
+      cs.z += __shfl_xor(cs.z, m, 64);
+      cs.w += __shfl_xor(cs.w, m, 64);
+    }
+    if (q == 0) *reinterpret_cast<f32x4*>(&sSum[sb][wave][4 * i16]) = cs;
+  };
+  auto stage_split = [&](const f32x4 (&vv)[LPW], int sb, unsigned char* P) {
+    f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+      f32x4 s8[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s8[w] = *reinterpret_cast<const f32x4*>(&sSum[sb][w][4 * i16]);
+      r = (((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]))) * invK;
+    }
+#pragma unroll
+    for (int u = 0; u < LPW; ++u) {
+      if (4 * u + q < RPW) {
+        const f32x4 cc = masked(vv[u], u) - r;
+        const uint32_t h01 = pk_bf16(cc.x, cc.y), h23 = pk_bf16(cc.z, cc.w);
+        const float e0 = cc.x - bf16_lo(h01), e1 = cc.y - bf16_hi(h01);
+        const float e2 = cc.z - bf16_lo(h23), e3 = cc.w - bf16_hi(h23);
+        const uint32_t m01 = pk_bf16(e0, e1), m23 = pk_bf16(e2, e3);
+        const uint32_t l01 = pk_bf16(e0 - bf16_lo(m01), e1 - bf16_hi(m01));
+        const uint32_t l23 = pk_bf16(e2 - bf16_lo(m23), e3 - bf16_hi(m23));
+        unsigned char* d = P + (wave * RPW + 4 * u + q) * kSplitRB + 8 * i16;
+        *reinterpret_cast<u32x2v*>(d) = u32x2v{h01, h23};
+        *reinterpret_cast<u32x2v*>(d + PLANE) = u32x2v{m01, m23};
+        *reinterpret_cast<u32x2v*>(d + 2 * PLANE) = u32x2v{l01, l23};
+      }
+    }
+  };
+  int unfolded = 0;
+  auto fold = [&]() {
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      asm volatile("s_nop 15" : "+v"(acc[j]));  // MFMA -> VALU wait states (see pairgram_split_kernel)
+      acc64[j][0] += double(acc[j].x);
+      acc64[j][1] += double(acc[j].y);
+      acc64[j][2] += double(acc[j].z);
+      acc64[j][3] += double(acc[j].w);
+      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+    unfolded = 0;
+  };
+  const int fo = i16 * kSplitRB + 16 * q;
+  auto compute = [&](const unsigned char* P) {
+    if (nmine > 0) {
+      const unsigned char* fp = P + fo;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8v A1[3], A2[3], B[2][3];
+        split_frag<PLANE>(fp, r1, ks, A1);
+        split_frag<PLANE>(fp, b1, ks, B[0]);
+        if (n2) split_frag<PLANE>(fp, r2, ks, A2);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          if (j < nmine) {
+            if (j + 1 < nmine)
+              split_frag<PLANE>(fp, j + 1 < n1 ? b1 + j + 1 : b2 + (j + 1 - n1), ks, B[(j + 1) & 1]);
+            acc[j] = j < n1 ? split_mfma6(A1, B[j & 1], acc[j]) : split_mfma6(A2, B[j & 1], acc[j]);
+          }
+        }
+      }
+    }
+    if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
+  };
+  // prologue: stages 0 and 1 loaded, stage 0 split, stage 1's sums published
+  bool h0 = fetch(v[0]);
+  bool h1 = h0 && fetch(v[1]);
+  if (h0) {
+    stage_sums(v[0], 0);
+    lds_barrier();
+    stage_split(v[0], 0, sP[0]);
+    bool h2 = h1 && fetch(v[0]);  // stage 2
+    if (h1) stage_sums(v[1], 1);
+    lds_barrier();
+    // iteration k (two at a time, so the register sets are static)
+    auto iter = [&](auto cur_tag, bool& hn, bool& hnn) {
+      constexpr int C = decltype(cur_tag)::value;  // k % 2
+      // hn: stage k + 1 exists (in v[C ^ 1], sums in sSum[C ^ 1]); hnn: stage k + 2 (in v[C])
+      bool hnnn = false;
+      if (hn) {
+        stage_split(v[C ^ 1], C ^ 1, sP[C ^ 1]);
+        hnnn = hnn && fetch(v[C ^ 1]);  // stage k + 3
+      }
+      compute(sP[C]);
+      if (hnn) stage_sums(v[C], C);
+      lds_barrier();
+      const bool more = hn;
+      hn = hnn;
+      hnn = hnnn;
+      return more;
+    };
+    bool hn = h1, hnn = h2;
+    while (true) {
+      if (!iter(std::integral_constant<int, 0>{}, hn, hnn)) break;
+      if (!iter(std::integral_constant<int, 1>{}, hn, hnn)) break;
+    }
+  }
+  if (unfolded) fold();
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    if (j < nmine) {
+      const int a = j < n1 ? r1 : r2, b = j < n1 ? b1 + j : b2 + (j - n1);
+      const int tt = a * NB - a * (a - 1) / 2 + (b - a);
+      double* out = partial + (int64_t(g) * NT + tt) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(4 * q + r) * 16 + i16] = acc64[j][r];
+    }
+  }
+}
+
 // M (K x K, fp64, both triangles) = the tiles' partials summed over the chunk
 // groups in four fixed-order quarters (as tri_finish_kernel)
 __global__ __launch_bounds__(256) void gram_sum_kernel(const double* __restrict__ partial, int G, int K,
@@ -1367,9 +1585,24 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
   const int64_t mat = int64_t(K) * K;
   if (work_len < per + mat)
     return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: workspace too small (fedagg_robust_work_len)");
-  const int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, work_len - mat, per);
+  int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, work_len - mat, per);
   double* M = d_work + int64_t(G) * per;
-  if (FEDAGG_GRAM_SPLIT) {
+  if (FEDAGG_GRAM_SPLIT == 2) {
+    auto kern = pairgram_split8_kernel<8>;
+    switch (gram_groups(K)) {
+      case 1: kern = pairgram_split8_kernel<1>; break;
+      case 2: kern = pairgram_split8_kernel<2>; break;
+      case 3: kern = pairgram_split8_kernel<3>; break;
+      case 4: kern = pairgram_split8_kernel<4>; break;
+      case 5: kern = pairgram_split8_kernel<5>; break;
+      case 6: kern = pairgram_split8_kernel<6>; break;
+      case 7: kern = pairgram_split8_kernel<7>; break;
+      default: break;
+    }
+    const int G1 = G < 256 ? G : 256;  // one block per CU
+    hipLaunchKernelGGL(kern, dim3(unsigned(G1)), dim3(kSplit8BS), 0, st, d_src, K, d_chunks, n_chunks, G1, d_work);
+    G = G1;
+  } else if (FEDAGG_GRAM_SPLIT) {
     auto kern = pairgram_split_kernel<8>;
     switch (gram_groups(K)) {
       case 1: kern = pairgram_split_kernel<1>; break;
