@@ -726,10 +726,10 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
       for (int u = 0; u < LPW; ++u) {
         const float* p = rowp[u] + col0;
         const bool ok = rlive[u];
-        v[u].x = ok && c4 < w_next ? p[c4] : 0.f;
-        v[u].y = ok && c4 + 1 < w_next ? p[c4 + 1] : 0.f;
-        v[u].z = ok && c4 + 2 < w_next ? p[c4 + 2] : 0.f;
-        v[u].w = ok && c4 + 3 < w_next ? p[c4 + 3] : 0.f;
+        v[u].x = ok && c4 < w_next ? gptr(p)[c4] : 0.f;
+        v[u].y = ok && c4 + 1 < w_next ? gptr(p)[c4 + 1] : 0.f;
+        v[u].z = ok && c4 + 2 < w_next ? gptr(p)[c4 + 2] : 0.f;
+        v[u].w = ok && c4 + 3 < w_next ? gptr(p)[c4 + 3] : 0.f;
       }
     }
     s0 += kStage;
@@ -911,6 +911,10 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 #ifndef FEDAGG_GRAM_SPLIT_FOLD
 #define FEDAGG_GRAM_SPLIT_FOLD 4
 #endif
+// producer waves' stages of loads in flight (FEDAGG_GRAM_SPLIT == 3): 2, 4 or 6
+#ifndef FEDAGG_GRAM_WS_PD
+#define FEDAGG_GRAM_WS_PD 4
+#endif
 constexpr int kSplitRB = 144;                  // bytes per plane row: 64 bf16 + 16 B
 
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
@@ -1001,10 +1005,10 @@ __global__ __launch_bounds__(kGramBS, 2) void pairgram_split_kernel(const float*
       for (int u = 0; u < LPW; ++u) {
         const float* p = rowp[u] + col0;
         const bool ok = rlive[u];
-        v[u].x = ok && c4 < w ? p[c4] : 0.f;
-        v[u].y = ok && c4 + 1 < w ? p[c4 + 1] : 0.f;
-        v[u].z = ok && c4 + 2 < w ? p[c4 + 2] : 0.f;
-        v[u].w = ok && c4 + 3 < w ? p[c4 + 3] : 0.f;
+        v[u].x = ok && c4 < w ? gptr(p)[c4] : 0.f;
+        v[u].y = ok && c4 + 1 < w ? gptr(p)[c4 + 1] : 0.f;
+        v[u].z = ok && c4 + 2 < w ? gptr(p)[c4 + 2] : 0.f;
+        v[u].w = ok && c4 + 3 < w ? gptr(p)[c4 + 3] : 0.f;
       }
     }
     s0 += kStage;
@@ -1144,6 +1148,7 @@ __global__ __launch_bounds__(kGramBS, 2) void pairgram_split_kernel(const float*
   }
 }
 
+#if FEDAGG_GRAM_SPLIT >= 2  // experimental variants, not built by default
 // FEDAGG_GRAM_SPLIT == 2: the same split Gram with 8 waves per block and ONE
 // block per CU, so the planes can be double-buffered (2 x 55 KB) and a stage
 // needs one barrier, and each lane's raw rows are prefetched two stages
@@ -1222,12 +1227,22 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
       for (int u = 0; u < LPW; ++u) {
         const float* pp = rowp[u] + col0;
         const bool ok = rlive[u];
-        vv[u].x = ok && c4 < w ? pp[c4] : 0.f;
-        vv[u].y = ok && c4 + 1 < w ? pp[c4 + 1] : 0.f;
-        vv[u].z = ok && c4 + 2 < w ? pp[c4 + 2] : 0.f;
-        vv[u].w = ok && c4 + 3 < w ? pp[c4 + 3] : 0.f;
+        vv[u].x = ok && c4 < w ? gptr(pp)[c4] : 0.f;
+        vv[u].y = ok && c4 + 1 < w ? gptr(pp)[c4 + 1] : 0.f;
+        vv[u].z = ok && c4 + 2 < w ? gptr(pp)[c4 + 2] : 0.f;
+        vv[u].w = ok && c4 + 3 < w ? gptr(pp)[c4 + 3] : 0.f;
       }
     }
+    s0 += kStage;
+    if (s0 >= len) {
+      s0 = 0;
+      c += G;
+    }
+    return true;
+  };
+  auto fetch_skip = [&]() {
+    if (c >= n_chunks) return false;
+    const int len = int(chunks[2 * c + 1]);
     s0 += kStage;
     if (s0 >= len) {
       s0 = 0;
@@ -1293,6 +1308,10 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
   };
   const int fo = i16 * kSplitRB + 16 * q;
   auto compute = [&](const unsigned char* P) {
+    if constexpr (FEDAGG_GRAM_DIAG == 1) {  // staging only: one LDS read keeps the planes live
+      acc[0].x += *reinterpret_cast<const float*>(P + fo);
+      return;
+    }
     if (nmine > 0) {
       const unsigned char* fp = P + fo;
 #pragma unroll
@@ -1328,12 +1347,13 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
       constexpr int C = decltype(cur_tag)::value;  // k % 2
       // hn: stage k + 1 exists (in v[C ^ 1], sums in sSum[C ^ 1]); hnn: stage k + 2 (in v[C])
       bool hnnn = false;
-      if (hn) {
+      if (hn && FEDAGG_GRAM_DIAG != 2) {
         stage_split(v[C ^ 1], C ^ 1, sP[C ^ 1]);
         hnnn = hnn && fetch(v[C ^ 1]);  // stage k + 3
       }
+      if (FEDAGG_GRAM_DIAG == 2) hnnn = hnn && fetch_skip();  // compute only: same stage count
       compute(sP[C]);
-      if (hnn) stage_sums(v[C], C);
+      if (hnn && FEDAGG_GRAM_DIAG != 2) stage_sums(v[C], C);
       lds_barrier();
       const bool more = hn;
       hn = hnn;
@@ -1358,6 +1378,281 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     }
   }
 }
+
+// Consumer wave W's tiles, unrolled at compile time (no branches between
+// tiles): tile J of its row pair, B fragments ping-ponged by J, tile J + 1's
+// read issued before tile J's six MFMAs.  Rows W (n1 tiles) and NB - 1 - W
+// (n2 tiles), as pairgram_split_kernel's run-time schedule.
+template <int NB, int W>
+struct WsRows {
+  static constexpr int n1 = W < (NB + 1) / 2 ? NB - W : 0;
+  static constexpr int n2 = (NB - 1 - W > W) && n1 ? W + 1 : 0;
+  static constexpr int nm = n1 + n2;
+  static constexpr int bgrp(int j) { return j < n1 ? W + j : (NB - 1 - W) + (j - n1); }
+};
+
+template <int NB, int PLANE, int W, int KS, int BG, int TPW>
+__device__ __forceinline__ void ws_tiles(const unsigned char* fp, f32x4v (&acc)[TPW], const bf16x8v (&A1)[3],
+                                         const bf16x8v (&A2)[3], bf16x8v (&B)[2][3]) {
+  // column group BG: tile (W, BG), and (NB - 1 - W, BG) when BG is in that
+  // row too -- both from ONE read of BG's fragments
+  using R = WsRows<NB, W>;
+  constexpr int r2 = NB - 1 - W;
+  if constexpr (BG < NB && R::n1 > 0) {
+    if constexpr (BG + 1 < NB) split_frag<PLANE>(fp, BG + 1, KS, B[(BG + 1) & 1]);
+    acc[BG - W] = split_mfma6(A1, B[BG & 1], acc[BG - W]);
+    if constexpr (R::n2 > 0 && BG >= r2) acc[R::n1 + (BG - r2)] = split_mfma6(A2, B[BG & 1], acc[R::n1 + (BG - r2)]);
+    ws_tiles<NB, PLANE, W, KS, BG + 1, TPW>(fp, acc, A1, A2, B);
+  }
+}
+
+template <int NB, int PLANE, int W, int TPW>
+__device__ __forceinline__ void ws_compute(const unsigned char* fp, f32x4v (&acc)[TPW]) {
+  using R = WsRows<NB, W>;
+  if constexpr (R::nm > 0) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8v A1[3], A2[3], B[2][3];
+      split_frag<PLANE>(fp, W, ks, A1);
+      split_frag<PLANE>(fp, W, ks, B[W & 1]);  // the first column group is the row's own
+      if constexpr (R::n2 > 0) split_frag<PLANE>(fp, NB - 1 - W, ks, A2);
+      if (ks == 0)
+        ws_tiles<NB, PLANE, W, 0, W, TPW>(fp, acc, A1, A2, B);
+      else
+        ws_tiles<NB, PLANE, W, 1, W, TPW>(fp, acc, A1, A2, B);
+    }
+  }
+}
+
+// FEDAGG_GRAM_SPLIT == 3: producer / consumer waves.  One block of 8 waves
+// per CU; waves 0-3 (one per SIMD) only run MFMAs, waves 4-7 (one per SIMD)
+// only load, centre and split, so every SIMD has its matrix work and its
+// VALU work in two different waves that the scheduler interleaves (in the
+// other variants both phases sit in the same waves between barriers and do
+// not overlap).  A producer owns 16 of a stage's 64 columns for ALL rows, so
+// its column sums stay inside the wave (no exchange, no extra barrier), and
+// keeps two stages of loads in flight in registers.  The planes are double-
+// buffered: at barrier k the producers have written stage k + 1 and the
+// consumers have finished stage k, so one barrier per stage.  Consumers use
+// the row-pair tile schedule of pairgram_split_kernel.
+template <int NB>
+__global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split_ws_kernel(const float* const* __restrict__ src, int K,
+                                                                       const int64_t* __restrict__ chunks,
+                                                                       int64_t n_chunks, int G,
+                                                                       double* __restrict__ partial) {
+  constexpr int ROWS = NB * 16;
+  constexpr int NT = NB * (NB + 1) / 2;
+  constexpr int TPW = NB + 1;
+  constexpr int PLANE = ROWS * kSplitRB;
+  __shared__ __attribute__((aligned(16))) unsigned char sP[2][3 * PLANE];
+  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  // this block's stage count (every wave walks the chunk table: wave-uniform)
+  int S = 0;
+  for (int64_t cc = g; cc < n_chunks; cc += G) S += int((chunks[2 * cc + 1] + kStage - 1) / kStage);
+  constexpr int PD = FEDAGG_GRAM_WS_PD;  // stages of loads in flight per producer
+  const int Spad = (S + PD - 1) / PD * PD;  // barriers: one per (padded) stage
+  if (wave >= 4) {
+    // ---- producer: columns 16 pw .. 16 pw + 15 of every stage, all rows ----
+    // lane = (rsub = l & 15, cq = l >> 4): a column quad's 16 row groups sit
+    // in one 16-lane DPP row, so the column sums need no cross-row shuffles
+    const int pw = wave - 4, cq = lane >> 4, rsub = lane & 15;
+    const int cofs = 16 * pw + 4 * cq;  // this lane's 4 columns in the stage
+    const float* rowp[NB];
+    bool rlive[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int cl = rsub + 16 * u;
+      rlive[u] = cl < K;
+      rowp[u] = src[cl < K ? cl : 0];
+    }
+    const float invK = 1.0f / float(K);
+    int64_t c = g;
+    int s0 = 0;
+    f32x4 v[PD][NB];
+    // One code path for full and ragged stages, so every stage issues the
+    // same NB loads and the compiler's load counting stays exact across the
+    // register sets (a ragged branch made it wait for every load in flight,
+    // s_waitcnt vmcnt(0), at each stage).  Lanes past the stage's width w
+    // load the stage's first quad (valid memory) and are zeroed when used;
+    // a quad that starts inside the stage stays inside the 16-byte aligned,
+    // 256-byte padded row.
+    auto fetch = [&](f32x4 (&vv)[NB], int& wout) __attribute__((always_inline)) {
+      // past this block's last stage: the same loads from column 0 (valid
+      // memory), width 0 -- the load count must not depend on the data
+      const bool live = c < n_chunks;
+      const int64_t cc = live ? c : 0;
+      const int len = live ? int(chunks[2 * cc + 1]) : 0;
+      const int64_t col0 = live ? chunks[2 * cc] + s0 : 0;
+      const int w = live ? (len - s0 < kStage ? len - s0 : kStage) : 0;
+      const int off = cofs < w ? cofs : 0;
+#pragma unroll
+      for (int u = 0; u < NB; ++u) vv[u] = ld4<true>(rowp[u] + col0 + off);
+      wout = w;
+      if (live) {
+        s0 += kStage;
+        if (s0 >= len) {
+          s0 = 0;
+          c += G;
+        }
+      }
+    };
+    // rows past K and columns past the stage's width read as 0
+    auto masked = [&](const f32x4& x, int u, int w) __attribute__((always_inline)) {
+      const uint32_t m = rlive[u] ? 0xffffffffu : 0u;
+      return f32x4{__uint_as_float(__float_as_uint(x.x) & (cofs < w ? m : 0u)),
+                   __uint_as_float(__float_as_uint(x.y) & (cofs + 1 < w ? m : 0u)),
+                   __uint_as_float(__float_as_uint(x.z) & (cofs + 2 < w ? m : 0u)),
+                   __uint_as_float(__float_as_uint(x.w) & (cofs + 3 < w ? m : 0u))};
+    };
+    // column means of this lane's 4 columns (sum over the wave's 16 row
+    // groups: lanes with the same cq, lane bits 2..5), centre, split, write
+    // sum over the 16 lanes of a DPP row: xor 1, xor 2 (quad_perm), then the
+    // half-row and row mirrors
+    auto row_sum = [](float x) __attribute__((always_inline)) {
+      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xf, 0xf, false));
+      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xf, 0xf, false));
+      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
+      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false));
+      return x;
+    };
+    const bool all_rows = K >= ROWS;
+    auto split_stage = [&](const f32x4 (&vv)[NB], int w, unsigned char* P) __attribute__((always_inline)) {
+      // a full stage of live rows (the common case) needs no masking
+      const bool plain = all_rows && w == kStage;
+      f32x4 x[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) x[u] = plain ? vv[u] : masked(vv[u], u, w);
+      f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NB; ++u) cs += x[u];
+      cs = f32x4{row_sum(cs.x), row_sum(cs.y), row_sum(cs.z), row_sum(cs.w)};
+      const f32x4 r = cs * invK;
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const f32x4 cc = x[u] - r;
+        const uint32_t h01 = pk_bf16(cc.x, cc.y), h23 = pk_bf16(cc.z, cc.w);
+        const float e0 = cc.x - bf16_lo(h01), e1 = cc.y - bf16_hi(h01);
+        const float e2 = cc.z - bf16_lo(h23), e3 = cc.w - bf16_hi(h23);
+        const uint32_t m01 = pk_bf16(e0, e1), m23 = pk_bf16(e2, e3);
+        const uint32_t l01 = pk_bf16(e0 - bf16_lo(m01), e1 - bf16_hi(m01));
+        const uint32_t l23 = pk_bf16(e2 - bf16_lo(m23), e3 - bf16_hi(m23));
+        unsigned char* d = P + (rsub + 16 * u) * kSplitRB + 2 * cofs;
+        *reinterpret_cast<u32x2v*>(d) = u32x2v{h01, h23};
+        *reinterpret_cast<u32x2v*>(d + PLANE) = u32x2v{m01, m23};
+        *reinterpret_cast<u32x2v*>(d + 2 * PLANE) = u32x2v{l01, l23};
+      }
+    };
+    // prologue: stages 0 .. PD - 1 in flight (stage s in register set s % PD),
+    // stage 0 split into P[0], stage PD issued into the freed set
+    int wset[PD];  // each register set's stage width
+    // (no loop here: a loop over the sets, even unrolled, left v[][] in
+    // scratch memory)
+    fetch(v[0], wset[0]);
+    fetch(v[1], wset[1]);
+    if constexpr (PD > 2) {
+      fetch(v[2], wset[2]);
+      fetch(v[3], wset[3]);
+    }
+    if constexpr (PD > 4) {
+      fetch(v[4], wset[4]);
+      fetch(v[5], wset[5]);
+    }
+    if (S > 0) split_stage(v[0], wset[0], sP[0]);
+    fetch(v[0], wset[0]);
+    lds_barrier();
+    // iteration k: split stage k + 1 (set (k + 1) % PD) into P[(k + 1) & 1],
+    // issue stage k + 1 + PD into that set, barrier.  Every iteration issues
+    // its loads (past the end: dummies), and the trip count is a multiple of
+    // PD, so the compiler's count of loads in flight is exact.
+    f32x4 diag_acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto iter = [&](auto set_tag, int k) __attribute__((always_inline)) {
+      constexpr int SL = decltype(set_tag)::value;
+      if constexpr (FEDAGG_GRAM_DIAG == 3) {  // loads only: the data feeds one sum
+#pragma unroll
+        for (int u = 0; u < NB; ++u) diag_acc += v[SL][u];
+      } else if (k + 1 < S && FEDAGG_GRAM_DIAG != 2) split_stage(v[SL], wset[SL], sP[(k + 1) & 1]);
+      fetch(v[SL], wset[SL]);
+      lds_barrier();
+    };
+    for (int k = 0; k < Spad; k += PD) {
+      iter(std::integral_constant<int, 1 % PD>{}, k);
+      if constexpr (PD > 1) iter(std::integral_constant<int, 2 % PD>{}, k + 1);
+      if constexpr (PD > 2) iter(std::integral_constant<int, 3 % PD>{}, k + 2);
+      if constexpr (PD > 3) iter(std::integral_constant<int, 4 % PD>{}, k + 3);
+      if constexpr (PD > 4) iter(std::integral_constant<int, 5 % PD>{}, k + 4);
+      if constexpr (PD > 5) iter(std::integral_constant<int, 6 % PD>{}, k + 5);
+    }
+    if constexpr (FEDAGG_GRAM_DIAG == 3)
+      if (diag_acc.x == 1.2345f && n_chunks < 0) partial[0] = diag_acc.y;  // never: keeps the loads
+    return;
+  }
+  // ---- consumer: the MFMAs of its row pair of tiles, one static code path
+  // per wave (the producers' registers are not live here, so the four paths
+  // do not crowd each other) ----
+  const int i16 = lane & 15, q = lane >> 4;
+  const unsigned char* fp0 = sP[0] + i16 * kSplitRB + 16 * q;
+  const unsigned char* fp1 = sP[1] + i16 * kSplitRB + 16 * q;
+  auto consume = [&](auto wtag) __attribute__((always_inline)) {
+    constexpr int W = decltype(wtag)::value;
+    using R = WsRows<NB, W>;
+    double acc64[TPW][4];
+    f32x4v acc[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc64[j][r] = 0.0;
+    }
+    int unfolded = 0;
+    auto fold = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < R::nm; ++j) {
+        asm volatile("s_nop 15" : "+v"(acc[j]));  // MFMA -> VALU wait states (see pairgram_split_kernel)
+        acc64[j][0] += double(acc[j].x);
+        acc64[j][1] += double(acc[j].y);
+        acc64[j][2] += double(acc[j].z);
+        acc64[j][3] += double(acc[j].w);
+        acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+      unfolded = 0;
+    };
+    auto step = [&](const unsigned char* fp, bool live) __attribute__((always_inline)) {
+      if (live) {
+        if constexpr (FEDAGG_GRAM_DIAG == 1)  // staging only: one LDS read keeps the planes live
+          acc[0].x += *reinterpret_cast<const float*>(fp);
+        else
+          ws_compute<NB, PLANE, W, TPW>(fp, acc);
+        if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
+      }
+      lds_barrier();
+    };
+    lds_barrier();  // the prologue's barrier: stage 0 in P[0]
+    for (int k = 0; k < Spad; k += 2) {  // Spad is even when PD is
+      step(fp0, k < S);
+      step(fp1, k + 1 < S);
+    }
+    if (unfolded) fold();
+#pragma unroll
+    for (int j = 0; j < R::nm; ++j) {
+      const int a = j < R::n1 ? W : NB - 1 - W, b = R::bgrp(j);
+      const int tt = a * NB - a * (a - 1) / 2 + (b - a);
+      double* out = partial + (int64_t(g) * NT + tt) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(4 * q + r) * 16 + i16] = acc64[j][r];
+    }
+  };
+  if (wave == 0)
+    consume(std::integral_constant<int, 0>{});
+  else if (wave == 1)
+    consume(std::integral_constant<int, 1>{});
+  else if (wave == 2)
+    consume(std::integral_constant<int, 2>{});
+  else
+    consume(std::integral_constant<int, 3>{});
+}
+
+#endif  // FEDAGG_GRAM_SPLIT >= 2
 
 // M (K x K, fp64, both triangles) = the tiles' partials summed over the chunk
 // groups in four fixed-order quarters (as tri_finish_kernel)
@@ -1587,7 +1882,23 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: workspace too small (fedagg_robust_work_len)");
   int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, work_len - mat, per);
   double* M = d_work + int64_t(G) * per;
-  if (FEDAGG_GRAM_SPLIT == 2) {
+#if FEDAGG_GRAM_SPLIT >= 2
+  if (FEDAGG_GRAM_SPLIT == 3) {
+    auto kern = pairgram_split_ws_kernel<8>;
+    switch (gram_groups(K)) {
+      case 1: kern = pairgram_split_ws_kernel<1>; break;
+      case 2: kern = pairgram_split_ws_kernel<2>; break;
+      case 3: kern = pairgram_split_ws_kernel<3>; break;
+      case 4: kern = pairgram_split_ws_kernel<4>; break;
+      case 5: kern = pairgram_split_ws_kernel<5>; break;
+      case 6: kern = pairgram_split_ws_kernel<6>; break;
+      case 7: kern = pairgram_split_ws_kernel<7>; break;
+      default: break;
+    }
+    const int G1 = G < 256 ? G : 256;  // one block per CU
+    hipLaunchKernelGGL(kern, dim3(unsigned(G1)), dim3(kSplit8BS), 0, st, d_src, K, d_chunks, n_chunks, G1, d_work);
+    G = G1;
+  } else if (FEDAGG_GRAM_SPLIT == 2) {
     auto kern = pairgram_split8_kernel<8>;
     switch (gram_groups(K)) {
       case 1: kern = pairgram_split8_kernel<1>; break;
@@ -1602,7 +1913,9 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     const int G1 = G < 256 ? G : 256;  // one block per CU
     hipLaunchKernelGGL(kern, dim3(unsigned(G1)), dim3(kSplit8BS), 0, st, d_src, K, d_chunks, n_chunks, G1, d_work);
     G = G1;
-  } else if (FEDAGG_GRAM_SPLIT) {
+  } else
+#endif
+  if (FEDAGG_GRAM_SPLIT) {
     auto kern = pairgram_split_kernel<8>;
     switch (gram_groups(K)) {
       case 1: kern = pairgram_split_kernel<1>; break;

@@ -43,7 +43,7 @@ def build() -> None:
     assert all(p.wait() == 0 for p in procs)
 
 
-def bench(rounds: int, out_path: str) -> None:
+def bench(rounds: int, out_path: str, chunk: int = 0) -> None:
     import torch
 
     from fedml_amd import _native as nat
@@ -97,7 +97,7 @@ def bench(rounds: int, out_path: str) -> None:
     cn = exact.mean(1) - exact.sum() / (2 * K * K)
     scale = cn[:, None] + cn[None, :]
     off = ~torch.eye(K, dtype=torch.bool, device=dev)
-    res = {"K": K, "n_chunks": int(n_chunks), "variants": VARIANTS}
+    res = {"K": K, "n_chunks": int(n_chunks), "chunk": chunk or nat.PAIR_CHUNK, "variants": VARIANTS}
     for tag in tags:
         err = ((outs[tag] - exact).abs() / scale)[off]
         res[tag] = {"ms": round(statistics.median(times[tag]), 4),
@@ -115,6 +115,7 @@ if __name__ == "__main__":
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--out", default="gpurun_out/gram_variants.json")
     ap.add_argument("--variant", action="append", default=[], help="TAG=-DFLAG=V[,-DFLAG2=V2]")
+    ap.add_argument("--chunk", type=int, default=0, help="chunk-table piece length (default FEDAGG_PAIR_CHUNK)")
     a = ap.parse_args()
     for v in a.variant:
         tag, flags = v.split("=", 1)
@@ -122,4 +123,4 @@ if __name__ == "__main__":
     if a.build:
         build()
     else:
-        bench(a.rounds, a.out)
+        bench(a.rounds, a.out, a.chunk)
