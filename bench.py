@@ -678,7 +678,7 @@ def main():
                           else achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "kernel": ({"secagg": "reduce_kernel<OpSumModI64>", "lsa": "reduce_kernel<OpWrapSumI64, LsaEpi>",
-                        "krum": ((f"pairgram_split_kernel<{(K + 15) // 16}> + gram_sum_kernel + gram_dist_kernel "
+                        "krum": ((f"pairgram_split8_kernel<{(K + 15) // 16}> + gram_sum_kernel + gram_dist_kernel "
                                   "(centred Gram, exact 3-way bf16 split, 16x16x32 bf16 MFMA)") if a.pair_distance == "gram" or
                                  (a.pair_distance == "auto" and K <= 128) else
                                  ("pairtri_kernel<16> + tri_finish_kernel" if K <= 64 else

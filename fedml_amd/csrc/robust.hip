@@ -906,7 +906,7 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 // 32 ks + 8q .. + 7.  A wave's tiles are a contiguous run in row-major order,
 // so consecutive tiles share their A group: its fragments are read once per run.
 #ifndef FEDAGG_GRAM_SPLIT
-#define FEDAGG_GRAM_SPLIT 1
+#define FEDAGG_GRAM_SPLIT 2
 #endif
 #ifndef FEDAGG_GRAM_SPLIT_FOLD
 #define FEDAGG_GRAM_SPLIT_FOLD 4
