@@ -916,6 +916,10 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 #ifndef FEDAGG_GRAM_SPLIT_FOLD
 #define FEDAGG_GRAM_SPLIT_FOLD 4
 #endif
+// 1: the 8-wave kernel's 2 x 2 group-block schedule at 8 groups (K 113..128)
+#ifndef FEDAGG_GRAM_BLK8
+#define FEDAGG_GRAM_BLK8 1
+#endif
 // producer waves' stages of loads in flight (FEDAGG_GRAM_SPLIT == 3): 2, 4 or 6
 #ifndef FEDAGG_GRAM_WS_PD
 #define FEDAGG_GRAM_WS_PD 4
@@ -1170,6 +1174,57 @@ __global__ __launch_bounds__(kGramBS, 2) void pairgram_split_kernel(const float*
 // rest, so every SIMD runs one pair's MFMAs per stage.
 constexpr int kSplit8BS = 512;
 
+// K = 113..128 (8 groups): the 36 tiles as 2 x 2 group blocks, so one read
+// of a group's fragments feeds two tiles.  Wave s (s < 4) takes a full block
+// (4 tiles: rows {A0, A1} x columns {B0, B1}); wave s + 4, on the same SIMD,
+// a diagonal block (3 tiles) and half of a full block (2 tiles, one column):
+// 9 tiles per SIMD, 27 fragment reads per SIMD and k-step where the row-run
+// schedule needs 36.
+constexpr int kBlk8[8][2][5] = {
+    // {A0, A1, B0, B1, diag} x 2 blocks (A0 < 0: none)
+    {{0, 1, 2, 3, 0}, {-1, -1, -1, -1, 0}}, {{0, 1, 4, 5, 0}, {-1, -1, -1, -1, 0}},
+    {{0, 1, 6, 7, 0}, {-1, -1, -1, -1, 0}}, {{2, 3, 4, 5, 0}, {-1, -1, -1, -1, 0}},
+    {{0, 1, 0, 1, 1}, {2, 3, 6, -1, 0}},    {{2, 3, 2, 3, 1}, {2, 3, 7, -1, 0}},
+    {{4, 5, 4, 5, 1}, {4, 5, 6, -1, 0}},    {{6, 7, 6, 7, 1}, {4, 5, 7, -1, 0}}};
+// the (row, column) group of each accumulator slot, in gblock's order
+__constant__ constexpr int kBlk8Tile[8][5][2] = {
+    {{0, 2}, {0, 3}, {1, 2}, {1, 3}, {-1, -1}}, {{0, 4}, {0, 5}, {1, 4}, {1, 5}, {-1, -1}},
+    {{0, 6}, {0, 7}, {1, 6}, {1, 7}, {-1, -1}}, {{2, 4}, {2, 5}, {3, 4}, {3, 5}, {-1, -1}},
+    {{0, 0}, {0, 1}, {1, 1}, {2, 6}, {3, 6}},   {{2, 2}, {2, 3}, {3, 3}, {2, 7}, {3, 7}},
+    {{4, 4}, {4, 5}, {5, 5}, {4, 6}, {5, 6}},   {{6, 6}, {6, 7}, {7, 7}, {4, 7}, {5, 7}}};
+
+// one block's tiles for k-step ks: (A0,B0), (A0,B1), (A1,B0) unless diagonal,
+// (A1,B1), into acc[S0 ..]; a diagonal block reads its rows once (B = A)
+template <int PLANE, int A0, int A1, int B0, int B1, bool DIAG, int S0, int TPW>
+__device__ __forceinline__ void gblock(const unsigned char* fp, int ks, f32x4v (&acc)[TPW]) {
+  bf16x8v FA0[3], FA1[3], FB0[3], FB1[3];
+  split_frag<PLANE>(fp, A0, ks, FA0);
+  split_frag<PLANE>(fp, A1, ks, FA1);
+  if constexpr (!DIAG) {
+    split_frag<PLANE>(fp, B0, ks, FB0);
+    if constexpr (B1 >= 0) split_frag<PLANE>(fp, B1, ks, FB1);
+  }
+  const bf16x8v(&b0)[3] = DIAG ? FA0 : FB0;
+  const bf16x8v(&b1)[3] = DIAG ? FA1 : FB1;
+  constexpr int s1 = S0 + 1, s2 = S0 + (B1 >= 0 ? 2 : 1), s3 = s2 + (DIAG ? 0 : 1);
+  acc[S0] = split_mfma6(FA0, b0, acc[S0]);
+  if constexpr (B1 >= 0) acc[s1] = split_mfma6(FA0, b1, acc[s1]);
+  if constexpr (!DIAG) acc[s2] = split_mfma6(FA1, b0, acc[s2]);
+  if constexpr (B1 >= 0) acc[s3] = split_mfma6(FA1, b1, acc[s3]);
+}
+
+template <int PLANE, int W, int TPW>
+__device__ __forceinline__ void gblocks8(const unsigned char* fp, f32x4v (&acc)[TPW]) {
+  constexpr int d0 = kBlk8[W][0][4], d1 = kBlk8[W][1][4];
+  constexpr int n0 = d0 ? 3 : (kBlk8[W][0][3] >= 0 ? 4 : 2);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    gblock<PLANE, kBlk8[W][0][0], kBlk8[W][0][1], kBlk8[W][0][2], kBlk8[W][0][3], d0 != 0, 0, TPW>(fp, ks, acc);
+    if constexpr (kBlk8[W][1][0] >= 0)
+      gblock<PLANE, kBlk8[W][1][0], kBlk8[W][1][1], kBlk8[W][1][2], kBlk8[W][1][3], d1 != 0, n0, TPW>(fp, ks, acc);
+  }
+}
+
 template <int NB>
 __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const float* const* __restrict__ src, int K,
                                                                      const int64_t* __restrict__ chunks,
@@ -1221,7 +1276,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
   int64_t c = g;
   int s0 = 0;
   f32x4 v[2][LPW];
-  auto fetch = [&](f32x4 (&vv)[LPW]) {
+  auto fetch = [&](f32x4 (&vv)[LPW]) __attribute__((always_inline)) {
     if (c >= n_chunks) return false;
     const int len = int(chunks[2 * c + 1]);
     const int64_t col0 = chunks[2 * c] + s0;
@@ -1248,7 +1303,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     }
     return true;
   };
-  auto fetch_skip = [&]() {
+  auto fetch_skip = [&]() __attribute__((always_inline)) {
     if (c >= n_chunks) return false;
     const int len = int(chunks[2 * c + 1]);
     s0 += kStage;
@@ -1258,12 +1313,12 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     }
     return true;
   };
-  auto masked = [&](const f32x4& x, int u) {
+  auto masked = [&](const f32x4& x, int u) __attribute__((always_inline)) {
     const uint32_t m = rlive[u] ? 0xffffffffu : 0u;
     return f32x4{__uint_as_float(__float_as_uint(x.x) & m), __uint_as_float(__float_as_uint(x.y) & m),
                  __uint_as_float(__float_as_uint(x.z) & m), __uint_as_float(__float_as_uint(x.w) & m)};
   };
-  auto stage_sums = [&](const f32x4 (&vv)[LPW], int sb) {
+  auto stage_sums = [&](const f32x4 (&vv)[LPW], int sb) __attribute__((always_inline)) {
     f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < LPW; ++u) cs += masked(vv[u], u);
@@ -1276,7 +1331,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     }
     if (q == 0) *reinterpret_cast<f32x4*>(&sSum[sb][wave][4 * i16]) = cs;
   };
-  auto stage_split = [&](const f32x4 (&vv)[LPW], int sb, unsigned char* P) {
+  auto stage_split = [&](const f32x4 (&vv)[LPW], int sb, unsigned char* P) __attribute__((always_inline)) {
     f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
     {
       f32x4 s8[8];
@@ -1302,7 +1357,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     }
   };
   int unfolded = 0;
-  auto fold = [&]() {
+  auto fold = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       asm volatile("s_nop 15" : "+v"(acc[j]));  // MFMA -> VALU wait states (see pairgram_split_kernel)
@@ -1315,9 +1370,24 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     unfolded = 0;
   };
   const int fo = i16 * kSplitRB + 16 * q;
-  auto compute = [&](const unsigned char* P) {
+  auto compute = [&](const unsigned char* P) __attribute__((always_inline)) {
     if constexpr (FEDAGG_GRAM_DIAG == 1) {  // staging only: one LDS read keeps the planes live
       acc[0].x += *reinterpret_cast<const float*>(P + fo);
+      return;
+    }
+    if constexpr (NB == 8 && FEDAGG_GRAM_BLK8) {
+      const unsigned char* fp = P + fo;
+      switch (wave) {
+        case 0: gblocks8<PLANE, 0>(fp, acc); break;
+        case 1: gblocks8<PLANE, 1>(fp, acc); break;
+        case 2: gblocks8<PLANE, 2>(fp, acc); break;
+        case 3: gblocks8<PLANE, 3>(fp, acc); break;
+        case 4: gblocks8<PLANE, 4>(fp, acc); break;
+        case 5: gblocks8<PLANE, 5>(fp, acc); break;
+        case 6: gblocks8<PLANE, 6>(fp, acc); break;
+        default: gblocks8<PLANE, 7>(fp, acc); break;
+      }
+      if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
       return;
     }
     if (nmine > 0) {
@@ -1351,7 +1421,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     if (h1) stage_sums(v[1], 1);
     lds_barrier();
     // iteration k (two at a time, so the register sets are static)
-    auto iter = [&](auto cur_tag, bool& hn, bool& hnn) {
+    auto iter = [&](auto cur_tag, bool& hn, bool& hnn) __attribute__((always_inline)) {
       constexpr int C = decltype(cur_tag)::value;  // k % 2
       // hn: stage k + 1 exists (in v[C ^ 1], sums in sSum[C ^ 1]); hnn: stage k + 2 (in v[C])
       bool hnnn = false;
@@ -1375,10 +1445,15 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     }
   }
   if (unfolded) fold();
+  const int nout = NB == 8 && FEDAGG_GRAM_BLK8 ? (wave < 4 ? 4 : 5) : nmine;
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
-    if (j < nmine) {
-      const int a = j < n1 ? r1 : r2, b = j < n1 ? b1 + j : b2 + (j - n1);
+    if (j < nout) {
+      int a = j < n1 ? r1 : r2, b = j < n1 ? b1 + j : b2 + (j - n1);
+      if constexpr (NB == 8 && FEDAGG_GRAM_BLK8) {
+        a = kBlk8Tile[wave][j][0];
+        b = kBlk8Tile[wave][j][1];
+      }
       const int tt = a * NB - a * (a - 1) / 2 + (b - a);
       double* out = partial + (int64_t(g) * NT + tt) * 256;
 #pragma unroll
