@@ -936,11 +936,11 @@ typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 
 // two floats -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
 }
-__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+[[maybe_unused]] __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+[[maybe_unused]] __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
 // The split kernel's tile schedule: wave w takes the two rows of tiles w and
 // NB - 1 - w of the group triangle (NB - w and w + 1 tiles: NB + 1 in all, the
@@ -955,7 +955,7 @@ __device__ __forceinline__ void split_frag(const unsigned char* fp, int grp, int
   for (int pl = 0; pl < 3; ++pl) F[pl] = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(p + pl * PLANE));
 }
 
-__device__ __forceinline__ f32x4v split_mfma6(const bf16x8v (&A)[3], const bf16x8v (&B)[3], f32x4v x) {
+[[maybe_unused]] __device__ __forceinline__ f32x4v split_mfma6(const bf16x8v (&A)[3], const bf16x8v (&B)[3], f32x4v x) {
   x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], x, 0, 0, 0);
   x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[1], x, 0, 0, 0);
   x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[0], x, 0, 0, 0);
@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(kGramBS, 2) void pairgram_split_kernel(const float*
   }
 }
 
-#if FEDAGG_GRAM_SPLIT >= 2  // experimental variants, not built by default
+#if FEDAGG_GRAM_SPLIT >= 2  // the 8-wave kernel (default) and the experimental producer / consumer one
 // FEDAGG_GRAM_SPLIT == 2: the same split Gram with 8 waves per block and ONE
 // block per CU, so the planes can be double-buffered (2 x 55 KB) and a stage
 // needs one barrier, and each lane's raw rows are prefetched two stages
@@ -1462,6 +1462,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
   }
 }
 
+#if FEDAGG_GRAM_SPLIT == 3  // the producer / consumer variant
 // Consumer wave W's tiles, unrolled at compile time (no branches between
 // tiles): tile J of its row pair, B fragments ping-ponged by J, tile J + 1's
 // read issued before tile J's six MFMAs.  Rows W (n1 tiles) and NB - 1 - W
@@ -1735,6 +1736,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split_ws_kernel(const f
     consume(std::integral_constant<int, 3>{});
 }
 
+#endif  // FEDAGG_GRAM_SPLIT == 3
 #endif  // FEDAGG_GRAM_SPLIT >= 2
 
 // M (K x K, fp64, both triangles) = the tiles' partials summed over the chunk
@@ -1965,8 +1967,9 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: workspace too small (fedagg_robust_work_len)");
   int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, work_len - mat, per);
   double* M = d_work + int64_t(G) * per;
-#if FEDAGG_GRAM_SPLIT >= 2
-  if (FEDAGG_GRAM_SPLIT == 3) {
+  // one kernel per build (FEDAGG_GRAM_SPLIT): only the selected one is instantiated
+#if FEDAGG_GRAM_SPLIT == 3
+  {
     auto kern = pairgram_split_ws_kernel<8>;
     switch (gram_groups(K)) {
       case 1: kern = pairgram_split_ws_kernel<1>; break;
@@ -1981,7 +1984,9 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     const int G1 = G < 256 ? G : 256;  // one block per CU
     hipLaunchKernelGGL(kern, dim3(unsigned(G1)), dim3(kSplit8BS), 0, st, d_src, K, d_chunks, n_chunks, G1, d_work);
     G = G1;
-  } else if (FEDAGG_GRAM_SPLIT == 2) {
+  }
+#elif FEDAGG_GRAM_SPLIT == 2
+  {
     auto kern = pairgram_split8_kernel<8>;
     switch (gram_groups(K)) {
       case 1: kern = pairgram_split8_kernel<1>; break;
@@ -1996,9 +2001,9 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     const int G1 = G < 256 ? G : 256;  // one block per CU
     hipLaunchKernelGGL(kern, dim3(unsigned(G1)), dim3(kSplit8BS), 0, st, d_src, K, d_chunks, n_chunks, G1, d_work);
     G = G1;
-  } else
-#endif
-  if (FEDAGG_GRAM_SPLIT) {
+  }
+#elif FEDAGG_GRAM_SPLIT == 1
+  {
     auto kern = pairgram_split_kernel<8>;
     switch (gram_groups(K)) {
       case 1: kern = pairgram_split_kernel<1>; break;
@@ -2012,12 +2017,14 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     }
     hipLaunchKernelGGL(kern, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G, d_work);
   }
-  else if (K <= 64)
+#else
+  if (K <= 64)
     hipLaunchKernelGGL(pairgram_kernel<4>, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G,
                        d_work);
   else
     hipLaunchKernelGGL(pairgram_kernel<8>, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G,
                        d_work);
+#endif
   hipLaunchKernelGGL(gram_sum_kernel, dim3(unsigned((per + 63) / 64)), dim3(256), 0, st, d_work, G, K, M);
   hipLaunchKernelGGL(gram_dist_kernel, dim3(unsigned((mat + 255) / 256)), dim3(256), 0, st, M, K, d_out);
   return rcheck("fedagg_pairgram2_f32");
