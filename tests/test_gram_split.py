@@ -58,3 +58,45 @@ def test_six_products_bound():
     # and the dropped terms are what makes the difference
     dropped = f(ma) * f(lb) + f(la) * f(mb) + f(la) * f(lb)
     np.testing.assert_allclose(kept + dropped, exact, rtol=0, atol=1e-300)
+
+
+def test_block_schedule_covers_the_triangle_once():
+    """pairgram_split8_kernel's 2 x 2 group-block schedule at 8 groups
+    (csrc/robust.hip, kBlk8 / kBlk8Tile): every tile (a <= b) of the 8 x 8
+    group triangle exactly once, 9 tiles per SIMD (waves s and s + 4), and the
+    slot table agrees with the blocks' order (A0B0, A0B1, A1B0 unless diagonal,
+    A1B1)."""
+    import os
+    import re
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "fedml_amd", "csrc", "robust.hip")).read()
+
+    def table(name):
+        body = src[src.index(name):]
+        body = body[body.index("{"):body.index("};") + 1]
+        return [int(x) for x in re.findall(r"-?\d+", body)]
+
+    blk = table("constexpr int kBlk8[8][2][5]")
+    tiles = table("kBlk8Tile[8][5][2]")
+    assert len(blk) == 80 and len(tiles) == 80
+    seen = []
+    for w in range(8):
+        slots = []
+        for k in range(2):
+            a0, a1, b0, b1, diag = blk[w * 10 + k * 5: w * 10 + k * 5 + 5]
+            if a0 < 0:
+                continue
+            slots.append((a0, b0))
+            if b1 >= 0:
+                slots.append((a0, b1))
+            if not diag:
+                slots.append((a1, b0))
+            if b1 >= 0:
+                slots.append((a1, b1))
+        want = [(tiles[w * 10 + 2 * j], tiles[w * 10 + 2 * j + 1]) for j in range(5)]
+        want = [t for t in want if t[0] >= 0]
+        assert slots == want, w
+        seen += slots
+    assert sorted(seen) == [(a, b) for a in range(8) for b in range(a, 8)]
+    per_simd = [sum(1 for w in (s, s + 4) for j in range(5) if tiles[w * 10 + 2 * j] >= 0) for s in range(4)]
+    assert per_simd == [9, 9, 9, 9]
