@@ -74,6 +74,7 @@ def test_block_schedule_covers_the_triangle_once():
     def table(name):
         body = src[src.index(name):]
         body = body[body.index("{"):body.index("};") + 1]
+        body = re.sub(r"//[^\n]*", "", body)  # comments
         return [int(x) for x in re.findall(r"-?\d+", body)]
 
     blk = table("constexpr int kBlk8[8][2][5]")
