@@ -63,8 +63,8 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # packed fp32 vector peak (v_pk_fma_f32: 64 FLOP/clk/SIMD x 1,024 SIMDs x 2.4 GHz), the ceiling of
 # the exact-difference Krum pair kernel, whose packed subtract + packed FMA are 3 flops per client pair and
-# element; the fp32 MFMA (v_mfma_f32_16x16x4_f32, the centred-Gram kernel) has the same 157.3 TF peak
-# (MI355X_MICROARCH.md, chip-level parameters)
+# element (the centred-Gram kernel on the bf16 matrix cores is priced against HBM instead: it reads the
+# rows once; MI355X_MICROARCH.md, chip-level parameters)
 VALU_PEAK_TFLOPS = 157.3
 SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
 CLOCK_GHZ = 2.4

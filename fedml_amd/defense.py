@@ -278,8 +278,9 @@ def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks:
     """K x K fp64 squared distances of K fp32 device rows over the chunked
     columns.  method "exact": the reference's fp32 differences, squared and
     summed on the VALU (fedagg_pairdist2_f32); "gram": the centred Gram on the
-    fp32 matrix cores (fedagg_pairgram2_f32, K <= 128); "auto": gram when K
-    allows it (same Krum selections, ~2x faster at config 3)
+    bf16 matrix cores with an exact three-way split (fedagg_pairgram2_f32,
+    K <= 128); "auto": gram when K allows it (same Krum
+    selections, ~3x faster at config 3)
     and the result is well conditioned (``gram_condition`` <=
     GRAM_MAX_CONDITION), else the exact kernel: one far-away update (the case
     Krum exists for) moves the client mean, and the honest clients' distances

@@ -291,13 +291,14 @@ int fedagg_pairdist2_f32(const float* const* d_src, int32_t K,
                          double* d_work, int64_t work_len, fedagg_stream_t stream);
 
 /* The same K x K matrix as fedagg_pairdist2_f32 (the same replaced lines,
- * krum_defense.py:47-60) for K <= 128, as a centred Gram on the fp32 matrix
- * cores: per 64-column stage c = x - (column mean over the K clients),
- * G = C C^T on v_mfma_f32_16x16x4_f32 (fp32 over the stage, fp64 across
- * stages), d_out[i*K + j] = max(0, G_ii + G_jj - 2 G_ij).  Not the reference's
- * fp32 differences: |error| ~ 1e-7 (|c_i|^2 + |c_j|^2), the order of the
- * reference's own fp32 torch.norm when the clients are spread about as far
- * as they are apart.  d_work: fedagg_robust_work_len(FEDAGG_WORK_PAIRGRAM,
+ * krum_defense.py:47-60) for K <= 128, as a centred Gram on the bf16 matrix
+ * cores: per 64-column stage c = x - (column mean over the K clients), each
+ * c split exactly into three bf16 parts h + m + l, G = C C^T from six
+ * v_mfma_f32_16x16x32_bf16 products per 32 columns (hh, hm, mh, mm, hl, lh;
+ * fp32 over 4 stages, fp64 across), d_out[i*K + j] = max(0, G_ii + G_jj -
+ * (G_ij + G_ji)).  Not the reference's fp32 differences: |error| ~ 1e-7
+ * (|c_i|^2 + |c_j|^2), the order of the reference's own fp32 torch.norm when
+ * the clients are spread about as far as they are apart.  d_work: fedagg_robust_work_len(FEDAGG_WORK_PAIRGRAM,
  * K, n_chunks) doubles (-1 there for K > 128). */
 int fedagg_pairgram2_f32(const float* const* d_src, int32_t K,
                          const int64_t* d_chunks, int64_t n_chunks, double* d_out,
