@@ -916,6 +916,10 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 #ifndef FEDAGG_GRAM_SPLIT_FOLD
 #define FEDAGG_GRAM_SPLIT_FOLD 4
 #endif
+// diagnostic: per-phase s_memtime stamps of the 8-wave kernel (wrong results)
+#ifndef FEDAGG_GRAM_STAMPS
+#define FEDAGG_GRAM_STAMPS 0
+#endif
 // 1: the 8-wave kernel's 2 x 2 group-block schedule at 8 groups (K 113..128)
 #ifndef FEDAGG_GRAM_BLK8
 #define FEDAGG_GRAM_BLK8 1
@@ -938,6 +942,15 @@ typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 // two floats -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32)
 [[maybe_unused]] __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
+// FEDAGG_GRAM_STAMPS (diagnostic builds only, tools/gram_variants.py):
+// s_memtime with its lgkmcnt wait in one statement, fenced for the scheduler
+[[maybe_unused]] __device__ __forceinline__ unsigned long long gram_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
 }
 [[maybe_unused]] __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 [[maybe_unused]] __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -1421,18 +1434,34 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     if (h1) stage_sums(v[1], 1);
     lds_barrier();
     // iteration k (two at a time, so the register sets are static)
+    [[maybe_unused]] int it = 0;
+    [[maybe_unused]] double phase_sum[4] = {0.0, 0.0, 0.0, 0.0};
     auto iter = [&](auto cur_tag, bool& hn, bool& hnn) __attribute__((always_inline)) {
       constexpr int C = decltype(cur_tag)::value;  // k % 2
       // hn: stage k + 1 exists (in v[C ^ 1], sums in sSum[C ^ 1]); hnn: stage k + 2 (in v[C])
       bool hnnn = false;
+      unsigned long long ts[5] = {0, 0, 0, 0, 0};
+      if constexpr (FEDAGG_GRAM_STAMPS) ts[0] = gram_stamp();
       if (hn && FEDAGG_GRAM_DIAG != 2) {
         stage_split(v[C ^ 1], C ^ 1, sP[C ^ 1]);
         hnnn = hnn && fetch(v[C ^ 1]);  // stage k + 3
       }
       if (FEDAGG_GRAM_DIAG == 2) hnnn = hnn && fetch_skip();  // compute only: same stage count
+      if constexpr (FEDAGG_GRAM_STAMPS) ts[1] = gram_stamp();
       compute(sP[C]);
+      if constexpr (FEDAGG_GRAM_STAMPS) ts[2] = gram_stamp();
       if (hnn && FEDAGG_GRAM_DIAG != 2) stage_sums(v[C], C);
+      if constexpr (FEDAGG_GRAM_STAMPS) ts[3] = gram_stamp();
       lds_barrier();
+      if constexpr (FEDAGG_GRAM_STAMPS) {
+        ts[4] = gram_stamp();
+        // iterations 64..191: the four phase lengths, summed (written at the end)
+        if (it >= 64 && it < 192) {
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph) phase_sum[ph] += double(ts[ph + 1] - ts[ph]);
+        }
+        ++it;
+      }
       const bool more = hn;
       hn = hnn;
       hnn = hnnn;
@@ -1442,6 +1471,16 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     while (true) {
       if (!iter(std::integral_constant<int, 0>{}, hn, hnn)) break;
       if (!iter(std::integral_constant<int, 1>{}, hn, hnn)) break;
+    }
+    if constexpr (FEDAGG_GRAM_STAMPS) {
+      // blocks 0..7, every wave: the four phase lengths summed over
+      // iterations 64..191, into the workspace's unused tail (G1 = 256 of the
+      // G it was sized for)
+      if (g < 8 && lane == 0) {
+        double* st = partial + int64_t(256) * NT * 256 + (g * 8 + wave) * 4;
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) st[ph] = phase_sum[ph];
+      }
     }
   }
   if (unfolded) fold();

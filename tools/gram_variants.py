@@ -68,6 +68,7 @@ def bench(rounds: int, out_path: str, chunk: int = 0) -> None:
         libs[tag] = ctypes.CDLL(os.path.join(OUT, f"robust_{tag}.so"))
     outs = {t: torch.empty((K, K), dtype=torch.float64, device=dev) for t in libs}
     times = {t: [] for t in libs}
+    stamps = {}
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     tags = list(libs)
     for r in range(rounds + 1):
@@ -84,6 +85,16 @@ def bench(rounds: int, out_path: str, chunk: int = 0) -> None:
             assert rc == 0, tag
             if r:
                 times[tag].append(ev0.elapsed_time(ev1))
+            if tag.startswith("stamps") and r == rounds:
+                # FEDAGG_GRAM_STAMPS: blocks 0..7 x 8 waves x 4 phases (split +
+                # fetch, MFMAs, sums, barrier) in s_memtime ticks summed over
+                # 128 iterations, after the 256 used blocks' partials
+                nt = ((K + 15) // 16) * ((K + 15) // 16 + 1) // 2
+                stt = work[256 * nt * 256: 256 * nt * 256 + 8 * 8 * 4].view(8, 8, 4).cpu() / 128
+                stamps[tag] = {"per_wave_mean_ticks": [[round(float(x), 1) for x in stt[:, w, :].mean(0)]
+                                                       for w in range(8)],
+                               "phases": ["split+fetch", "mfma", "sums", "barrier"]}
+                print(tag, stamps[tag], flush=True)
     # the exact-difference kernel's D, and each variant's error against it in
     # the units test_gpu_dist_defenses.py bounds (|c_i|^2 + |c_j|^2, the
     # double-centred norms)
@@ -106,6 +117,7 @@ def bench(rounds: int, out_path: str, chunk: int = 0) -> None:
                     "krum_order_same_as_exact": bool(torch.equal(outs[tag].sort(1).values[:, :64].sum(1).argsort(),
                                                                  exact.sort(1).values[:, :64].sum(1).argsort()))}
         print(tag, res[tag], flush=True)
+    res["stamps"] = stamps
     json.dump(res, open(out_path, "w"), indent=1)
 
 
