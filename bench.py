@@ -30,6 +30,12 @@ Every config keeps BASELINE.json's client count (4 / 32 / 128 / 512 / 64;
     python bench.py                       # 1 GPU, default steps
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8
+    python bench.py --gpus 8              # the same: bench.py spawns the 8 ranks itself
+
+In --mode param every multi-GPU line also nests "inprocess": rank 0 alone
+drives all N GPUs from ONE process through fedml_amd.multidev.MultiDeviceBucket
+(the only multi-GPU mode FedML's single server process can use), same clients,
+per-device kernel GB/s and roofline fraction (--no-inprocess skips it).
 
 Prints ONE JSON line on rank 0 (contract in the task statement); at N = 1 the
 cpu_baseline leg times the reference's own CPU loop (oracle/cpu_baseline.py)
@@ -118,7 +124,57 @@ def parse(argv=None):
     ap.add_argument("--no-exchange", action="store_true",
                     help="multi-GPU --mode param: skip the nested client-axis (RCCL reduce-scatter) measurement")
     ap.add_argument("--cpu-reps", type=int, default=5, help="cpu_baseline: timed runs after one warm-up")
+    ap.add_argument("--no-inprocess", action="store_true",
+                    help="multi-GPU --mode param: skip the nested one-process measurement (MultiDeviceBucket over "
+                         "the N GPUs, the mode FedML's single server process uses)")
+    ap.add_argument("--spawn-probe", action="store_true", help=argparse.SUPPRESS)  # CPU test of the self-launch
     return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, probe: bool = False) -> int:
+    """`python bench.py --gpus N` without torch.distributed.run: start N
+    worker processes of this script, one per GPU, with torchrun's environment
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* on 127.0.0.1), wait for them and
+    return the first failing exit code (0 if all succeed).  The parent never
+    touches the GPU (no HIP call before or after the spawn: the workers start
+    as fresh processes, not forks), and rank 0 prints the JSON line."""
+    import subprocess
+
+    assert not torch.cuda.is_initialized(), "the launcher must not initialise HIP"
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # a rank died: the others would wait in a collective forever
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    if probe:
+        print(json.dumps({"probe": "parent", "cuda_initialized": torch.cuda.is_initialized(),
+                          "exit_codes": [p.returncode for p in procs]}), flush=True)
+    return rc
 
 
 def plan_clients(config: str, world: int, rank: int, mode: str, clients_total=None, weak: bool = False,
@@ -387,14 +443,100 @@ def measure_client_axis(a, entries, n_elems: int, K_total: int, world: int, rank
     return out
 
 
+def measure_inprocess(a, entries, n_elems: int, K_total: int, world: int) -> dict:
+    """The multi-GPU mode FedML's server can use: ONE process (the server is
+    one process, python/fedml/__init__.py:330-348) driving `world` GPUs
+    through fedml_amd.multidev.MultiDeviceBucket: whole keys per device, every
+    device reducing its keys of all K_total clients in the reference order (no
+    exchange, bit-exact with one GPU; cross_silo/server/fedml_aggregator.py:
+    58-67 feeds it).  Device-resident rows, the same clients and weights as
+    the headline; runs on rank 0 while the other ranks wait at a barrier with
+    their rows freed.  Returns the "inprocess" object of the JSON line."""
+    from fedml_amd.synth import sample_nums
+
+    n_dev = torch.cuda.device_count()
+    devices = [torch.device("cuda", i % n_dev) for i in range(world)]
+    mb = multidev.MultiDeviceBucket(entries, K_total, devices, low_precision_acc=a.acc)
+    for s, b in enumerate(mb.shards):
+        with torch.cuda.device(b.device):
+            for gi, (dt, g) in enumerate(b.groups.items()):
+                fill_rows(g.rows, g.length, seed=5000 + 100 * s + gi, round_idx=3)
+    ns = sample_nums(K_total, seed=1)
+    w = mb.weights(ns)
+    outs = [b.new_outputs() for b in mb.shards]
+    doms = [b.dominant_dtype() for b in mb.shards]
+    used = sorted({d.index for d in mb.devices})
+
+    def sync_all():
+        for i in used:
+            torch.cuda.synchronize(i)
+
+    def step(evs=None):
+        for s, b in enumerate(mb.shards):  # every device's launches queued before any is waited for
+            b.reduce_into(outs[s], w, events={doms[s]: evs[s]} if evs is not None else None)
+
+    for _ in range(a.warmup):
+        step()
+    evs = []
+    for _ in range(a.steps):
+        per = []
+        for b in mb.shards:
+            with torch.cuda.device(b.device):
+                per.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        evs.append(per)
+    sync_all()
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        step(evs[s])
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    per_dev = []
+    total_bytes = 0
+    for s, b in enumerate(mb.shards):
+        g = b.groups[doms[s]]
+        dom_bytes = K_total * g.length * g.rows.element_size() + \
+            g.length * torch.empty((), dtype=g.out_dtype).element_size()
+        kern_ms = sum(ev[s][0].elapsed_time(ev[s][1]) for ev in evs) / a.steps
+        gbps = dom_bytes / (kern_ms / 1e3) / 1e9
+        total_bytes += b.algorithmic_bytes()
+        per_dev.append({"device": str(b.device), "keys": len(b.entries), "alg_bytes_per_step": dom_bytes,
+                        "kernel_ms_per_step": round(kern_ms, 4), "gbps": round(gbps, 1),
+                        "frac": round(gbps / HBM_PEAK_GBPS, 4)})
+    ms = elapsed / a.steps * 1e3
+    shared = len(used) < len(mb.shards)
+    out = {"mode": "one process, G GPUs (fedml_amd.multidev.MultiDeviceBucket)", "devices": len(mb.shards),
+           "distinct_gpus": len(used), "clients_total": K_total,
+           "value": K_total * n_elems / (elapsed / a.steps), "unit": "client-params/s", "ms_per_step": ms,
+           "slowest_device_kernel_ms": max(d["kernel_ms_per_step"] for d in per_dev),
+           "per_device": per_dev, "aggregate_gbps": round(total_bytes / (elapsed / a.steps) / 1e9, 1),
+           "aggregate_frac_of_n_peaks": round(total_bytes / (elapsed / a.steps) / 1e9 / (len(used) * HBM_PEAK_GBPS),
+                                              4),
+           "shard_balance": round(max(mb.shard_bytes()) / (sum(mb.shard_bytes()) / len(mb.shards)), 4),
+           "parity": "bit-exact with one GPU (whole keys per device, reference client order; "
+                     "tests/test_gpu_multidev.py)",
+           "note": ("shards share one GPU here: a rehearsal of the launch pattern, not a multi-GPU rate"
+                    if shared else "device-resident rows; reduce_to_host (D2H) excluded, as in the headline")}
+    del mb, outs
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launched as `python bench.py --gpus N`: become torchrun ourselves
+        raise SystemExit(spawn_ranks(a.gpus, sys.argv[1:], probe=a.spawn_probe))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
+    if a.gpus > 1 and world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one process per GPU (or drop WORLD_SIZE "
+                         "and let bench.py spawn them)")
+    if a.spawn_probe:
+        print(json.dumps({"probe": "rank", "rank": rank, "local_rank": local, "world": world,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
+                          "cuda_initialized": torch.cuda.is_initialized()}), flush=True)
+        return
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     if world > 1:
@@ -730,15 +872,28 @@ def main():
                                 "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
                                 "note": "comm_ms: mean over ranks of the chunks' reduce-scatter time on the comm "
                                         "stream (overlapping the next chunk's reduction)"}
-        elif mode == "param" and a.op == "fedavg" and not a.fedopt and not a.no_exchange:
-            # the headline is the exchange-free parameter axis; north_star's
-            # client axis + RCCL reduce-scatter runs next on the same clients
-            del step, outs, gd, groups, bucket  # free this rank's rows first
+        elif mode == "param" and a.op == "fedavg" and not a.fedopt:
+            # the headline is the exchange-free parameter axis of N processes;
+            # two more measurements on the same clients follow, each after this
+            # rank's rows are freed
+            del step, outs, gd, groups, bucket
             torch.cuda.empty_cache()
-            try:
-                line["exchange"] = measure_client_axis(a, entries, n_elems, K_total, world, rank, dev)
-            except Exception as e:  # the headline above stands; report what the nested run hit
-                line["exchange"] = {"mode": "client", "error": f"{type(e).__name__}: {e}"}
+            if not a.no_exchange:
+                # north_star's client axis + RCCL reduce-scatter over xGMI
+                try:
+                    line["exchange"] = measure_client_axis(a, entries, n_elems, K_total, world, rank, dev)
+                except Exception as e:  # the headline above stands; report what the nested run hit
+                    line["exchange"] = {"mode": "client", "error": f"{type(e).__name__}: {e}"}
+            if not a.no_inprocess:
+                # FedML's server is ONE process: rank 0 alone drives all N
+                # GPUs through the multi-device bucket while the others wait
+                dist.barrier()
+                if rank == 0:
+                    try:
+                        line["inprocess"] = measure_inprocess(a, entries, n_elems, K_total, world)
+                    except Exception as e:
+                        line["inprocess"] = {"error": f"{type(e).__name__}: {e}"}
+                dist.barrier()
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
         line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
     if rank == 0:

@@ -176,54 +176,103 @@ def agg(args, raw_grad_list):
     return torch_aggregator(args, raw_grad_list, training_num)
 
 
+def scale(t: torch.Tensor, w: float) -> torch.Tensor:
+    """torch's `t * w` for a Python-float w, one rounding in the opmath type:
+    float types keep their dtype, integer / bool tensors become float32
+    (agg_operator.py:41,44 `local_model_params[k] * w`)."""
+    dt = t.dtype
+    if dt == torch.float32 or dt in _INT_DTYPES:
+        return from_np((to_np(t).astype(np.float32) * np.float32(w)).astype(np.float32), torch.float32, t.shape)
+    if dt == torch.float64:
+        return from_np(to_np(t) * np.float64(w), torch.float64, t.shape)
+    if dt == torch.bfloat16:
+        return from_np(f32_to_bf16_bits(bf16_bits_to_f32(to_np(t)) * np.float32(w)), torch.bfloat16, t.shape)
+    if dt == torch.float16:
+        return from_np((to_np(t).astype(np.float32) * np.float32(w)).astype(np.float16), torch.float16, t.shape)
+    raise TypeError(f"oracle: unsupported dtype {dt}")
+
+
+def add(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """torch's `a += b` for same-dtype tensors (float32 when a promoted
+    integer key meets a float32 one): one rounding in the dtype; integer adds
+    wrap."""
+    dt = a.dtype
+    if dt == torch.bfloat16:
+        return from_np(f32_to_bf16_bits(bf16_bits_to_f32(to_np(a)) + bf16_bits_to_f32(to_np(b))), dt, a.shape)
+    if dt == torch.float16:
+        return from_np((to_np(a).astype(np.float32) + to_np(b).astype(np.float32)).astype(np.float16), dt, a.shape)
+    if dt == torch.float32:
+        return from_np(to_np(a) + to_np(b).astype(np.float32), dt, a.shape)
+    with np.errstate(over="ignore"):
+        return from_np((to_np(a) + to_np(b)).astype(to_np(a).dtype), dt, a.shape)
+
+
+def _set_inplace(t: torch.Tensor, v: torch.Tensor) -> None:
+    """`t += x` keeps t's storage: write v's bits into t."""
+    if t.dtype == torch.bfloat16:
+        t.view(torch.int16).copy_(v.view(torch.int16).reshape(t.shape))
+    else:
+        t.copy_(v.reshape(t.shape))
+
+
 def torch_aggregator(args, raw_grad_list, training_num):
+    """agg_operator.py:33-134 step by step: every client's tensors are looked
+    up in its dict at the moment the reference's loop reads them, so a dict
+    listed twice reads the running accumulator exactly as the reference does
+    (the accumulator IS client 0's dict entry; FedAvg_seq / FedDyn and
+    SCAFFOLD's control variates add into client 0's own tensors in place)."""
     opt = args.federated_optimizer
     K = len(raw_grad_list)
     if opt in ("FedAvg", "FedProx"):
         avg_params = raw_grad_list[0][1]
         for k in list(avg_params.keys()):
-            ts = [raw_grad_list[i][1][k] for i in range(K)]
-            ws = [raw_grad_list[i][0] / training_num for i in range(K)]
-            avg_params[k] = wsum(ts, ws)
+            for i in range(K):
+                local_sample_number, local_model_params = raw_grad_list[i]
+                w = local_sample_number / training_num
+                x = scale(local_model_params[k], w)
+                avg_params[k] = x if i == 0 else add(avg_params[k], x)
         return avg_params
     if opt in ("FedAvg_seq", "FedDyn"):
         avg_params = raw_grad_list[0][1]
         for k in list(avg_params.keys()):
-            ts = [raw_grad_list[i][1][k] for i in range(K)]
-            res = seqsum(ts)
-            t0 = ts[0]  # aliased: client 0's tensor is updated in place
-            if t0.dtype == torch.bfloat16:
-                t0.view(torch.int16).copy_(torch.from_numpy(res.view(np.int16)).reshape(t0.shape))
-            else:
-                t0.copy_(torch.from_numpy(np.ascontiguousarray(res)).reshape(t0.shape))
-            avg_params[k] = t0
+            for i in range(K):
+                local_model_params = raw_grad_list[i][1]
+                if i == 0:
+                    avg_params[k] = local_model_params[k]  # client 0's own tensor, summed into in place
+                else:
+                    _set_inplace(avg_params[k], add(avg_params[k], local_model_params[k]))
         return avg_params
     if opt == "SCAFFOLD":
         total_weights_delta, total_c_delta_para = raw_grad_list[0][1], raw_grad_list[0][2]
+        w_c = 1 / args.client_num_in_total
         for k in list(total_weights_delta.keys()):
-            # :110,113: at i == 0 the key is bound to client 0's own c_delta
-            # tensor, then `+=` adds every other client's into it in place
-            if K > 1:
-                c0 = total_c_delta_para[k]
-                res = seqsum([c0] + [raw_grad_list[i][2][k] for i in range(1, K)])
-                if c0.dtype == torch.bfloat16:
-                    c0.view(torch.int16).copy_(torch.from_numpy(res.view(np.int16)).reshape(c0.shape))
+            for i in range(K):
+                local_sample_number, weights_delta, c_delta_para = raw_grad_list[i]
+                w = local_sample_number / training_num
+                if i == 0:
+                    total_weights_delta[k] = scale(weights_delta[k], w)
+                    total_c_delta_para[k] = c_delta_para[k]  # bound, then `+=` in place (:110,113)
                 else:
-                    c0.copy_(torch.from_numpy(np.ascontiguousarray(res)).reshape(c0.shape))
-            # The weighted sums of :106-115 are computed and then discarded by
-            # :116-117; only the last client's tensors survive.
-            _, weights_delta, c_delta_para = raw_grad_list[K - 1]
-            w_c = 1 / args.client_num_in_total
+                    total_weights_delta[k] = add(total_weights_delta[k], scale(weights_delta[k], w))
+                    _set_inplace(total_c_delta_para[k], add(total_c_delta_para[k], c_delta_para[k]))
+            # :116-117 overwrite both with the LAST client's entries (which are
+            # the running sums themselves when that client's dicts are client 0's)
             total_weights_delta[k] = weights_delta[k]
-            total_c_delta_para[k] = wsum([c_delta_para[k]], [w_c])
+            total_c_delta_para[k] = scale(c_delta_para[k], w_c)
         return (total_weights_delta, total_c_delta_para)
     if opt == "Mime":
         avg_params, avg_local_grad = raw_grad_list[0][1], raw_grad_list[0][2]
         assert args.client_num_per_round == K
         for k in list(avg_params.keys()):
-            ws = [raw_grad_list[i][0] / training_num for i in range(K)]
-            avg_params[k] = wsum([raw_grad_list[i][1][k] for i in range(K)], ws)
-            avg_local_grad[k] = wsum([raw_grad_list[i][2][k] for i in range(K)], ws)
+            for i in range(K):
+                local_sample_number, local_model_params, local_grad = raw_grad_list[i]
+                w = local_sample_number / training_num
+                if i == 0:
+                    avg_params[k] = scale(local_model_params[k], w)
+                    avg_local_grad[k] = scale(local_grad[k], w)
+                else:
+                    avg_params[k] = add(avg_params[k], scale(local_model_params[k], w))
+                    avg_local_grad[k] = add(avg_local_grad[k], scale(local_grad[k], w))
         return (avg_params, avg_local_grad)
     # FedOpt, FedNova (`pass`) and unknown names leave avg_params unbound.
     raise UnboundLocalError("local variable 'avg_params' referenced before assignment")

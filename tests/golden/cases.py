@@ -203,7 +203,69 @@ def build_inputs(spec: Dict[str, Any]):
     if spec.get("drop_key"):
         idx, key = spec["drop_key"]
         del raw[idx][1][key]
+    return _apply_alias(spec, raw)
+
+
+def _apply_alias(spec, raw):
+    """spec["alias"]: [[j, how], ...] puts client 0's OWN dict object(s) at
+    position j ("first": its model dict, "second": its second dict, "both",
+    "swap": the two crossed); spec["tensor_alias"]: [[j, key], ...] puts client
+    0's tensor object under `key` into client j's dict.  The sample counts
+    stay client j's."""
+    for j, how in spec.get("alias", []):
+        item = raw[j]
+        first, second = raw[0][1], (raw[0][2] if len(raw[0]) > 2 else None)
+        if how == "first":
+            raw[j] = (item[0], first) + tuple(item[2:])
+        elif how == "second":
+            raw[j] = (item[0], item[1], second)
+        elif how == "both":
+            raw[j] = (item[0], first) + ((second,) if second is not None else ())
+        elif how == "swap":
+            raw[j] = (item[0], second, first)
+        else:
+            raise ValueError(how)
+    for j, key in spec.get("tensor_alias", []):
+        raw[j][1][key] = raw[0][1][key]
     return raw
+
+
+# The same dict object listed several times (agg_operator.py:36-44): client 0's
+# dict is the accumulator, so a later entry that IS that dict reads the running
+# (partially reduced) tensors, not the originals.  FedAvg_seq / FedDyn add into
+# client 0's own tensors in place (:58-63), so an entry sharing those TENSORS
+# (same dict or not) reads the running sum too.
+ALIAS_CASES: List[Dict[str, Any]] = []
+
+
+def _alias(name, optimizer, K, keys, seed, **kw):
+    ALIAS_CASES.append(dict(name=name, optimizer=optimizer, K=K, keys=keys, seed=seed, **kw))
+
+
+_alias("alias_fedavg_k3_x2", "FedAvg", 3, RAGGED_F32[:4], 400, alias=[[1, "first"]])
+_alias("alias_fedavg_k6_x3", "FedAvg", 6, RESNET_MINI, 401, alias=[[2, "first"], [5, "first"]])
+_alias("alias_fedavg_k4_last", "FedAvg", 4, RAGGED_F32, 402, alias=[[3, "first"]],
+       sample_nums=[3, 1, 4, 1.5])
+_alias("alias_fedavg_bf16_k5_x3", "FedAvg", 5, RAGGED_BF16, 403, alias=[[1, "first"], [2, "first"]])
+_alias("alias_fedavg_mixed_k4", "FedAvg", 4, [["w", [513], F32], ["h", [257], BF16], ["d", [33], F64],
+                                              ["n", [3], I64], ["m", [65], F16]], 404, alias=[[2, "first"]])
+_alias("alias_fedprox_k5_x2", "FedProx", 5, RESNET_MINI, 405, alias=[[3, "first"]])
+_alias("alias_mime_k4_both", "Mime", 4, RAGGED_F32[:4], 406, client_num_per_round=4, triple=True,
+       alias=[[2, "both"]])
+_alias("alias_mime_k4_split", "Mime", 4, RAGGED_F32[:4], 407, client_num_per_round=4, triple=True,
+       alias=[[1, "first"], [3, "second"]])
+_alias("alias_mime_k3_swap", "Mime", 3, RAGGED_F32[:4], 408, client_num_per_round=3, triple=True,
+       alias=[[1, "swap"]])
+_alias("alias_fedavg_seq_k4_x2", "FedAvg_seq", 4, [["w", [1001], F32], ["n", [2], I64], ["h", [300], BF16]], 409,
+       alias=[[2, "first"]])
+_alias("alias_fedavg_seq_k5_tensor", "FedAvg_seq", 5, [["w", [1001], F32], ["n", [2], I64], ["h", [300], BF16]],
+       410, alias=[[1, "first"]], tensor_alias=[[3, "w"], [4, "h"]])
+_alias("alias_feddyn_k4_x3", "FedDyn", 4, [["w", [513], F32], ["n", [], I64]], 411,
+       alias=[[1, "first"], [3, "first"]])
+_alias("alias_scaffold_k3_last", "SCAFFOLD", 3, RAGGED_F32[:4], 412, client_num_in_total=10, triple=True,
+       alias=[[2, "both"]])
+_alias("alias_scaffold_k4_mid", "SCAFFOLD", 4, RAGGED_F32[:4], 413, client_num_in_total=10, triple=True,
+       alias=[[2, "both"]])
 
 
 class Args:

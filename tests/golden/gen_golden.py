@@ -377,7 +377,7 @@ def main(only=()):
         return not only or any(spec["name"].startswith(p) for p in only)
 
     FedMLAggOperator, FedOptAggregator = import_reference()
-    for spec in filter(want, cases.CASES):
+    for spec in filter(want, cases.CASES + cases.ALIAS_CASES):
         run_agg_case(FedMLAggOperator, spec)
         print("wrote", spec["name"])
     for spec in filter(want, cases.FEDOPT_CASES):

@@ -33,6 +33,24 @@ def _to_device(raw, dev):
     return out
 
 
+def _to_device_aliased(raw, dev):
+    """_to_device keeping the round's aliasing: a dict (or tensor) object that
+    appears several times on the host appears as ONE device object."""
+    memo = {}
+
+    def dmove(d):
+        if id(d) not in memo:
+            memo[id(d)] = OrderedDict((k, tmove(t)) for k, t in d.items())
+        return memo[id(d)]
+
+    def tmove(t):
+        if id(t) not in memo:
+            memo[id(t)] = t.to(dev)
+        return memo[id(t)]
+
+    return [(item[0],) + tuple(dmove(d) for d in item[1:]) for item in raw]
+
+
 def _cpu(res):
     if isinstance(res, tuple):
         return tuple(_cpu(r) for r in res)
@@ -87,6 +105,59 @@ def test_device_inputs_match_reference(name, cuda_device):
         assert t.is_cuda
     gu.assert_groups(_cpu(res), meta, arrays, name)
     gu.assert_third_mutation(third, meta, arrays, name)
+
+
+ALIAS_CASES = [c["name"] for c in cases.ALIAS_CASES]
+
+
+@pytest.mark.parametrize("name", ALIAS_CASES)
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_alias_rounds_match_reference(name, where, cuda_device):
+    """A dict (or, for FedAvg_seq, a tensor) of client 0 listed again reads the
+    running accumulator in the reference (agg_operator.py:36-44,55-63,121-133);
+    the GPU path reproduces it bit for bit, outputs and in-place side effects."""
+    meta, arrays = gu.load(name)
+    spec = meta["spec"]
+    raw = cases.build_inputs(spec)
+    if where == "device":
+        raw = _to_device_aliased(raw, cuda_device)
+    client0, objs = raw[0][1], dict(raw[0][1])
+    before = {k: t.clone() for k, t in objs.items()}
+    third = gu.snapshot_third(raw)
+    res = ao.FedMLAggOperator.agg(cases.Args(spec), raw)
+    gu.assert_groups(_cpu(res), meta, arrays, name)
+    gu.assert_third_mutation(third, meta, arrays, name)
+    first = res[0] if isinstance(res, tuple) else res
+    assert (first is client0) == meta["result_is_client0_dict"]
+    for t in first.values():
+        assert t.device.type == ("cuda" if where == "device" else "cpu")
+    for k, t in objs.items():
+        if t.is_floating_point() and torch.isnan(t).any():
+            continue
+        assert (not torch.equal(t, before[k])) == (k in meta["client0_tensors_mutated"]), k
+
+
+def test_alias_known_answer(cuda_device):
+    """[(1, d), (1, d), (2, e)], d = [1, 2], e = [3, 4]: [1.8125, 2.625] as the
+    reference computes it here (not the naive mean [2.0, 3.0])."""
+    class A:
+        federated_optimizer = "FedAvg"
+
+    for dev in ("cpu", cuda_device):
+        d = OrderedDict(x=torch.tensor([1.0, 2.0], device=dev))
+        e = OrderedDict(x=torch.tensor([3.0, 4.0], device=dev))
+        res = ao.FedMLAggOperator.agg(A(), [(1, d), (1, d), (2, e)])
+        assert res is d and res["x"].cpu().tolist() == [1.8125, 2.625]
+
+
+def test_alias_partial_overlap_is_refused(cuda_device):
+    class A:
+        federated_optimizer = "FedAvg_seq"
+
+    buf = torch.arange(8, dtype=torch.float32, device=cuda_device)
+    raw = [(1, OrderedDict(x=buf[0:4])), (1, OrderedDict(x=buf[2:6]))]
+    with pytest.raises(NotImplementedError):
+        ao.FedMLAggOperator.agg(A(), raw)
 
 
 @pytest.mark.parametrize("name", [c["name"] for c in cases.CASES
