@@ -42,6 +42,7 @@ SIGNATURES = {
     "fedagg_wsum_f64": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _U32, _P]),
     "fedagg_wsum_i64_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _U32, _P]),
     "fedagg_sum": (ctypes.c_int, [_I32, _P, _I32, _I64, _P, _U32, _P]),
+    "fedagg_wsum_muldiv": (ctypes.c_int, [_I32, _P, _P, _I32, _I64, _P, _U32, _P]),
     "fedagg_multi_blocks": (_I64, [_I32, _I64]),
     "fedagg_wsum_multi_f32": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _I32, _I64, _P]),
     "fedagg_wsum_multi": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P, _I32, _P, _I32, _I64, _P]),

@@ -345,6 +345,7 @@ def _reduce_host_batched(w, dicts, keys, weights, args, acc_mode) -> "OrderedDic
     devices = _round_devices(args, layout, K, device, acc_mode)
     if len(devices) > 1:
         return _reduce_host_multi(layout, devices, tables, numels, codes, dicts, weights, acc_mode)
+    device = devices[0]  # args.fedagg_devices may name the one device
     with torch.cuda.device(device):
         bucket = _cached_bucket(layout, K, device, _ACC_NAME[acc_mode])
         if K * sum(n * _ROW_ESZ[c] for n, c in zip(numels, codes)) <= _BATCH_MAX_BYTES:
@@ -365,13 +366,19 @@ def _round_devices(args, layout, K: int, device: torch.device, acc_mode) -> list
     again would not count that bucket's own rows as free, so a round that fit
     one GPU in round 1 could flip to several GPUs in round 2 and hold its rows
     twice (the cached one-device bucket plus the new shards)."""
-    if not _multi_requested(args):
-        lk = tuple((k, s, str(d)) for k, s, d in layout)
+    listed = multidev.parse_devices(getattr(args, "fedagg_devices", None))
+    lk = tuple((k, s, str(d)) for k, s, d in layout)
+    if not listed:
         if (lk, K, str(device), _ACC_NAME[acc_mode]) in _BUCKETS:
             return [device]
         for key in _MULTI:
             if key[0] == lk and key[1] == K and key[3] == acc_mode:
                 return [torch.device(d) for d in key[2]]
+    elif len(listed) == 1:
+        # one device named explicitly: honour it, and drop a multi-device
+        # bucket of this layout so its rows do not stay resident beside it
+        for key in [k for k in _MULTI if k[0] == lk]:
+            del _MULTI[key]
     devices = multidev.devices_for_round(args, layout, K, device)
     if len(devices) > 1:
         # the round goes multi-device: a one-device bucket of the same layout
@@ -427,7 +434,7 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
         dicts, keys = list(dicts), list(keys)
         t0 = dicts[0].get(keys[0]) if isinstance(dicts[0], dict) else None
         if isinstance(t0, torch.Tensor) and not t0.is_cuda and getattr(args, "fedagg_device", None) is None \
-                and torch.cuda.is_available() and not _multi_requested(args):
+                and torch.cuda.is_available() and not multidev.parse_devices(getattr(args, "fedagg_devices", None)):
             res = _reduce_host_round(w, dicts, keys, weights)
             if res is not None:
                 return res
@@ -454,6 +461,7 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
                 bucket.put(i, {k: per_key[k][i] for k in host_keys}, 1)
             results.update(bucket.reduce_to_host(weights))
         else:
+            device = devices[0]
             with torch.cuda.device(device):
                 bucket = _cached_bucket(layout, K, device, _ACC_NAME[acc_mode])
                 for i in range(K):
@@ -499,6 +507,64 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
                     plan = kn.MultiPlan([results[k].numel() for k in mk], dt, acc_mode)
                     plan.launch(ms, mo, w32, K, device)
 
+    return OrderedDict((k, results[k]) for k in keys)
+
+
+_MULDIV_INT_OK = (torch.int64, torch.bool)
+
+
+def muldiv_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], pairs: Sequence, args
+                  ) -> "OrderedDict[str, torch.Tensor]":
+    """avg[k] = Σ_i fl(fl(p_i[k]·n_i) / N) in client order for every key, with
+    pairs[i] = (n_i, N): the MPI simulation's term order
+    (simulation/mpi/fedavg/FedAVGAggregator.py:99-116).  Host keys are staged
+    into exact rows (integer keys as int64: `int64 * int` multiplies in int64
+    first), device keys are read in place; one fedagg_wsum_muldiv launch per
+    dtype group or device key.  Results live where the inputs did."""
+    per_key = _gather(dicts, keys)
+    K = len(dicts)
+    for k in keys:
+        dt = per_key[k][0].dtype
+        if dt in _INT_TO_I64 and dt not in _MULDIV_INT_OK:
+            raise NotImplementedError(f"key {k!r}: {dt} * int wraps at {dt}'s width in torch; "
+                                      "fedml_amd's MPI-order path takes int64 / bool integer keys")
+    results: Dict[str, torch.Tensor] = {}
+    keep = []
+    host_keys = [k for k in keys if not per_key[k][0].is_cuda]
+    if host_keys:
+        device = _host_device(args)
+        with torch.cuda.device(device):
+            layout = [(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in host_keys]
+            bucket = ClientBucket(layout, K, device, promote_ints=False)
+            for i in range(K):
+                bucket.put(i, {k: per_key[k][i] for k in host_keys}, 1)
+            bucket.sync_ingest()
+            outs = {}
+            for dt, g in bucket.groups.items():
+                odt = torch.float32 if dt == torch.int64 else dt
+                outs[dt] = torch.empty(max(g.length, 1), dtype=odt, device=device)
+                if g.length:
+                    keep.append(kn.muldiv_ptrs(dt, g.d_ptrs, pairs, K, g.length, outs[dt], True))
+            host = {dt: o.cpu() for dt, o in outs.items()}
+            for k in host_keys:
+                g, j = bucket.where[k]
+                results[k] = host[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].view(g.shapes[j]).clone()
+    for k in keys:
+        if k in results:
+            continue
+        ts = [t if t.is_contiguous() else t.contiguous() for t in per_key[k]]
+        if ts[0].dtype == torch.bool:
+            ts = [t.to(torch.int64) for t in ts]
+        dt = ts[0].dtype
+        device = ts[0].device
+        with torch.cuda.device(device):
+            out = torch.empty(ts[0].shape, dtype=torch.float32 if dt == torch.int64 else dt, device=device)
+            if out.numel():
+                ptrs = [t.data_ptr() for t in ts]
+                keep.append((ts, kn.muldiv_ptrs(dt, kn.upload_i64(ptrs, device), pairs, K, out.numel(), out,
+                                                kn.aligned16(ptrs))))
+        results[k] = out
+    del keep  # stream-ordered: the caching allocator reuses these only after the launches
     return OrderedDict((k, results[k]) for k in keys)
 
 
@@ -636,7 +702,7 @@ def _reads_running_cell(raw_grad_list, roles: Sequence[int]) -> bool:
     return False
 
 
-def _reduce_chain(chain, keys: Sequence[str], args) -> "OrderedDict[str, torch.Tensor]":
+def _reduce_chain(chain, keys: Sequence[str], args, reduce=None) -> "OrderedDict[str, torch.Tensor]":
     """One weighted chain over (dict, weight) sources.  A running value of an
     integer key is float32 (torch promotes `int * w`), so where a chain mixes
     it with original integer tensors those go in as fl32(v), which is what the
@@ -651,16 +717,19 @@ def _reduce_chain(chain, keys: Sequence[str], args) -> "OrderedDict[str, torch.T
     if mixed:
         dicts = [OrderedDict((k, d[k].to(torch.float32) if k in mixed and not d[k].is_floating_point() else d[k])
                              for k in keys) for d in dicts]
-    return weighted_reduce(dicts, keys, ws, args)
+    return (reduce or weighted_reduce)(dicts, keys, ws, args)
 
 
-def _run_cells(raw_grad_list, roles: Sequence[int], keys: Sequence[str], weights: Sequence[float], args) -> None:
+def _run_cells(raw_grad_list, roles: Sequence[int], keys: Sequence[str], weights: Sequence, args, reduce=None,
+               one=1.0) -> None:
     """The reference's FedAvg / FedProx / Mime loop with its aliasing: cells
     are the accumulated dicts (client 0's), each step `cell = src * w`
     (i == 0) or `cell += src * w`, src read at that moment (a cell's running
     value if src is a cell already written).  Pending steps of a cell batch
     into one weighted reduction until another step reads it; the final values
-    are bound into the cell dicts."""
+    are bound into the cell dicts.  reduce / one: the chain's reduction and
+    the weight that passes a running value through unchanged (muldiv_reduce
+    with (1, 1) for the MPI simulation's order)."""
     cells: List[object] = []
     for r in roles:
         if _is_in(raw_grad_list[0][r], cells) < 0:
@@ -672,9 +741,9 @@ def _run_cells(raw_grad_list, roles: Sequence[int], keys: Sequence[str], weights
     def flush(c: int) -> None:
         ch = chain[c]
         chain[c] = None
-        if ch is None or (len(ch) == 1 and ch[0][0] is value[c] and ch[0][1] == 1.0):
+        if ch is None or (len(ch) == 1 and ch[0][0] is value[c] and ch[0][1] == one):
             return
-        value[c] = _reduce_chain(ch, keys, args)
+        value[c] = _reduce_chain(ch, keys, args, reduce)
 
     for i in range(len(raw_grad_list)):
         w = weights[i]
@@ -689,7 +758,7 @@ def _run_cells(raw_grad_list, roles: Sequence[int], keys: Sequence[str], weights
                 chain[tc] = [(src, w)]
             else:
                 if chain[tc] is None:
-                    chain[tc] = [(value[tc], 1.0)]
+                    chain[tc] = [(value[tc], one)]
                 chain[tc].append((src, w))
             written[tc] = True
     for c in range(len(cells)):

@@ -43,6 +43,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <pthread.h>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -185,6 +186,63 @@ struct OpI64F32 {  // int64 buffers (BN num_batches_tracked) promote to float32
 };
 
 // Unweighted sums (FedAvg_seq / FedDyn), source dtype preserved.
+// MPI simulation FedAvg (simulation/mpi/fedavg/FedAVGAggregator.py:99-116):
+// `local_model_params[k] * local_sample_number / training_num` is evaluated
+// left to right, so every client's term is fl(fl(p * n_i) / N): two roundings
+// (a correctly rounded division; hipcc's default) instead of the plugin
+// path's fl(p * fl(n_i / N)).  The weight of client i carries (n_i, N) as the
+// tensor's opmath type rounds them.
+struct MulDivF { float n, d; };
+struct MulDivD { double n, d; };
+// int64 rows: an integral n_i multiplies in int64 (two's-complement wrap, as
+// torch's int64 * int), then true division promotes to float32; a float n_i
+// promotes first: fl32(fl32(v) * fl32(n_i)).
+struct MulDivI { int64_t n; float nf, d; int32_t is_int, pad; };
+
+struct OpF32MulDiv {
+  using in_t = float; using out_t = float; using acc_t = float; using w_t = MulDivF;
+  static __device__ __forceinline__ float term(in_t x, w_t w) { return fp32_materialise(x * w.n) / w.d; }
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return term(x, w); }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return a + term(x, w); }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return a; }
+};
+struct OpBF16MulDiv {  // torch CPU chain: bf16 after the mul, the div and the add
+  using in_t = uint16_t; using out_t = uint16_t; using acc_t = float; using w_t = MulDivF;
+  static __device__ __forceinline__ float r(float f) { return bf16_round(f); }
+  static __device__ __forceinline__ float term(in_t x, w_t w) { return r(r(bf16_to_f32(x) * w.n) / w.d); }
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return term(x, w); }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return r(a + term(x, w)); }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return f32_to_bf16(a); }
+};
+struct OpF16MulDiv {  // fp32 results rounded to f16 after every op (products kept in fp32 first)
+  using in_t = uint16_t; using out_t = uint16_t; using acc_t = float; using w_t = MulDivF;
+  static __device__ __forceinline__ float r(float f) { return f16_to_f32(f32_to_f16(f)); }
+  static __device__ __forceinline__ float term(in_t x, w_t w) {
+    return r(fp32_materialise(r(fp32_materialise(f16_to_f32(x) * w.n)) / w.d));
+  }
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return term(x, w); }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return r(a + term(x, w)); }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return f32_to_f16(a); }
+};
+struct OpF64MulDiv {
+  using in_t = double; using out_t = double; using acc_t = double; using w_t = MulDivD;
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return (x * w.n) / w.d; }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return a + (x * w.n) / w.d; }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return a; }
+};
+struct OpI64MulDiv {
+  using in_t = int64_t; using out_t = float; using acc_t = float; using w_t = MulDivI;
+  static __device__ __forceinline__ float term(in_t x, w_t w) {
+    const float v = w.is_int ? static_cast<float>(static_cast<int64_t>(static_cast<uint64_t>(x) *
+                                                                      static_cast<uint64_t>(w.n)))
+                             : fp32_materialise(static_cast<float>(x) * w.nf);
+    return v / w.d;
+  }
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return term(x, w); }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return a + term(x, w); }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return a; }
+};
+
 struct OpSumF32 {
   using in_t = float; using out_t = float; using acc_t = float; using w_t = float;
   static __device__ __forceinline__ acc_t first(in_t x, w_t) { return x; }
@@ -317,7 +375,7 @@ __device__ __forceinline__ void store_pack(T* p, const T (&v)[E]) {
 template <class T>
 struct PtrW {
   const T* p;
-  __device__ __forceinline__ T operator[](int i) const { return p ? p[i] : T(0); }
+  __device__ __forceinline__ T operator[](int i) const { return p ? p[i] : T{}; }
 };
 template <class T>
 struct ConstW {  // one value for every client (the field prime of the mod-p sum)
@@ -1223,11 +1281,31 @@ namespace {
 // parts, work on it themselves, and idle workers join in; a batch leaves the
 // queue when its parts are all claimed, and its caller returns once every
 // part has run and no worker still holds it.
+//
+// Fork: the workers do not exist in a child process and the pool's mutex may
+// have been held by one of them at the fork, so a pthread_atfork child
+// handler drops the pool (leaked, never touched again) and the child's first
+// pack builds its own.
 class PackPool {
  public:
   static PackPool& get() {
-    static PackPool* p = new PackPool(15);  // + the caller: 16, the GPU box's CPU share
-    return *p;
+    for (;;) {
+      PackPool* p = pool_.load(std::memory_order_acquire);
+      if (p) return *p;
+      int idle = 0;
+      if (creating_.compare_exchange_strong(idle, 1)) {
+        static const int registered = pthread_atfork(nullptr, nullptr, [] {
+          pool_.store(nullptr);
+          creating_.store(0);
+        });
+        (void)registered;
+        p = new PackPool(15);  // + the caller: 16, the GPU box's CPU share
+        pool_.store(p, std::memory_order_release);
+        creating_.store(0);
+        return *p;
+      }
+      std::this_thread::yield();
+    }
   }
   void run(int parts, const std::function<void(int)>& fn) {
     if (parts <= 1) {
@@ -1288,7 +1366,11 @@ class PackPool {
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<Batch*> q_;
+  static std::atomic<PackPool*> pool_;
+  static std::atomic<int> creating_;
 };
+std::atomic<PackPool*> PackPool::pool_{nullptr};
+std::atomic<int> PackPool::creating_{0};
 
 // Parallel copy of n byte ranges: range i goes from src_base[i] to dst_base[i]
 // (nbytes[i] bytes).  The total is cut into `threads` contiguous slices, run
@@ -1638,6 +1720,31 @@ int fedagg_sum(int32_t dtype, const void* const* d_src, int32_t K, int64_t N, vo
     case FEDAGG_DT_I64: return launch<OpSumI64>(d_src, nullptr, K, N, d_out, flags, stream, "fedagg_sum", false);
     case FEDAGG_DT_I32: return launch<OpSumI32>(d_src, nullptr, K, N, d_out, flags, stream, "fedagg_sum", false);
     default: return set_error(FEDAGG_EINVAL, "fedagg_sum: unsupported dtype");
+  }
+}
+
+int fedagg_wsum_muldiv(int32_t dtype, const void* const* d_src, const void* d_w, int32_t K, int64_t N, void* d_out,
+                       uint32_t flags, fedagg_stream_t stream) {
+  const char* name = "fedagg_wsum_muldiv";
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, std::string(name) + ": K must be >= 1 and N >= 0");
+  if (!d_src || !d_out || !d_w) return set_error(FEDAGG_EINVAL, std::string(name) + ": null pointer");
+  if (flags & FEDAGG_HOST_WEIGHTS) return set_error(FEDAGG_EINVAL, std::string(name) + ": device weights only");
+  if (N == 0) return FEDAGG_OK;
+  const bool al = (flags & FEDAGG_ALIGNED16) != 0;
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  auto go = [&](auto op) {
+    using OP = decltype(op);
+    Seg<OP> seg{reinterpret_cast<const typename OP::in_t* const*>(d_src), N};
+    return launch_epi<OP>(seg, StoreEpi<OP>{reinterpret_cast<typename OP::out_t*>(d_out)},
+                          PtrW<typename OP::w_t>{reinterpret_cast<const typename OP::w_t*>(d_w)}, K, al, st, name);
+  };
+  switch (dtype) {
+    case FEDAGG_DT_F32: return go(OpF32MulDiv{});
+    case FEDAGG_DT_BF16: return go(OpBF16MulDiv{});
+    case FEDAGG_DT_F16: return go(OpF16MulDiv{});
+    case FEDAGG_DT_F64: return go(OpF64MulDiv{});
+    case FEDAGG_DT_I64: return go(OpI64MulDiv{});
+    default: return set_error(FEDAGG_EINVAL, std::string(name) + ": unsupported dtype");
   }
 }
 

@@ -1817,7 +1817,10 @@ __global__ __launch_bounds__(256) void gram_dist_kernel(const double* __restrict
   // different MFMA order (h_i m_j before m_i h_j), so they may differ in the
   // last bits; the sum keeps D exactly symmetric (= 2 M_ij when M is)
   const double d = (M[int64_t(i) * K + i] + M[int64_t(j) * K + j]) - (M[e] + M[int64_t(j) * K + i]);
-  D[e] = i == j ? 0.0 : (d > 0.0 ? d : 0.0);
+  // negative rounding residue clamps to 0; NaN and inf pass through, so a
+  // non-finite client (inf elements, or squares beyond fp32) reaches
+  // gram_condition and sends "auto" to the exact kernel
+  D[e] = i == j ? 0.0 : (d < 0.0 ? 0.0 : d);
 }
 
 // ---------------------------------------------------------------------------

@@ -257,12 +257,17 @@ def gram_condition(D: np.ndarray) -> float:
     centred Gram's rounding error (~1e-7 (|c_i|^2 + |c_j|^2) per entry) exceeds
     a relative error of D_ij itself.  The centred norms come from D alone
     (double centring of a squared-distance matrix: |c_i|^2 = mean_j D_ij -
-    sum D / (2 K^2)).  inf when two distinct clients are at distance 0."""
+    sum D / (2 K^2)).  inf when two distinct clients are at distance 0, or when any distance
+    or centred norm is not finite (an inf client, squares beyond fp32)."""
     K = D.shape[0]
     if K < 2:
         return 0.0
     D = np.asarray(D, dtype=np.float64)
+    if not np.all(np.isfinite(D)):  # an inf / NaN client, or squares beyond fp32: only the exact kernel copes
+        return float("inf")
     c2 = np.maximum(D.sum(axis=1) / K - D.sum() / (2.0 * K * K), 0.0)
+    if not np.all(np.isfinite(c2)):
+        return float("inf")
     num = c2[:, None] + c2[None, :]
     off = ~np.eye(K, dtype=bool)
     d, s = D[off], num[off]
@@ -270,7 +275,8 @@ def gram_condition(D: np.ndarray) -> float:
         return float("inf")
     with np.errstate(invalid="ignore", divide="ignore"):
         r = np.where(d > 0, s / np.where(d > 0, d, 1.0), 0.0)
-    return float(r.max())
+    m = float(r.max())
+    return m if np.isfinite(m) else float("inf")
 
 
 def pairdist2_rows(d_ptrs: torch.Tensor, K: int, chunks: torch.Tensor, n_chunks: int, device,

@@ -309,8 +309,16 @@ class MultiDeviceFedOptServer:
     FedOptServer over its keys: its own client rows, global vector and
     optimizer state, its own fused FedAvg + server-step launches.  Every
     element's FedAvg chain and optimizer step are the one-device ones, so the
-    result is bit-exact with FedOptServer, and nothing is exchanged.  Same
-    interface as FedOptServer."""
+    result is bit-exact with FedOptServer, and nothing is exchanged.
+
+    It offers FedOptServer's round interface (add_local_trained_result,
+    check_whether_all_receive, aggregate, get_global_model_params,
+    optimizer_state / load_optimizer_state, sample_num_dict, step_count) and
+    its scalar settings (optimizer, lr, momentum, ...).  Where FedOptServer
+    has ONE bucket and device, this has one per shard: ``buckets`` and
+    ``devices`` (``device`` / ``bucket`` name the first shard's, for code that
+    only needs a device to allocate on).  Built by ``make_fedopt_server`` when
+    ``args.fedagg_devices`` lists several GPUs or the round does not fit one."""
 
     def __init__(self, global_state: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],
                  worker_num: int, server_optimizer: str = "sgd", server_lr: float = 1.0,
@@ -332,7 +340,12 @@ class MultiDeviceFedOptServer:
                                              server_optimizer, server_lr, server_momentum, dev, server_weight_decay))
         self.owner = {k: i for i, s in enumerate(self.servers) for k, _, _ in s.bucket.entries}
         self.worker_num = worker_num
-        self.optimizer = self.servers[0].optimizer
+        first = self.servers[0]
+        self.optimizer = first.optimizer
+        for a in ("lr", "momentum", "betas", "eps", "alpha", "weight_decay", "lr_decay"):
+            setattr(self, a, getattr(first, a))
+        self.buckets = [s.bucket for s in self.servers]
+        self.bucket, self.device = first.bucket, first.device
         self.param_names = list(param_names)
         self.sample_num_dict = _SharedDict(self.servers, "sample_num_dict")
         self.flag_client_model_uploaded_dict = {i: False for i in range(worker_num)}

@@ -130,6 +130,70 @@ def wsum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, d_w: torch.Tensor, K: in
     nat.check(rc, f"wsum[{dtype}]")
 
 
+_MULDIV_F = np.dtype([("n", "<f4"), ("d", "<f4")])
+_MULDIV_D = np.dtype([("n", "<f8"), ("d", "<f8")])
+_MULDIV_I = np.dtype([("n", "<i8"), ("nf", "<f4"), ("d", "<f4"), ("is_int", "<i4"), ("pad", "<i4")])
+
+
+def _is_int(v) -> bool:
+    import numbers
+
+    return isinstance(v, numbers.Integral)
+
+
+def scalar_f32(v) -> float:
+    """The float32 torch's CPU kernels use for a Python scalar next to an fp32
+    (or bf16 / f16: opmath float) tensor: an int converts int64 -> float
+    with one round-to-nearest-even, a float double -> float."""
+    if _is_int(v):
+        return float(torch.tensor(int(v), dtype=torch.int64).to(torch.float32).item())
+    return float(np.float32(float(v)))
+
+
+def muldiv_weights(dtype: torch.dtype, pairs: Sequence, device: torch.device) -> torch.Tensor:
+    """fedagg_wsum_muldiv's K weight records for (n_i, N) pairs, uploaded as
+    bytes: {fl32(n_i), fl32(N)} for fp32 / bf16 / f16 rows, doubles for f64,
+    {n_i, fl32(n_i), fl32(N), is_int} for int64 rows (include/fedagg.h)."""
+    K = len(pairs)
+    if dtype == torch.float64:
+        rec = np.zeros(K, dtype=_MULDIV_D)
+        rec["n"] = [float(n) for n, _ in pairs]
+        rec["d"] = [float(d) for _, d in pairs]
+    elif dtype == torch.int64:
+        rec = np.zeros(K, dtype=_MULDIV_I)
+        rec["is_int"] = [1 if _is_int(n) else 0 for n, _ in pairs]
+        rec["n"] = [int(n) if _is_int(n) else 0 for n, _ in pairs]
+        rec["nf"] = [scalar_f32(n) for n, _ in pairs]
+        rec["d"] = [scalar_f32(d) for _, d in pairs]
+    else:
+        rec = np.zeros(K, dtype=_MULDIV_F)
+        rec["n"] = [scalar_f32(n) for n, _ in pairs]
+        rec["d"] = [scalar_f32(d) for _, d in pairs]
+    raw = np.frombuffer(rec.tobytes(), dtype=np.uint8)
+    host = torch.from_numpy(raw.copy())
+    if torch.cuda.is_available():
+        host = host.pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def muldiv_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, pairs: Sequence, K: int, N: int, out: torch.Tensor,
+                aligned: bool) -> torch.Tensor:
+    """fedagg_wsum_muldiv: out = Σ_i fl(fl(p_i·n_i)/N) over a device pointer
+    table (the MPI simulation's term order).  Returns the uploaded weight
+    records (keep them alive until the launch has run)."""
+    _require_cuda(out, "muldiv")
+    if dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64):
+        raise TypeError(f"muldiv: unsupported dtype {dtype}")
+    want = torch.float32 if dtype == torch.int64 else dtype
+    if out.dtype != want:
+        raise TypeError(f"muldiv: {dtype} rows produce {want}")
+    w = muldiv_weights(dtype, pairs, out.device)
+    flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0
+    nat.check(nat.lib().fedagg_wsum_muldiv(_DT_CODE[dtype], d_ptrs.data_ptr(), w.data_ptr(), K, N, out.data_ptr(),
+                                           flags, nat.stream_handle()), f"muldiv[{dtype}]")
+    return w
+
+
 def sum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor, aligned: bool) -> None:
     """Unweighted sequential sum (FedAvg_seq / FedDyn)."""
     _require_cuda(out, "sum")

@@ -11,12 +11,21 @@ and runs the reduction in libfedagg.so through fedml_amd.agg_operator.
 A simulator swaps the method in one line:
 
     FedAvgAPI._aggregate = lambda self, w_locals: fedavg_aggregate(w_locals)
+
+The MPI simulator's FedAVGAggregator._fedavg_aggregation_
+(simulation/mpi/fedavg/FedAVGAggregator.py:99-116) writes each term as
+``local_model_params[k] * local_sample_number / training_num``: two roundings
+per client, fl(fl(p·n_i)/N), in a different order from the plugin path's
+fl(p·fl(n_i/N)).  ``fedavg_mpi_aggregate`` reproduces that order bit for bit
+(fedagg_wsum_muldiv):
+
+    FedAVGAggregator._fedavg_aggregation_ = lambda self, model_list: fedavg_mpi_aggregate(model_list)
 """
 from __future__ import annotations
 
 from typing import List, Tuple
 
-from .agg_operator import weighted_reduce
+from .agg_operator import _reads_running_cell, _run_cells, muldiv_reduce, weighted_reduce
 
 
 class _Defaults:
@@ -40,6 +49,31 @@ def fedavg_aggregate(w_locals: List[Tuple[float, "OrderedDict"]], args=None) -> 
     weights = [w_locals[i][0] / training_num for i in range(len(w_locals))]
     res = weighted_reduce([w_locals[i][1] for i in range(len(w_locals))], keys, weights,
                           args if args is not None else _Defaults())
+    for k in keys:
+        averaged_params[k] = res[k]
+    return averaged_params
+
+
+def fedavg_mpi_aggregate(model_list: List[Tuple[float, "OrderedDict"]], args=None) -> "OrderedDict":
+    """FedAVGAggregator._fedavg_aggregation_ (FedAVGAggregator.py:99-116): the
+    same unpacking, Σn loop and returned object (client 0's dict, keys
+    rebound), each term fl(fl(p·n_i)/Σn).  Σn = 0 divides tensors by zero as
+    torch does (inf / NaN, no exception).  Client 0's dict listed again reads
+    the running sum, as in the reference (fedml_amd.agg_operator._run_cells)."""
+    training_num = 0
+    for i in range(0, len(model_list)):
+        local_sample_number, local_model_params = model_list[i]
+        training_num += local_sample_number
+    (num0, averaged_params) = model_list[0]
+    keys = list(averaged_params.keys())
+    if not keys:
+        return averaged_params
+    a = args if args is not None else _Defaults()
+    pairs = [(model_list[i][0], training_num) for i in range(len(model_list))]
+    if _reads_running_cell(model_list, (1,)):
+        _run_cells(model_list, (1,), keys, pairs, a, reduce=muldiv_reduce, one=(1, 1))
+        return averaged_params
+    res = muldiv_reduce([model_list[i][1] for i in range(len(model_list))], keys, pairs, a)
     for k in keys:
         averaged_params[k] = res[k]
     return averaged_params

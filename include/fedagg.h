@@ -142,6 +142,25 @@ int fedagg_wsum_multi_f32(const float* const* d_src, float* const* d_out,
                           int32_t T, const float* d_w, int32_t K,
                           int64_t total_blocks, fedagg_stream_t stream);
 
+/* ---- MPI simulation FedAvg order --------------------------------------- */
+
+/* out = sum_i fl( fl(p_i * n_i) / N ) in client order: the term order of the
+ * MPI simulation's FedAVGAggregator._fedavg_aggregation_
+ * (simulation/mpi/fedavg/FedAVGAggregator.py:99-116, `local_model_params[k] *
+ * local_sample_number / training_num`), two roundings per client where the
+ * plugin path (fedagg_wsum_*) has fl(p * fl(n_i / N)).  d_w is a DEVICE array
+ * of K weight records of the dtype's layout:
+ *   FEDAGG_DT_F32 / _BF16 / _F16: {float n, float d}    (fl32(n_i), fl32(N))
+ *   FEDAGG_DT_F64:                {double n, double d}
+ *   FEDAGG_DT_I64:                {int64 n, float nf, float d, int32 is_int, int32 pad}
+ *     (is_int: n_i is an integer and multiplies in int64 with wrap-around;
+ *      else fl32(v) * nf; the result is float32, as torch's true division)
+ * bf16 / f16 round after the mul, the div and the add (torch's CPU chain).
+ * Outputs keep the dtype (float32 for int64).  FEDAGG_HOST_WEIGHTS is refused. */
+int fedagg_wsum_muldiv(int32_t dtype, const void* const* d_src, const void* d_w,
+                       int32_t K, int64_t N, void* d_out, uint32_t flags,
+                       fedagg_stream_t stream);
+
 /* ---- FedOpt server step (fused epilogue) ------------------------------- */
 
 /* Server SGD with momentum over named parameters, fused with the pseudo

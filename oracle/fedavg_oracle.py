@@ -14,7 +14,9 @@ It restates, branch by branch, python/fedml/ml/aggregator/agg_operator.py:
                     SCAFFOLD      :100-118 (overwrites with the last client)
                     Mime          :119-133
 and the FedOpt server step of simulation/mpi/fedopt/FedOptAggregator.py:81-130
-(SGD) and of sp/fedopt/fedopt_api.py:121-130 (Adam, Adagrad).
+(SGD) and of sp/fedopt/fedopt_api.py:121-130 (Adam, Adagrad), and the MPI
+simulation's FedAvg term order (simulation/mpi/fedavg/FedAVGAggregator.py:
+99-116, mpi_fedavg).
 
 Inputs and outputs are CPU torch tensors (the reference's own currency); all
 arithmetic is numpy in the tensor's opmath type with one IEEE rounding per
@@ -276,6 +278,76 @@ def torch_aggregator(args, raw_grad_list, training_num):
         return (avg_params, avg_local_grad)
     # FedOpt, FedNova (`pass`) and unknown names leave avg_params unbound.
     raise UnboundLocalError("local variable 'avg_params' referenced before assignment")
+
+
+# --------------------------------------------------------------------------
+# MPI simulation FedAvg (simulation/mpi/fedavg/FedAVGAggregator.py:99-116)
+
+
+def _f32_scalar(v) -> np.float32:
+    """A Python scalar as torch's CPU kernels take it next to an fp32 / bf16 /
+    f16 tensor: int -> int64 -> float (one RNE), float -> double -> float."""
+    import numbers
+
+    if isinstance(v, numbers.Integral):
+        return np.float32(torch.tensor(int(v), dtype=torch.int64).to(torch.float32).item())
+    return np.float32(float(v))
+
+
+def mul_scalar(t: torch.Tensor, n) -> torch.Tensor:
+    """torch's `t * n` for a Python scalar n (FedAVGAggregator.py:108,112):
+    int64 / bool tensors times an int stay int64 (two's-complement wrap),
+    times a float promote to float32; float tensors round once in their
+    opmath type (f16: the fp32 product, then f16)."""
+    import numbers
+
+    dt = t.dtype
+    if dt in (torch.int64, torch.bool) and isinstance(n, numbers.Integral):
+        with np.errstate(over="ignore"):
+            prod = np.asarray(to_np(t).astype(np.int64) * np.int64(int(n)), dtype=np.int64)
+            return torch.from_numpy(prod.copy()).reshape(t.shape)
+    if dt == torch.float64:
+        return from_np(to_np(t) * np.float64(n), dt, t.shape)
+    if dt == torch.bfloat16:
+        return from_np(f32_to_bf16_bits(bf16_bits_to_f32(to_np(t)) * _f32_scalar(n)), dt, t.shape)
+    if dt == torch.float16:
+        return from_np((to_np(t).astype(np.float32) * _f32_scalar(n)).astype(np.float16), dt, t.shape)
+    if dt == torch.float32 or dt in (torch.int64, torch.bool):
+        return from_np((to_np(t).astype(np.float32) * _f32_scalar(n)).astype(np.float32), torch.float32, t.shape)
+    raise TypeError(f"oracle: unsupported dtype {dt}")
+
+
+def div_scalar(t: torch.Tensor, d) -> torch.Tensor:
+    """torch's true division `t / d` by a Python scalar: integer tensors
+    promote to float32 (fl32(v) / fl32(d)), float tensors divide by the
+    scalar rounded to their opmath type."""
+    dt = t.dtype
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if dt == torch.float64:
+            return from_np(to_np(t) / np.float64(d), dt, t.shape)
+        if dt == torch.bfloat16:
+            return from_np(f32_to_bf16_bits(bf16_bits_to_f32(to_np(t)) / _f32_scalar(d)), dt, t.shape)
+        if dt == torch.float16:
+            return from_np((to_np(t).astype(np.float32) / _f32_scalar(d)).astype(np.float16), dt, t.shape)
+        return from_np((to_np(t).astype(np.float32) / _f32_scalar(d)).astype(np.float32), torch.float32, t.shape)
+
+
+def mpi_fedavg(model_list):
+    """FedAVGAggregator._fedavg_aggregation_ (:99-116) step by step: each term
+    `local_model_params[k] * local_sample_number / training_num` left to right,
+    accumulated into client 0's dict (live lookups: a dict listed again reads
+    the running sum)."""
+    training_num = 0
+    for i in range(len(model_list)):
+        local_sample_number, local_model_params = model_list[i]
+        training_num += local_sample_number
+    (num0, averaged_params) = model_list[0]
+    for k in list(averaged_params.keys()):
+        for i in range(len(model_list)):
+            local_sample_number, local_model_params = model_list[i]
+            x = div_scalar(mul_scalar(local_model_params[k], local_sample_number), training_num)
+            averaged_params[k] = x if i == 0 else add(averaged_params[k], x)
+    return averaged_params
 
 
 # --------------------------------------------------------------------------

@@ -474,3 +474,33 @@ def secagg_inputs(spec):
     dim = sum(int(np.prod(s)) for _, s, _ in SECAGG_KEYS)
     mask = rng.integers(0, p, size=(dim, 1), dtype=np.int64)
     return dicts, mask
+
+
+# The MPI simulation's FedAvg (simulation/mpi/fedavg/FedAVGAggregator.py:
+# 99-116): each term is `p * n_i / N`, two roundings in that order.  Run through
+# the reference's own FedAVGAggregator._fedavg_aggregation_.
+MPI_CASES: List[Dict[str, Any]] = []
+
+
+def _mpi(name, K, keys, seed, **kw):
+    MPI_CASES.append(dict(name=name, optimizer="FedAvg", K=K, keys=keys, seed=seed, **kw))
+
+
+_mpi("mpi_cfg2_cnn_web_k32", 32, _model_keys("cnn_web"), 500)
+_mpi("mpi_resnet_mini_k5", 5, RESNET_MINI, 501, round_idx=3)
+_mpi("mpi_ragged_f32_k17", 17, RAGGED_F32, 502)
+_mpi("mpi_ragged_bf16_k9", 9, RAGGED_BF16, 503)
+_mpi("mpi_ragged_f16_k4", 4, [[k, s, F16] for k, s, _ in RAGGED_BF16], 504)
+_mpi("mpi_ragged_f64_k3", 3, [[k, s, F64] for k, s, _ in RAGGED_BF16], 505)
+_mpi("mpi_mixed_k4", 4, [["w", [513], F32], ["h", [257], BF16], ["d", [33], F64], ["n", [3], I64],
+                         ["m", [65], F16]], 506)
+_mpi("mpi_float_samples_k5", 5, RESNET_MINI, 507, sample_nums=[10.5, 0.25, 3.0, 1e-3, 77.7])
+_mpi("mpi_huge_samples_k4", 4, RAGGED_F32[:4], 508, sample_nums=[10 ** 12, 3, 10 ** 15 + 1, 7])
+# int64 values up to 2^40 times sample counts up to 3e7: int64 products wrap
+_mpi("mpi_bigint_wrap_k3", 3, RESNET_MINI, 509, int_range=[-(2 ** 40), 2 ** 40],
+     sample_nums=[10 ** 7, 3 * 10 ** 7 + 1, 12345])
+_mpi("mpi_specials_f32_k4", 4, [["x", [64], F32]], 510, specials=True)
+_mpi("mpi_specials_bf16_k4", 4, [["x", [64], BF16]], 511, specials=True)
+_mpi("mpi_k1", 1, RAGGED_F32, 512)
+_mpi("mpi_zero_samples_k2", 2, RAGGED_F32[:3], 513, sample_nums=[0, 0])
+_mpi("mpi_alias_k4", 4, RESNET_MINI, 514, alias=[[2, "first"]])

@@ -371,6 +371,27 @@ def run_secagg_case(spec):
     save(spec["name"], meta, arrays)
 
 
+def import_mpi_fedavg():
+    """simulation/mpi/fedavg/FedAVGAggregator.py with its module-level imports
+    stubbed: wandb, fedml.mlops, and the attacker / defender singletons (only
+    _fedavg_aggregation_ runs; it touches none of them)."""
+    for name, path in [("fedml.simulation.mpi.fedavg", f"{REF}/simulation/mpi/fedavg"),
+                       ("fedml.core.security", f"{REF}/core/security")]:
+        m = types.ModuleType(name)
+        m.__path__ = [path]
+        sys.modules.setdefault(name, m)
+    sys.modules.setdefault("fedml.mlops", types.ModuleType("fedml.mlops"))
+    sys.modules["fedml"].mlops = sys.modules["fedml.mlops"]
+    for mod, cls in [("fedml.core.security.fedml_attacker", "FedMLAttacker"),
+                     ("fedml.core.security.fedml_defender", "FedMLDefender")]:
+        if mod not in sys.modules:
+            m = types.ModuleType(mod)
+            setattr(m, cls, type(cls, (), {}))
+            sys.modules[mod] = m
+    from fedml.simulation.mpi.fedavg.FedAVGAggregator import FedAVGAggregator
+    return FedAVGAggregator
+
+
 def main(only=()):
     """only: case-name prefixes to regenerate (default: every case)."""
     def want(spec):
@@ -407,6 +428,13 @@ def main(only=()):
     for spec in filter(want, cases.SECAGG_CASES):
         run_secagg_case(spec)
         print("wrote", spec["name"])
+    mpi = [spec for spec in cases.MPI_CASES if want(spec)]
+    if mpi:
+        FedAVGAggregator = import_mpi_fedavg()
+        agg = object.__new__(FedAVGAggregator)
+        for spec in mpi:
+            run_agg_case(FedMLAggOperator, spec, aggregate=agg._fedavg_aggregation_)
+            print("wrote", spec["name"])
 
 
 if __name__ == "__main__":

@@ -148,7 +148,9 @@ def test_pairdist2_vs_numpy(K, cuda_device):
     np.testing.assert_array_equal(D, D.T)
 
 
-@pytest.mark.parametrize("K", [1, 2, 3, 16, 17, 63, 64, 65, 100, 127, 128])
+# every group count NB = ceil(K / 16) of the split kernel's builds, 1 .. 8
+# (33 / 48: NB = 3, 81 / 96: NB = 6), with both full and partial last groups
+@pytest.mark.parametrize("K", [1, 2, 3, 16, 17, 33, 48, 63, 64, 65, 81, 96, 100, 127, 128])
 def test_pairgram2_vs_numpy(K, cuda_device):
     """The centred Gram: every pair within 2e-6 of the exact fp32-difference
     distances relative to (|c_i|^2 + |c_j|^2) of the column-centred rows (and
@@ -201,6 +203,43 @@ def test_auto_pair_distance_falls_back_for_a_far_outlier(scale, cuda_device):
     assert sa[:10] == se[:10]
     if scale > 1.0:
         assert 7 not in sa[:K - 5]
+
+
+@pytest.mark.parametrize("bad", ["inf", "nan", "1e30"])
+def test_auto_pair_distance_falls_back_for_a_non_finite_outlier(bad, cuda_device):
+    """A client with an inf / NaN element, or scaled so far (1e30) that its
+    fp32 squares overflow, makes the centred Gram non-finite.  auto must then
+    hand the exact kernel's distances back (bit for bit, inf where the
+    reference's torch.norm gives inf), and Krum keeps that client out, as the
+    exact kernel and the reference do."""
+    K, L = 24, 30_000
+    rows = _rows(K, L, cuda_device, 11)
+    if bad == "inf":
+        rows[5, 123] = float("inf")
+    elif bad == "nan":
+        rows[5, 77] = float("nan")
+    else:
+        rows[5] *= 1e30
+    segs = [(0, L)]
+    ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    ch, n = _chunks(segs, nat.PAIR_CHUNK, cuda_device)
+    Dg = dfn.pairdist2_rows(ptrs, K, ch, n, cuda_device, "gram").cpu().numpy()
+    De = dfn.pairdist2_rows(ptrs, K, ch, n, cuda_device, "exact").cpu().numpy()
+    Da = dfn.pairdist2_rows(ptrs, K, ch, n, cuda_device, "auto").cpu().numpy()
+    assert dfn.gram_condition(Dg) == float("inf")
+    np.testing.assert_array_equal(Da, De)
+    if bad != "nan":
+        sa = np.argsort(dfn.krum_scores(Da, 3), kind="stable").tolist()
+        assert sa[-1] == 5 and 5 not in sa[:K - 3]
+
+
+def test_gram_condition_non_finite_entries():
+    D = np.ones((3, 3)) - np.eye(3)
+    assert dfn.gram_condition(D) < dfn.GRAM_MAX_CONDITION
+    for v in (float("inf"), float("nan")):
+        E = D.copy()
+        E[0, 1] = E[1, 0] = v
+        assert dfn.gram_condition(E) == float("inf")
 
 
 def test_pairgram2_rejects_more_than_128_clients(cuda_device):

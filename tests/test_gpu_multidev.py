@@ -99,6 +99,23 @@ def test_agg_with_fedagg_devices_matches_reference(G, name, cuda_device):
     assert 1 <= len(b.shards) <= G
 
 
+def test_one_listed_device_after_a_multi_device_round(cuda_device):
+    """A round with args.fedagg_devices naming ONE device after a multi-device
+    round of the same layout runs on that device and drops the cached
+    multi-device bucket (it does not reuse the earlier placement)."""
+    meta, arrays = gu.load("ragged_f32_k17")
+    spec = meta["spec"]
+    args = cases.Args(spec)
+    args.fedagg_devices = [cuda_device] * 2
+    ao._MULTI.clear()
+    ao._BUCKETS.clear()
+    gu.assert_groups(ao.FedMLAggOperator.agg(args, cases.build_inputs(spec)), meta, arrays, "multi")
+    assert len(ao._MULTI) == 1
+    args.fedagg_devices = [cuda_device]
+    gu.assert_groups(ao.FedMLAggOperator.agg(args, cases.build_inputs(spec)), meta, arrays, "one")
+    assert len(ao._MULTI) == 0 and len(ao._BUCKETS) == 1
+
+
 @pytest.mark.parametrize("G", [2, 3])
 def test_agg_multidevice_per_client_staging(G, cuda_device, monkeypatch):
     """Rounds above the batched-pack size go client by client through each

@@ -144,3 +144,17 @@ def test_factory_places_the_server(cuda_device, monkeypatch):
     a, b = _run_round(one, raw), _run_round(s, host_clients(entries, 4, seed=9))
     for k in a:
         gu.assert_same(b[k], a[k], k)
+
+
+def test_multi_device_server_exposes_the_server_settings(cuda_device):
+    """The multi-device server carries FedOptServer's scalar settings and names
+    its per-shard buckets and devices."""
+    entries = [("w", (300, 64), torch.float32), ("b", (300,), torch.float32)]
+    init = host_clients(entries, 1, seed=5)[0][1]
+    one = FedOptServer(init, ["w", "b"], 3, "sgd", 0.5, 0.9, cuda_device)
+    multi = MultiDeviceFedOptServer(init, ["w", "b"], 3, "sgd", 0.5, 0.9, [cuda_device] * 2)
+    for a in ("optimizer", "lr", "momentum", "betas", "eps", "alpha", "weight_decay", "lr_decay", "worker_num",
+              "param_names"):
+        assert getattr(multi, a) == getattr(one, a), a
+    assert multi.device == one.device and multi.bucket is multi.buckets[0]
+    assert len(multi.buckets) == len(multi.devices) == 2
