@@ -48,6 +48,8 @@ def main() -> None:
     ap.add_argument("--out", default="gpurun_out/r04/multidev_bench.json")
     ap.add_argument("--ingest", action="store_true",
                     help="also time put() x K + reduce_to_host on resident buckets, the G values interleaved")
+    ap.add_argument("--shared-copy", action="store_true",
+                    help="--ingest: add arms where every shard of G > 1 stages on ONE shared copy stream")
     ap.add_argument("--ab-pack", action="store_true",
                     help="host rounds: time the pack pool and round 3's threads per call, interleaved")
     a = ap.parse_args()
@@ -129,35 +131,51 @@ def main() -> None:
         torch.cuda.empty_cache()
     if a.ingest:
         # the cross-silo arrival path: every client put() into resident
-        # buckets (one per G, built once), then reduce_to_host; the G values
-        # interleaved per round in this one process, so host drift cancels
-        buckets = {G: MultiDeviceBucket([(k, s, dt) for k, s, dt in entries], K, [dev] * G) for G in a.shards}
+        # buckets (one per arm, built once), then reduce_to_host; the arms
+        # interleaved per round in this one process, so host drift cancels.
+        # --shared-copy adds "G<n>s" arms whose shards all stage on ONE copy
+        # stream: if G shards on one GPU cost more only because their copy
+        # streams contend for the one PCIe link, a shared stream (strictly
+        # serial copies) should cost no more than the per-shard streams
+        arms = {f"G{G}": G for G in a.shards}
+        if a.shared_copy:
+            arms.update({f"G{G}s": G for G in a.shards if G > 1})
+        buckets = {}
+        for name, G in arms.items():
+            b = MultiDeviceBucket([(k, s, dt) for k, s, dt in entries], K, [dev] * G)
+            if name.endswith("s"):
+                shared = torch.cuda.Stream(dev)
+                for sh in b.shards:
+                    sh._copy = shared
+            buckets[name] = b
         ns = [n for n, _ in raw]
-        tin = {G: [] for G in a.shards}
+        names = list(arms)
+        tin = {n: [] for n in names}
         outs = {}
         for r in range(a.reps * 2 + 1):
-            order = a.shards[r % len(a.shards):] + a.shards[:r % len(a.shards)]
-            for G in order:
-                b = buckets[G]
+            order = names[r % len(names):] + names[:r % len(names)]
+            for name in order:
+                b = buckets[name]
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for i, (n, d) in enumerate(raw):
                     b.put(i, d, n)
-                outs[G] = b.reduce_to_host(b.weights(ns))
+                outs[name] = b.reduce_to_host(b.weights(ns))
                 torch.cuda.synchronize()
                 if r:
-                    tin[G].append(time.perf_counter() - t0)
-        g0 = a.shards[0]
+                    tin[name].append(time.perf_counter() - t0)
+        g0 = names[0]
         res["ingest"] = {}
-        for G in a.shards:
-            same = all(torch.equal(outs[G][k].view(-1).view(torch.int32) if outs[G][k].dtype == torch.float32 else
-                                   outs[G][k], outs[g0][k].view(-1).view(torch.int32)
+        for name in names:
+            same = all(torch.equal(outs[name][k].view(-1).view(torch.int32) if outs[name][k].dtype == torch.float32
+                                   else outs[name][k], outs[g0][k].view(-1).view(torch.int32)
                                    if outs[g0][k].dtype == torch.float32 else outs[g0][k]) for k in outs[g0])
-            ms = statistics.median(tin[G]) * 1e3
-            res["ingest"][f"G{G}"] = {"ms": round(ms, 2), "GBps_host_in": round(nbytes / ms / 1e6, 1),
-                                      "vs_G1": round(ms / (statistics.median(tin[g0]) * 1e3), 4),
-                                      "bitwise_equal_to_G1": same}
-            print("ingest", G, res["ingest"][f"G{G}"], flush=True)
+            ms = statistics.median(tin[name]) * 1e3
+            res["ingest"][name] = {"ms": round(ms, 2), "GBps_host_in": round(nbytes / ms / 1e6, 1),
+                                   "vs_G1": round(ms / (statistics.median(tin[g0]) * 1e3), 4),
+                                   "all_ms": [round(x * 1e3, 2) for x in tin[name]],
+                                   "shared_copy_stream": name.endswith("s"), "bitwise_equal_to_G1": same}
+            print("ingest", name, res["ingest"][name], flush=True)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
 
