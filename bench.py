@@ -114,7 +114,8 @@ def parse(argv=None):
                          "krum / dist2 / clip = the distance defenses' kernels; rlr = the robust-learning-rate "
                          "defense's fused pass)")
     ap.add_argument("--pair-distance", default="auto", choices=["auto", "gram", "exact"],
-                    help="--op krum: the centred fp32-MFMA Gram (K <= 128) or the exact-difference VALU kernel")
+                    help="--op krum: the centred Gram on the bf16 matrix cores with an exact three-way split "
+                         "(K <= 128) or the exact-difference VALU kernel")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged collectives, for rehearsing N ranks on one GPU (not a benchmark)")
     ap.add_argument("--clients", type=int, default=None,
@@ -539,9 +540,14 @@ def main():
         return
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    cpu_group = None
     if world > 1:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+            # host-side barriers around the one-process measurement: an RCCL
+            # barrier would leave a spinning kernel on every waiting rank's
+            # GPU while rank 0 runs its reductions there
+            cpu_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group("gloo")
 
@@ -887,13 +893,14 @@ def main():
             if not a.no_inprocess:
                 # FedML's server is ONE process: rank 0 alone drives all N
                 # GPUs through the multi-device bucket while the others wait
-                dist.barrier()
+                torch.cuda.synchronize()
+                dist.barrier(group=cpu_group)
                 if rank == 0:
                     try:
                         line["inprocess"] = measure_inprocess(a, entries, n_elems, K_total, world)
                     except Exception as e:
                         line["inprocess"] = {"error": f"{type(e).__name__}: {e}"}
-                dist.barrier()
+                dist.barrier(group=cpu_group)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
         line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
     if rank == 0:
