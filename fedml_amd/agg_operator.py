@@ -23,6 +23,7 @@ Options read from ``args`` (all optional, duck-typed like FedML's Arguments):
 """
 from __future__ import annotations
 
+import weakref
 from collections import OrderedDict
 from typing import Dict, List, Sequence, Tuple
 
@@ -298,6 +299,46 @@ def _reduce_device_walked(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str
     return OrderedDict((k, results[k]) for k in keys)
 
 
+# Buckets whose slot views callers hold as client dicts (the cross-silo
+# mirror rebinds every arriving update to its slot's views): a round over
+# exactly such dicts reduces the bucket's rows with one launch per dtype
+# group, with no walk over K x keys tensors.
+_RESIDENT: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def register_resident(bucket) -> None:
+    _RESIDENT.add(bucket)
+
+
+def _reduce_resident(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
+    """The round's dicts are ALL dicts a registered ClientBucket bound to its
+    slots (identity), with the bucket's keys in its order, and every value is
+    still that slot's view (the native same_values check): reduce those rows
+    in the list's order.  The same kernels and client order as the walked
+    path, so the same bits.  Else None."""
+    if not _RESIDENT or not hasattr(w, "same_values"):
+        return None
+    for b in list(_RESIDENT):
+        if not b._slot_dicts or b.acc_mode != acc_mode:
+            continue
+        slots = []
+        for d in dicts:
+            s = b._slot_of.get(id(d))
+            if s is None or b._slot_dicts[s][0] is not d:
+                break
+            slots.append(s)
+        else:
+            if list(keys) != b.entry_keys:
+                return None
+            if not w.same_values(list(dicts), [b._slot_dicts[s][1] for s in slots], list(keys)):
+                return None
+            with torch.cuda.device(b.device):
+                outs = b.new_outputs()
+                b.reduce_into(outs, weights, len(slots), slots=slots)
+                return b.unflatten(outs)
+    return None
+
+
 _HOST_ROUND_MAX_BYTES = 32 << 20  # host rounds up to this size: one native call, host to host
 _HOST_ROUND_FN: "int | None" = None
 
@@ -436,6 +477,10 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
         if isinstance(t0, torch.Tensor) and not t0.is_cuda and getattr(args, "fedagg_device", None) is None \
                 and torch.cuda.is_available() and not multidev.parse_devices(getattr(args, "fedagg_devices", None)):
             res = _reduce_host_round(w, dicts, keys, weights)
+            if res is not None:
+                return res
+        if isinstance(t0, torch.Tensor) and t0.is_cuda:
+            res = _reduce_resident(w, dicts, keys, weights, acc_mode)
             if res is not None:
                 return res
         res = _reduce_device_walked(w, dicts, keys, weights, acc_mode)

@@ -118,6 +118,13 @@ class ClientBucket:
         self._plans: Dict[tuple, list] = {}
         self._pool: Optional[Dict[str, torch.Tensor]] = None
         self._pool_thread = None
+        # slot -> (client dict, its view dict): dicts whose values a caller
+        # bound to this bucket's views (the cross-silo ingest), so a round over
+        # them can reduce the rows directly (agg_operator._reduce_resident)
+        self._slot_dicts: Dict[int, tuple] = {}
+        self._slot_of: Dict[int, int] = {}
+        self.entry_keys = [k for k, _, _ in self.entries]
+        self._slot_ptrs: Dict[tuple, Dict[torch.dtype, torch.Tensor]] = {}
 
     # ---- ingest ---------------------------------------------------------------
 
@@ -450,18 +457,47 @@ class ClientBucket:
             return {dt: torch.empty(_pad(max(g.length, 1)), dtype=g.out_dtype, device=self.device)
                     for dt, g in self.groups.items()}
 
+    def bind_slot(self, slot: int, state_dict, view) -> None:
+        """Record that ``state_dict``'s values are now ``view``'s (this slot's
+        views): a later round over such dicts may reduce the rows in place."""
+        old = self._slot_dicts.get(slot)
+        if old is not None:
+            self._slot_of.pop(id(old[0]), None)
+        self._slot_dicts[slot] = (state_dict, view)
+        self._slot_of[id(state_dict)] = slot
+
+    def slot_ptrs(self, slots: Sequence[int]) -> Dict[torch.dtype, torch.Tensor]:
+        """Per dtype group, the device table of the given slots' row pointers
+        (rows in that order; cached per slot list)."""
+        key = tuple(slots)
+        t = self._slot_ptrs.get(key)
+        if t is None:
+            if len(self._slot_ptrs) >= 8:
+                self._slot_ptrs.pop(next(iter(self._slot_ptrs)))
+            with torch.cuda.device(self.device):
+                t = {dt: kn.upload_i64([g.rows[s].data_ptr() for s in slots], self.device)
+                     for dt, g in self.groups.items()}
+            self._slot_ptrs[key] = t
+        return t
+
     def reduce_into(self, outs: Dict[torch.dtype, torch.Tensor], weights: Sequence[float],
-                    num_clients: Optional[int] = None, events: Optional[Dict[torch.dtype, Sequence]] = None
-                    ) -> None:
+                    num_clients: Optional[int] = None, events: Optional[Dict[torch.dtype, Sequence]] = None,
+                    slots: Optional[Sequence[int]] = None) -> None:
         """Launch the weighted sum of rows [0, K) into the flat outputs: one
         kernel per dtype group, on the current stream, no host sync.  events
         maps a dtype to (start, end) torch.cuda.Events recorded around that
-        group's launch (the benchmark's per-kernel timing)."""
-        K = num_clients if num_clients is not None else self.capacity
-        if not 1 <= K <= self.capacity:
+        group's launch (the benchmark's per-kernel timing).  slots: the rows
+        to reduce, in this order (default 0 .. K-1)."""
+        K = num_clients if num_clients is not None else (len(slots) if slots is not None else self.capacity)
+        if slots is not None and (len(slots) != K or any(not 0 <= s < self.capacity for s in slots)):
+            raise ValueError("slots: one valid slot per client")
+        if slots is not None and list(slots) == list(range(K)):
+            slots = None
+        if not 1 <= K <= self.capacity and slots is None:
             raise ValueError(f"num_clients {K} outside [1, {self.capacity}]")
         if len(weights) != K:
             raise ValueError("one weight per client")
+        tables = self.slot_ptrs(slots) if slots is not None else None
         with torch.cuda.device(self.device):
             self.sync_ingest()
             cur = torch.cuda.current_stream(self.device)
@@ -484,8 +520,8 @@ class ClientBucket:
                 with torch.cuda.stream(cur if dt == dom else self._side):
                     if ev is not None:
                         ev[0].record()
-                    kn.wsum_ptrs(dt, g.d_ptrs, w64 if dt == torch.float64 else w32, K, g.length, outs[dt], True,
-                                 self.acc_mode)
+                    kn.wsum_ptrs(dt, g.d_ptrs if tables is None else tables[dt], w64 if dt == torch.float64 else w32,
+                                 K, g.length, outs[dt], True, self.acc_mode)
                     if ev is not None:
                         ev[1].record()
             if minor:

@@ -43,6 +43,7 @@ import time
 import numpy as np
 import torch
 
+from .agg_operator import register_resident
 from .bucket import ClientBucket
 from .context import Context, shared_context
 from .layout import ROW_DTYPES
@@ -135,6 +136,11 @@ class FedMLAggregator:
             view = self._views[index] = self.bucket.view(index)
         for key in list(model_params.keys()):
             model_params[key] = view[key]
+        if isinstance(self.bucket, ClientBucket):
+            # agg() over these very dicts then reduces the rows in place
+            # (agg_operator._reduce_resident), instead of walking K x keys views
+            self.bucket.bind_slot(index, model_params, view)
+            register_resident(self.bucket)
         return True
 
     def check_whether_all_receive(self):

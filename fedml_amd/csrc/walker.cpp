@@ -521,6 +521,40 @@ PyObject* group_by_device(PyObject*, PyObject* args) {
   return out;
 }
 
+// same_values(dicts: list, views: list, keys: list) -> bool
+// True when every dicts[i] is a plain-lookup dict whose value under every key
+// IS views[i]'s value (object identity): the round's dicts are still the
+// bucket views the cross-silo ingest bound them to, so the reduction can run
+// over the bucket's rows (agg_operator._reduce_resident).  No allocation; a
+// missing key is simply False.
+PyObject* same_values(PyObject*, PyObject* args) {
+  PyObject *dicts, *views, *keys;
+  if (!PyArg_ParseTuple(args, "O!O!O!", &PyList_Type, &dicts, &PyList_Type, &views, &PyList_Type, &keys))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(dicts), T = PyList_GET_SIZE(keys);
+  if (PyList_GET_SIZE(views) != K) Py_RETURN_FALSE;
+  for (Py_ssize_t i = 0; i < K; ++i) {
+    PyObject* d = PyList_GET_ITEM(dicts, i);
+    PyObject* v = PyList_GET_ITEM(views, i);
+    if (!plain_lookup(d) || !PyDict_Check(v)) Py_RETURN_FALSE;
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      PyObject* k = PyList_GET_ITEM(keys, t);
+      PyObject* a = PyDict_GetItemWithError(d, k);
+      if (!a) {
+        if (PyErr_Occurred()) return nullptr;
+        Py_RETURN_FALSE;
+      }
+      PyObject* b = PyDict_GetItemWithError(v, k);
+      if (!b) {
+        if (PyErr_Occurred()) return nullptr;
+        Py_RETURN_FALSE;
+      }
+      if (a != b) Py_RETURN_FALSE;
+    }
+  }
+  Py_RETURN_TRUE;
+}
+
 PyMethodDef kMethods[] = {
     {"group_by_device", group_by_device, METH_VARARGS,
      "Key indices of a state dict grouped by CUDA device, largest first, or None."},
@@ -528,6 +562,7 @@ PyMethodDef kMethods[] = {
     {"walk", walk, METH_VARARGS, "Pointer tables of K device state dicts for fedagg_wsum_multi, or None."},
     {"order_by_size", order_by_size, METH_VARARGS, "Key indices of a state dict, largest tensor first, or None."},
     {"walk_host", walk_host, METH_VARARGS, "Host pointer tables of K CPU state dicts for one batched pack, or None."},
+    {"same_values", same_values, METH_VARARGS, "Every dict's values are the given views' objects (identity)."},
     {nullptr, nullptr, 0, nullptr},
 };
 

@@ -216,3 +216,72 @@ def test_server_manager_sequence(K, cuda_device):
         x, y = test_set.tensors
         pred = model(x.to(cuda_device)).argmax(1).cpu()
     assert out[1]["metrics"][0] == (pred == y).sum().item() / len(y)
+
+
+def _ingested(K, device, seed=21, entries=None):
+    entries = entries or cases_entries()
+    raw = host_clients(entries, K, seed=seed, round_idx=2)
+    host = copy.deepcopy(raw)
+    server = _keyless_server(K, device)
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    return server, raw, host
+
+
+def cases_entries():
+    return [("w", (300, 17), torch.float32), ("b", (17,), torch.float32), ("h", (77,), torch.bfloat16),
+            ("n", (), torch.int64), ("z", (0,), torch.float32)]
+
+
+def test_aggregate_reduces_the_resident_rows(cuda_device, monkeypatch):
+    """aggregate() over the ingested dicts reduces the bucket rows directly
+    (agg_operator._reduce_resident: no walk over K x keys views), bit-exact."""
+    from fedml_amd import agg_operator as ao
+
+    def no_walk(*a, **k):
+        raise AssertionError("the resident round walked the views")
+
+    server, raw, host = _ingested(6, cuda_device)
+    exp = orc.agg(_Args(), copy.deepcopy(host))
+    monkeypatch.setattr(ao, "_reduce_device_walked", no_walk)
+    averaged, _, _ = server.aggregate()
+    for k in exp:
+        assert averaged[k].dtype == exp[k].dtype, k
+        gu.assert_same(averaged[k].cpu(), exp[k], k)
+
+
+def test_resident_rounds_in_any_order_and_subset(cuda_device):
+    """agg() over the ingested dicts in another order, or a subset of them:
+    the rows go in the list's order (a pointer table per slot list)."""
+    from fedml_amd.agg_operator import FedMLAggOperator
+
+    server, raw, host = _ingested(7, cuda_device, seed=22)
+    for order in ([6, 2, 0, 5, 1, 4, 3], [3, 1, 5], [4]):
+        lst = [(server.sample_num_dict[i], server.model_dict[i]) for i in order]
+        exp = orc.agg(_Args(), [copy.deepcopy(host[i]) for i in order])
+        keep = {k: t for k, t in lst[0][1].items()}
+        res = FedMLAggOperator.agg(_Args(), lst)
+        assert res is lst[0][1]
+        for k in exp:
+            gu.assert_same(res[k].cpu(), exp[k], f"{order} {k}")
+        for k, t in keep.items():  # the next order starts from the views again
+            lst[0][1][k] = t
+
+
+def test_a_dict_changed_after_ingest_is_walked(cuda_device, monkeypatch):
+    """A hook that rebinds one value of one client (a defense scaling an
+    update) makes the round leave the rows alone: the walked path reduces
+    what the dicts hold now."""
+    from fedml_amd import agg_operator as ao
+
+    server, raw, host = _ingested(5, cuda_device, seed=23)
+    server.model_dict[3]["w"] = server.model_dict[3]["w"] * 2.0
+    host[3][1]["w"] = host[3][1]["w"] * 2.0
+    walked = []
+    real = ao._reduce_device_walked
+    monkeypatch.setattr(ao, "_reduce_device_walked", lambda *a: walked.append(1) or real(*a))
+    exp = orc.agg(_Args(), copy.deepcopy(host))
+    averaged, _, _ = server.aggregate()
+    assert walked
+    for k in exp:
+        gu.assert_same(averaged[k].cpu(), exp[k], k)
