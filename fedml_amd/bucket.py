@@ -278,19 +278,21 @@ class ClientBucket:
         for i, n in enumerate(sample_nums):
             self.sample_nums[i] = n
 
-    def put_from_table(self, slot: int, tables: Dict[int, "np.ndarray"], state_dict, sample_num: float) -> None:
+    def put_from_table(self, slot: int, tables: Dict[int, "np.ndarray"], state_dict, sample_num: float,
+                       col: Optional[int] = None) -> None:
         """put() for one client of a walked host round: the walker's pointer
         tables (``{code: int64 [T_code, capacity]}``) give every key's host
         pointer, so each dtype group is ONE native pack into a pinned staging
         row of the ring plus ONE async H2D, with no per-key Python work apart
         from integer keys promoted into the fp32 rows (converted from
-        state_dict)."""
-        jobs = self.put_from_table_prepare(slot, tables, state_dict, sample_num)
+        state_dict).  col: the tables' column holding this client (default:
+        slot; 0 for a table walked from this one dict)."""
+        jobs = self.put_from_table_prepare(slot, tables, state_dict, sample_num, col)
         gather_jobs(jobs)
         self.put_issue(jobs)
 
     def put_from_table_prepare(self, slot: int, tables: Dict[int, "np.ndarray"], state_dict,
-                               sample_num: float) -> list:
+                               sample_num: float, col: Optional[int] = None) -> list:
         """put_from_table()'s first half (as put_prepare): per dtype group a
         staging job whose sources are the walker table's pointers of this
         slot; promoted integer keys are converted into the staging row here."""
@@ -310,7 +312,7 @@ class ClientBucket:
             stage = b[0]
             job = {"dt": dt, "slot": slot, "buf": b, "whole": True, "keep": None}
             if native.size:
-                job["srcs"] = np.ascontiguousarray(by_dt[dt][native, slot])
+                job["srcs"] = np.ascontiguousarray(by_dt[dt][native, slot if col is None else col])
                 job["dsts"] = offs + stage.data_ptr()
                 job["nbytes"] = nb
             for key, lo, n in ints:
