@@ -121,13 +121,13 @@ _BUCKETS: "OrderedDict[tuple, ClientBucket]" = OrderedDict()
 _BUCKET_CACHE_SIZE = 2
 
 
-def _cached_bucket(layout, K: int, device: torch.device, acc: str) -> ClientBucket:
+def _cached_bucket(layout, K: int, device: torch.device, acc: str, promote_ints: bool = True) -> ClientBucket:
     """Host-input rounds reuse their HBM rows and pinned staging: a server
     aggregates the same model shape every round (LRU of 2 layouts)."""
-    key = (tuple((k, s, str(d)) for k, s, d in layout), K, str(device), acc)
+    key = (tuple((k, s, str(d)) for k, s, d in layout), K, str(device), acc) + (() if promote_ints else ("exact",))
     b = _BUCKETS.pop(key, None)
     if b is None:
-        b = ClientBucket(layout, K, device, low_precision_acc=acc)
+        b = ClientBucket(layout, K, device, low_precision_acc=acc, promote_ints=promote_ints)
         while len(_BUCKETS) >= _BUCKET_CACHE_SIZE:
             _BUCKETS.popitem(last=False)
     _BUCKETS[key] = b
@@ -580,7 +580,7 @@ def muldiv_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], pairs: Se
         device = _host_device(args)
         with torch.cuda.device(device):
             layout = [(k, tuple(per_key[k][0].shape), per_key[k][0].dtype) for k in host_keys]
-            bucket = ClientBucket(layout, K, device, promote_ints=False)
+            bucket = _cached_bucket(layout, K, device, "reference", promote_ints=False)  # exact int64 rows
             for i in range(K):
                 bucket.put(i, {k: per_key[k][i] for k in host_keys}, 1)
             bucket.sync_ingest()
