@@ -311,10 +311,11 @@ def register_resident(bucket) -> None:
 
 
 def _reduce_resident(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str, torch.Tensor] | None":
-    """The round's dicts are ALL dicts a registered ClientBucket bound to its
-    slots (identity), with the bucket's keys in its order, and every value is
-    still that slot's view (the native same_values check): reduce those rows
-    in the list's order.  The same kernels and client order as the walked
+    """The round's dicts are ALL dicts a registered bucket (a ClientBucket,
+    or a MultiDeviceBucket: each device its keys) bound to its slots
+    (identity), with the bucket's keys in its order, and every value is still
+    that slot's view (the native same_values check): reduce those rows in the
+    list's order.  The same kernels and client order as the walked
     path, so the same bits.  Else None."""
     if not _RESIDENT or not hasattr(w, "same_values"):
         return None
@@ -332,10 +333,7 @@ def _reduce_resident(w, dicts, keys, weights, acc_mode) -> "OrderedDict[str, tor
                 return None
             if not w.same_values(list(dicts), [b._slot_dicts[s][1] for s in slots], list(keys)):
                 return None
-            with torch.cuda.device(b.device):
-                outs = b.new_outputs()
-                b.reduce_into(outs, weights, len(slots), slots=slots)
-                return b.unflatten(outs)
+            return b.reduce_slots(slots, weights)
     return None
 
 

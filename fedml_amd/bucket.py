@@ -468,6 +468,14 @@ class ClientBucket:
         self._slot_dicts[slot] = (state_dict, view)
         self._slot_of[id(state_dict)] = slot
 
+    def reduce_slots(self, slots: Sequence[int], weights: Sequence[float]) -> "OrderedDict[str, torch.Tensor]":
+        """FedAvg of the given slots' rows, in that order: per-key device
+        tensors (views of one fresh flat buffer per dtype group)."""
+        with torch.cuda.device(self.device):
+            outs = self.new_outputs()
+            self.reduce_into(outs, weights, len(slots), slots=slots)
+            return self.unflatten(outs)
+
     def slot_ptrs(self, slots: Sequence[int]) -> Dict[torch.dtype, torch.Tensor]:
         """Per dtype group, the device table of the given slots' row pointers
         (rows in that order; cached per slot list)."""

@@ -143,11 +143,10 @@ class FedMLAggregator:
             view = self._views[index] = self.bucket.view(index)
         for key in list(model_params.keys()):
             model_params[key] = view[key]
-        if isinstance(self.bucket, ClientBucket):
-            # agg() over these very dicts then reduces the rows in place
-            # (agg_operator._reduce_resident), instead of walking K x keys views
-            self.bucket.bind_slot(index, model_params, view)
-            register_resident(self.bucket)
+        # agg() over these very dicts then reduces the rows in place
+        # (agg_operator._reduce_resident), instead of walking K x keys views
+        self.bucket.bind_slot(index, model_params, view)
+        register_resident(self.bucket)
         return True
 
     @staticmethod

@@ -267,6 +267,10 @@ class MultiDeviceBucket:
         self.owner: Dict[str, int] = {k: g for g, sub in enumerate(self.plan) for k, _, _ in sub}
         self.sample_nums: List[Optional[float]] = [None] * capacity
         self.int_keys = set().union(*(b.int_keys for b in self.shards))
+        self.acc_mode = self.shards[0].acc_mode
+        self.entry_keys = [k for k, _, _ in self.entries]
+        self._slot_dicts: Dict[int, tuple] = {}
+        self._slot_of: Dict[int, int] = {}
 
     # ---- ingest ---------------------------------------------------------------
 
@@ -335,6 +339,21 @@ class MultiDeviceBucket:
                 b.reduce_into(outs, w, K)
                 parts.append(b.unflatten(outs))
         return merge_in_order(self.entries, parts)
+
+    def bind_slot(self, slot: int, state_dict, view) -> None:
+        """As ClientBucket.bind_slot: state_dict's values are now ``view``'s
+        (this slot's views on their keys' devices)."""
+        old = self._slot_dicts.get(slot)
+        if old is not None:
+            self._slot_of.pop(id(old[0]), None)
+        self._slot_dicts[slot] = (state_dict, view)
+        self._slot_of[id(state_dict)] = slot
+
+    def reduce_slots(self, slots: Sequence[int], weights: Sequence[float]) -> "OrderedDict[str, torch.Tensor]":
+        """FedAvg of the given slots on every device (each device's launches
+        enqueued before the next device's), results on their keys' devices
+        in the model's key order."""
+        return merge_in_order(self.entries, [b.reduce_slots(slots, weights) for b in self.shards])
 
     def reduce_to_host(self, weights: Sequence[float], num_clients: Optional[int] = None,
                        into: Optional[Dict[str, torch.Tensor]] = None, chunks: int = 8

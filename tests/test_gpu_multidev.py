@@ -135,6 +135,44 @@ def test_agg_multidevice_per_client_staging(G, cuda_device, monkeypatch):
         gu.assert_same(res[k], e, k)
 
 
+@pytest.mark.parametrize("G", [2, 3])
+def test_cross_silo_multidevice_round_reduces_resident_rows(G, cuda_device, monkeypatch):
+    """The multi-device cross-silo round end reduces every shard's rows in
+    place (agg_operator._reduce_resident on a MultiDeviceBucket), in any
+    client order, bit-exact; a rebound value sends the round to the walk."""
+    def no_walk(*a, **k):
+        raise AssertionError("walked")
+
+    args = _Args()
+    args.fedagg_devices = [cuda_device] * G
+    K = 6
+    server = FedMLAggregator(None, None, 0, {}, {}, {}, K, cuda_device, args,
+                             MI355XServerAggregator(torch.nn.Linear(1, 1), args))
+    server.aggregator.set_model_params = lambda p: None
+    raw = host_clients(ENTRIES, K, seed=61, round_idx=1)
+    host = copy.deepcopy(raw)
+    for i, (n, d) in enumerate(raw):
+        server.add_local_trained_result(i, d, n)
+    assert isinstance(server.bucket, MultiDeviceBucket)
+    real = ao._reduce_device_walked
+    monkeypatch.setattr(ao, "_reduce_device_walked", no_walk)
+    order = [4, 0, 5, 2, 1, 3]
+    lst = [(server.sample_num_dict[i], server.model_dict[i]) for i in order]
+    keep = dict(lst[0][1])
+    res = ao.FedMLAggOperator.agg(_Args(), lst)
+    exp = orc.agg(_Args(), [copy.deepcopy(host[i]) for i in order])
+    for k, e in exp.items():
+        gu.assert_same(res[k].cpu(), e, k)
+    lst[0][1].update(keep)  # back to the views
+    monkeypatch.setattr(ao, "_reduce_device_walked", real)
+    server.model_dict[2]["x.big"] = server.model_dict[2]["x.big"] + 1.0
+    host[2][1]["x.big"] = host[2][1]["x.big"] + 1.0
+    res = ao.FedMLAggOperator.agg(_Args(), [(server.sample_num_dict[i], server.model_dict[i]) for i in range(K)])
+    exp = orc.agg(_Args(), copy.deepcopy(host))
+    for k, e in exp.items():
+        gu.assert_same(res[k].cpu(), e, k)
+
+
 @pytest.mark.parametrize("G", [2, 4])
 def test_cross_silo_rounds_on_several_shards(G, cuda_device):
     """The cross-silo mirror with args.fedagg_devices: updates land in a
