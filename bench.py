@@ -444,6 +444,16 @@ def measure_client_axis(a, entries, n_elems: int, K_total: int, world: int, rank
     return out
 
 
+def host_barrier(tag: str, world: int) -> None:
+    """A barrier on the host only, through the rendezvous TCP store: around
+    the one-process measurement an RCCL barrier would leave a spinning kernel
+    on every waiting rank's GPU while rank 0 reduces there."""
+    store = dist.distributed_c10d._get_default_store()
+    store.add(tag, 1)
+    while store.add(tag, 0) < world:
+        time.sleep(0.005)
+
+
 def measure_inprocess(a, entries, n_elems: int, K_total: int, world: int) -> dict:
     """The multi-GPU mode FedML's server can use: ONE process (the server is
     one process, python/fedml/__init__.py:330-348) driving `world` GPUs
@@ -452,7 +462,8 @@ def measure_inprocess(a, entries, n_elems: int, K_total: int, world: int) -> dic
     exchange, bit-exact with one GPU; cross_silo/server/fedml_aggregator.py:
     58-67 feeds it).  Device-resident rows, the same clients and weights as
     the headline; runs on rank 0 while the other ranks wait at a barrier with
-    their rows freed.  Returns the "inprocess" object of the JSON line."""
+    their rows freed (host_barrier).  Returns the "inprocess" object of the
+    JSON line."""
     from fedml_amd.synth import sample_nums
 
     n_dev = torch.cuda.device_count()
@@ -540,14 +551,9 @@ def main():
         return
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    cpu_group = None
     if world > 1:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
-            # host-side barriers around the one-process measurement: an RCCL
-            # barrier would leave a spinning kernel on every waiting rank's
-            # GPU while rank 0 runs its reductions there
-            cpu_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group("gloo")
 
@@ -894,13 +900,13 @@ def main():
                 # FedML's server is ONE process: rank 0 alone drives all N
                 # GPUs through the multi-device bucket while the others wait
                 torch.cuda.synchronize()
-                dist.barrier(group=cpu_group)
+                host_barrier("inprocess_start", world)
                 if rank == 0:
                     try:
                         line["inprocess"] = measure_inprocess(a, entries, n_elems, K_total, world)
                     except Exception as e:
                         line["inprocess"] = {"error": f"{type(e).__name__}: {e}"}
-                dist.barrier(group=cpu_group)
+                host_barrier("inprocess_end", world)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
         line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
     if rank == 0:

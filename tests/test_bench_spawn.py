@@ -41,3 +41,41 @@ def test_spawn_propagates_a_failing_rank():
 def test_world_size_mismatch_is_refused():
     p = _run(["--gpus", "2"], env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE=3" in p.stderr
+
+
+def _barrier_rank(rank, world, port, out):
+    import time as _t
+
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    t0 = _t.perf_counter()
+    if rank == 1:
+        _t.sleep(0.5)
+    bench.host_barrier("t1", world)
+    waited = _t.perf_counter() - t0
+    bench.host_barrier("t2", world)  # a second barrier with its own tag
+    out.put((rank, waited))
+    dist.destroy_process_group()
+
+
+def test_host_barrier_waits_for_every_rank():
+    """bench.host_barrier (the TCP-store barrier around the one-process
+    measurement): rank 0 leaves only after the late rank 1 arrives."""
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    ps = [ctx.Process(target=_barrier_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert got[0] >= 0.45 and all(p.exitcode == 0 for p in ps)
