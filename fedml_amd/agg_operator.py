@@ -853,9 +853,10 @@ def torch_aggregator(args, raw_grad_list, training_num):
         # :116-117 overwrite the weighted sums with the LAST client's delta and
         # its control variate times w_c; only that survives.
         scaled = weighted_reduce([c_delta_para], keys, [w_c], args)
-        if weights_delta is total_weights_delta and K > 1:
-            # :116 binds the LAST client's entry, here client 0's dict itself:
-            # the weighted chain of :111,114 (with its aliasing) survives
+        if weights_delta is total_weights_delta:
+            # :116 binds the LAST client's entry, here client 0's dict itself
+            # (always so at K = 1): the weighted chain of :111,114 (with its
+            # aliasing) survives -- as float32 for integer keys
             _run_cells(raw_grad_list, (1,), keys, weights, args)
         for k in keys:
             total_weights_delta[k] = weights_delta[k]

@@ -100,6 +100,9 @@ _add("fedavg_seq_k4", "FedAvg_seq", 4, [["w", [1001], F32], ["n", [2], I64], ["h
 _add("feddyn_k3", "FedDyn", 3, [["w", [513], F32], ["n", [], I64]], seed=72)
 _add("mime_k3", "Mime", 3, RAGGED_F32[:4], seed=73, client_num_per_round=3, triple=True)
 _add("scaffold_k3", "SCAFFOLD", 3, RAGGED_F32[:4], seed=74, client_num_in_total=10, triple=True)
+# K = 1: the last client IS client 0, so :116 binds the weighted chain itself
+# (int64 buffers come back as float32 products)
+_add("scaffold_k1_ints", "SCAFFOLD", 1, RESNET_MINI, seed=75, client_num_in_total=10, triple=True)
 # errors the reference raises
 _add("err_zero_samples", "FedAvg", 2, RAGGED_F32[:2], seed=80, sample_nums=[0, 0], expect_error=True)
 _add("err_missing_key", "FedAvg", 2, RAGGED_F32[:2], seed=81, drop_key=[1, "b"], expect_error=True)
