@@ -24,6 +24,8 @@ from oracle import fedavg_oracle as orc
 from test_alias_program import _stub_seq_sum, _stub_weighted_reduce
 
 KEYS = [("w", (7,), torch.float32), ("h", (5,), torch.bfloat16), ("n", (2,), torch.int64)]
+KEYS_WIDE = KEYS + [("f", (3, 2), torch.float16), ("d", (4,), torch.float64), ("i", (3,), torch.int32),
+                    ("b", (2,), torch.bool), ("s", (), torch.float32), ("e", (0,), torch.float32)]
 
 
 class _A:
@@ -33,11 +35,13 @@ class _A:
         self.client_num_in_total = 10
 
 
-def _dict(g):
+def _dict(g, keys=KEYS):
     d = OrderedDict()
-    for k, s, dt in KEYS:
-        if dt == torch.int64:
-            d[k] = torch.randint(-50, 50, s, generator=g)
+    for k, s, dt in keys:
+        if dt == torch.bool:
+            d[k] = torch.randint(0, 2, s, generator=g).bool()
+        elif dt in (torch.int64, torch.int32):
+            d[k] = torch.randint(-50, 50, s, generator=g).to(dt)
         else:
             d[k] = torch.randn(s, generator=g).to(dt)
     return d
@@ -60,12 +64,12 @@ def _clone_round(raw):
     return [(item[0],) + tuple(dd(d) for d in item[1:]) for item in raw]
 
 
-def _round(opt, K, rnd, g):
+def _round(opt, K, rnd, g, keys=KEYS):
     triple = opt in ("Mime", "SCAFFOLD")
     raw = []
     for i in range(K):
         n = rnd.choice([1, 2, 3, 5, 7.5])
-        raw.append((n, _dict(g)) + ((_dict(g),) if triple else ()))
+        raw.append((n, _dict(g, keys)) + ((_dict(g, keys),) if triple else ()))
     d0 = raw[0][1]
     c0 = raw[0][2] if triple else None
     if opt == "Mime" and rnd.random() < 0.2:
@@ -94,13 +98,14 @@ def stubbed(monkeypatch):
     monkeypatch.setattr(ao, "_seq_sum_lists", _stub_seq_sum)
 
 
+@pytest.mark.parametrize("keys", [KEYS, KEYS_WIDE], ids=["f32-bf16-i64", "every-dtype"])
 @pytest.mark.parametrize("opt", ["FedAvg", "FedProx", "Mime", "FedAvg_seq", "FedDyn", "SCAFFOLD"])
-def test_random_alias_rounds_match_the_oracle(opt, stubbed):
-    rnd = random.Random(hash(opt) & 0xffff)
+def test_random_alias_rounds_match_the_oracle(opt, keys, stubbed):
+    rnd = random.Random(sum(map(ord, opt)) + len(keys))
     g = torch.Generator().manual_seed(7)
     for trial in range(60):
         K = rnd.randint(1, 7)
-        raw = _round(opt, K, rnd, g)
+        raw = _round(opt, K, rnd, g, keys)
         ref = _clone_round(raw)
         got = ao.FedMLAggOperator.agg(_A(opt, K), raw)
         exp = orc.agg(_A(opt, K), ref)
