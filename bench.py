@@ -147,31 +147,47 @@ def spawn_ranks(n: int, argv, probe: bool = False) -> int:
     return the first failing exit code (0 if all succeed).  The parent never
     touches the GPU (no HIP call before or after the spawn: the workers start
     as fresh processes, not forks), and rank 0 prints the JSON line."""
+    import signal
     import subprocess
 
     assert not torch.cuda.is_initialized(), "the launcher must not initialise HIP"
     port = free_port()
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+
+    def stop_all():
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+
+    def on_signal(signum, frame):  # the launcher is stopped (a time limit): take the ranks with it
+        stop_all()
+        raise SystemExit(128 + signum)
+
+    old = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                for q in live:  # a rank died: the others would wait in a collective forever
-                    q.terminate()
-        time.sleep(0.05)
-    for p in procs:
-        p.wait()
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    stop_all()  # a rank died: the others would wait in a collective forever
+            time.sleep(0.05)
+    finally:
+        stop_all()
+        for p in procs:
+            p.wait()
+        for sig, h in old.items():
+            signal.signal(sig, h)
     if probe:
         print(json.dumps({"probe": "parent", "cuda_initialized": torch.cuda.is_initialized(),
                           "exit_codes": [p.returncode for p in procs]}), flush=True)
