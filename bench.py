@@ -108,11 +108,12 @@ def parse(argv=None):
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
                          "or Adam / Adagrad lr=1.0 with torch defaults)")
     ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa", "krum", "dist2", "clip",
-                                                       "rlr"],
+                                                       "rlr", "mpi"],
                     help="1 GPU: the reduction measured (median = the wise_median defense kernel; secagg = "
                          "LightSecAgg's int64 sum mod p; lsa = its fused mask-cancel / de-quantize reconstruction; "
                          "krum / dist2 / clip = the distance defenses' kernels; rlr = the robust-learning-rate "
-                         "defense's fused pass)")
+                         "defense's fused pass; mpi = the MPI simulation's fl(fl(p n_i) / N) order, "
+                         "fedagg_wsum_muldiv)")
     ap.add_argument("--pair-distance", default="auto", choices=["auto", "gram", "exact"],
                     help="--op krum: the centred Gram on the bf16 matrix cores with an exact three-way split "
                          "(K <= 128) or the exact-difference VALU kernel")
@@ -695,6 +696,31 @@ def main():
 
         n_launch = 1
         dom_bytes = (K + 1) * gd.length * 4
+    elif a.op == "mpi":
+        # the MPI simulation's term order (FedAVGAggregator.py:99-116) over the
+        # dominant row: two roundings and a correctly rounded division per term
+        from fedml_amd import _native as nat
+        from fedml_amd import kernels as kn
+
+        if world > 1:
+            raise SystemExit("--op mpi is a 1-GPU measurement")
+        gd = bucket.groups[dom_dt]
+        mpi_out = torch.empty(gd.padded, dtype=gd.out_dtype, device=dev)
+        mpi_w = kn.muldiv_weights(dom_dt, [(n, sum(ns_local)) for n in ns_local], dev)
+        code = kn._DT_CODE[dom_dt]
+        call = lambda: nat.lib().fedagg_wsum_muldiv(  # noqa: E731
+            code, gd.d_ptrs.data_ptr(), mpi_w.data_ptr(), K, gd.length, mpi_out.data_ptr(), nat.FEDAGG_ALIGNED16,
+            nat.stream_handle())
+
+        def step(ev=None, cev=None):
+            if ev is not None:
+                ev[0].record()
+            nat.check(call(), "mpi")
+            if ev is not None:
+                ev[1].record()
+
+        n_launch = 1
+        dom_bytes = K * gd.length * gd.rows.element_size() + gd.length * torch.empty((), dtype=gd.out_dtype).element_size()
     elif a.op in ("krum", "dist2", "clip"):
         # the distance defenses' kernels over the fp32 row's weight keys
         # (csrc/robust.hip): krum = the K x K pair kernel, dist2 = every
@@ -855,8 +881,9 @@ def main():
                                   "pairtri_kernel<32> + tri_finish_kernel" if K <= 128 else
                                   "pairdist_kernel + pair_finish_kernel") + " (packed fp32)"),
                         "dist2": "dist2_kernel + sum_rows_kernel",
-                        "clip": "clip_diff_kernel", "rlr": "reduce_kernel<OpF32Rlr, RlrEpi>"}[a.op]
-                       if a.op in ("secagg", "lsa", "krum", "dist2", "clip", "rlr") else
+                        "clip": "clip_diff_kernel", "rlr": "reduce_kernel<OpF32Rlr, RlrEpi>",
+                        "mpi": "reduce_kernel<OpF32MulDiv> (fl(fl(p n_i) / N))"}[a.op]
+                       if a.op in ("secagg", "lsa", "krum", "dist2", "clip", "rlr", "mpi") else
                        median_kernel_name(K, dom_dt) if a.op == "median" else
                        ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
                          "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>"}

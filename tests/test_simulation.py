@@ -104,3 +104,29 @@ def test_mpi_weight_records():
     rec = kn._MULDIV_I
     assert rec.itemsize == 24 and kn._MULDIV_F.itemsize == 8 and kn._MULDIV_D.itemsize == 16
     assert [rec.fields[f][1] for f in ("n", "nf", "d", "is_int")] == [0, 8, 12, 16]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N", [(3, 1), (5, 4099), (17, 70_001), (64, 1_048_577), (9, 4_194_304)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64])
+def test_muldiv_kernel_every_tile_vs_oracle(K, N, dtype, cuda_device):
+    """fedagg_wsum_muldiv on device tensors across the tile configs (small,
+    mid, shipped tiles and their ragged edges), aligned and at a one-element
+    offset, integer and float sample counts, against the oracle's
+    element-wise restatement of `p * n / N` (oracle.mpi_fedavg)."""
+    from fedml_amd.simulation import fedavg_mpi_aggregate
+
+    g = torch.Generator(device=cuda_device).manual_seed(K * 7919 + N)
+
+    def make(n):
+        if dtype == torch.int64:
+            return torch.randint(-(2 ** 40), 2 ** 40, (n,), generator=g, device=cuda_device)
+        return (torch.randn(n, generator=g, device=cuda_device) * 0.05).to(dtype)
+
+    for offset in (0, 1):
+        ns = [(10 ** 7 + 13 * i) if i % 2 else (3.5 + i) for i in range(K)]  # ints (int64 products wrap) and floats
+        raw = [(ns[i], OrderedDict(x=make(N + offset)[offset:])) for i in range(K)]
+        host = [(n, OrderedDict(x=d["x"].cpu())) for n, d in raw]
+        exp = orc.mpi_fedavg(host)["x"]
+        got = fedavg_mpi_aggregate(raw)["x"]
+        gu.assert_same(got.cpu(), exp, f"K={K} N={N} {dtype} offset={offset}")
