@@ -91,10 +91,16 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 // Round an fp32 value to bf16 and back with gfx950's v_cvt_pk_bf16_f32 (RNE
 // under the default float mode; a NaN stays a NaN).  Used for the per-client
 // roundings of the reference chain; the final store uses f32_to_bf16 so a NaN
-// result carries torch's canonical 0x7FC0 pattern.
+// result carries torch's canonical 0x7FC0 pattern.  The value goes into the
+// HIGH half with +0 in the low half, so the packed register IS the rounded
+// fp32 value: one v_cvt_pk_bf16_f32 v, 0, f per rounding, where converting
+// into the low half needs a shift or mask per value afterwards (1.5
+// instructions per rounding; the chain has two per client and element).
+typedef float fedagg_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 fedagg_b2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bf16_round(float f) {
-  const __bf16 b = static_cast<__bf16>(f);
-  return bf16_to_f32(__builtin_bit_cast(uint16_t, b));
+  const fedagg_b2 b = __builtin_convertvector((fedagg_f2){0.0f, f}, fedagg_b2);
+  return __builtin_bit_cast(float, b);
 }
 
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
@@ -127,6 +133,16 @@ struct OpBF16Ref {  // bf16, torch CPU chain (round after every op)
   static __device__ __forceinline__ float r(float f) { return bf16_round(f); }
   static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return r(bf16_to_f32(x) * w); }
   static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return r(a + r(bf16_to_f32(x) * w)); }
+  // two neighbouring elements, the same arithmetic element by element: the
+  // mul and the add as v_pk_mul_f32 / v_pk_add_f32 (each lane-half IEEE RNE,
+  // as the scalar ops), the four roundings one v_cvt_pk_bf16_f32 each
+  static __device__ __forceinline__ void step2(acc_t& a0, acc_t& a1, in_t x0, in_t x1, w_t w) {
+    fedagg_f2 p = (fedagg_f2){bf16_to_f32(x0), bf16_to_f32(x1)} * (fedagg_f2){w, w};
+    p = (fedagg_f2){r(p.x), r(p.y)};
+    const fedagg_f2 t = (fedagg_f2){a0, a1} + p;
+    a0 = r(t.x);
+    a1 = r(t.y);
+  }
   static __device__ __forceinline__ out_t fin(acc_t a) { return f32_to_bf16(a); }
 };
 
@@ -737,6 +753,25 @@ __device__ __forceinline__ void reduce_edge(const Seg<OP>& s, const EPI& epi, co
     if (ok[j]) epi.one(e + int64_t(j) * BS, acc[j]);
 }
 
+// One client's pack into a lane's E chains: through OP::step2 two elements at
+// a time where the op has it (the packed-math form of the same arithmetic).
+template <class OP, class = void>
+struct HasStep2 : std::false_type {};
+template <class OP>
+struct HasStep2<OP, std::void_t<decltype(&OP::step2)>> : std::true_type {};
+
+template <class OP, int E>
+__device__ __forceinline__ void step_pack(typename OP::acc_t (&acc)[E], const Pack<typename OP::in_t, E>& x,
+                                          typename OP::w_t w) {
+  if constexpr (HasStep2<OP>::value && E % 2 == 0) {
+#pragma unroll
+    for (int e = 0; e < E; e += 2) OP::step2(acc[e], acc[e + 1], x.v[e], x.v[e + 1], w);
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = OP::step(acc[e], x.v[e], w);
+  }
+}
+
 // Body of one workgroup of BS lanes: packs [pack0, pack0 + BS*V) of segment s.
 template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI, class WS>
 __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi, const WS& w, int K, int64_t pack0) {
@@ -780,9 +815,7 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi, c
       for (int u = 0; u < U; ++u) {
         const w_t wu = w[c + u];
 #pragma unroll
-        for (int v = 0; v < V; ++v)
-#pragma unroll
-          for (int e = 0; e < E; ++e) acc[v][e] = OP::step(acc[v][e], x[u][v].v[e], wu);
+        for (int v = 0; v < V; ++v) step_pack<OP, E>(acc[v], x[u][v], wu);
       }
     }
     if constexpr (U > 1) {
@@ -800,9 +833,7 @@ __device__ __forceinline__ void reduce_block(const Seg<OP>& s, const EPI& epi, c
           if (c + u < K) {
             const w_t wu = w[c + u];
 #pragma unroll
-            for (int v = 0; v < V; ++v)
-#pragma unroll
-              for (int e = 0; e < E; ++e) acc[v][e] = OP::step(acc[v][e], x[u][v].v[e], wu);
+            for (int v = 0; v < V; ++v) step_pack<OP, E>(acc[v], x[u][v], wu);
           }
       }
     }
@@ -918,11 +949,7 @@ __global__ __launch_bounds__(BS) void reduce_narrow_kernel(Seg<OP> s, StoreEpi<O
 #pragma unroll
     for (int u = 0; u < U; ++u) x[u] = ld(c + u);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const auto wu = w[c + u];
-#pragma unroll
-      for (int j = 0; j < EL; ++j) acc[j] = OP::step(acc[j], x[u].v[j], wu);
-    }
+    for (int u = 0; u < U; ++u) step_pack<OP, EL>(acc, x[u], w[c + u]);
   }
   if (c < K) {  // fewer than U clients left (wave-uniform): every load before the first add
     Pack<in_t, EL> x[U - 1];
@@ -931,11 +958,7 @@ __global__ __launch_bounds__(BS) void reduce_narrow_kernel(Seg<OP> s, StoreEpi<O
       if (c + u < K) x[u] = ld(c + u);
 #pragma unroll
     for (int u = 0; u < U - 1; ++u)
-      if (c + u < K) {
-        const auto wu = w[c + u];
-#pragma unroll
-        for (int j = 0; j < EL; ++j) acc[j] = OP::step(acc[j], x[u].v[j], wu);
-      }
+      if (c + u < K) step_pack<OP, EL>(acc, x[u], w[c + u]);
   }
 #pragma unroll
   for (int j = 0; j < EL; ++j) epi.one(e0 + j, acc[j]);
@@ -1219,6 +1242,26 @@ int tiny_wide_fn(const void* const* src, const float* w, int32_t K, int64_t N, v
                                         reinterpret_cast<typename OP::out_t*>(out), true, st,
                                         "fedagg_wsum_tiny_variant");
 }
+template <class OP, int U, int V, int BS>
+int tiny_uv_fn(const void* const* src, const float* w, int32_t K, int64_t N, void* out, hipStream_t st) {
+  return launch_uvn<OP, U, V, true, BS>(reinterpret_cast<const typename OP::in_t* const*>(src), PtrW<float>{w}, K, N,
+                                        reinterpret_cast<typename OP::out_t*>(out), true, st,
+                                        "fedagg_wsum_tiny_variant");
+}
+// Round 5 A/B of the bf16 reference chain's instruction form: the rounding
+// into the LOW half of v_cvt_pk_bf16_f32 plus a shift / mask back to fp32, one
+// element at a time (what shipped until round 5), against the shipped
+// high-half rounding with OpBF16Ref::step2's packed mul / add.  Bit-identical.
+struct OpBF16RefLowHalf {
+  using in_t = uint16_t; using out_t = uint16_t; using acc_t = float; using w_t = float;
+  static __device__ __forceinline__ float r(float f) {
+    const __bf16 b = static_cast<__bf16>(f);
+    return bf16_to_f32(__builtin_bit_cast(uint16_t, b));
+  }
+  static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return r(bf16_to_f32(x) * w); }
+  static __device__ __forceinline__ acc_t step(acc_t a, in_t x, w_t w) { return r(a + r(bf16_to_f32(x) * w)); }
+  static __device__ __forceinline__ out_t fin(acc_t a) { return f32_to_bf16(a); }
+};
 template <class OP>
 int tiny_shipped_fn(const void* const* src, const float* w, int32_t K, int64_t N, void* out, hipStream_t st) {
   return launch_ws<OP>(reinterpret_cast<const typename OP::in_t* const*>(src), PtrW<float>{w}, K, N,
@@ -1232,6 +1275,16 @@ int tiny_shipped_fn(const void* const* src, const float* w, int32_t K, int64_t N
 const TinyVariant kTinyVariants[] = {
     {"shipped", tiny_shipped_fn<OpF32>, tiny_shipped_fn<OpBF16Ref>},
     {"wide_U16", tiny_wide_fn<OpF32, 16>, tiny_wide_fn<OpBF16Ref, 16>},
+    {"U4V4", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16Ref, 4, 4, 256>},
+    {"U4V4_lowhalf", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16RefLowHalf, 4, 4, 256>},
+    {"U1V4", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16Ref, 1, 4, 256>},
+    {"U1V4_lowhalf", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16RefLowHalf, 1, 4, 256>},
+    {"U2V4", tiny_uv_fn<OpF32, 2, 4, 256>, tiny_uv_fn<OpBF16Ref, 2, 4, 256>},
+    {"U1V8", tiny_uv_fn<OpF32, 1, 8, 256>, tiny_uv_fn<OpBF16Ref, 1, 8, 256>},
+    {"U1V2", tiny_uv_fn<OpF32, 1, 2, 256>, tiny_uv_fn<OpBF16Ref, 1, 2, 256>},
+    {"U2V2", tiny_uv_fn<OpF32, 2, 2, 256>, tiny_uv_fn<OpBF16Ref, 2, 2, 256>},
+    {"U8V1", tiny_uv_fn<OpF32, 8, 1, 256>, tiny_uv_fn<OpBF16Ref, 8, 1, 256>},
+    {"U4V2", tiny_uv_fn<OpF32, 4, 2, 256>, tiny_uv_fn<OpBF16Ref, 4, 2, 256>},
     FEDAGG_TINY_NARROW(16, 1), FEDAGG_TINY_NARROW(32, 1), FEDAGG_TINY_NARROW(64, 1),
     FEDAGG_TINY_NARROW(16, 2), FEDAGG_TINY_NARROW(32, 2), FEDAGG_TINY_NARROW(64, 2),
     FEDAGG_TINY_NARROW(16, 4), FEDAGG_TINY_NARROW(32, 4),

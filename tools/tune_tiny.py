@@ -42,7 +42,7 @@ def main() -> None:
         for K in a.K:
             for N in a.N:
                 L = (N + 63) // 64 * 64
-                rows = (torch.randn((K, L), device=dev) * 0.05).to(dt)
+                rows = torch.empty((K, L), device=dev, dtype=dt).normal_(0.0, 0.05)
                 ptrs = torch.tensor([rows[i].data_ptr() for i in range(K)], dtype=torch.int64, device=dev)
                 w = torch.rand(K, device=dev)
                 w /= w.sum()
