@@ -985,6 +985,19 @@ int launch_narrow(const typename OP::in_t* const* src, const WS& w, int32_t K, i
 
 // fp32 at 128 x 25.6M on MI355X: U4V4nt 6.44 TB/s vs U8V1nt 6.25 (profiles/r01_tune_variants_s2.json).
 template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; static constexpr bool NT = true; };
+// bf16 reference chain (round 5, after its packed rounding): one client per
+// step per lane.  tools/tune_tiny.py, interleaved, bit-identical
+// (profiles/r05/j/): 512 x 86.6M (config 4) 13.65 vs 14.04 ms for U4V4,
+// 128 x 86.6M 3.20 vs 3.31, 64 x 86.6M 1.60 vs 1.66.  (U1V8 is 0.6 % ahead at
+// config 4 but 272 VGPRs, one wave per SIMD, and 5-8 % behind at K <= 128.)
+template <> struct Cfg<OpBF16Ref> { static constexpr int U = 1, V = 4, BS = 256; static constexpr bool NT = true; };
+// ... and from 256 clients, eight packs per lane (U1V8: 272 VGPRs, one wave
+// per SIMD).  tools/ab_backtoback.py, 10 launches back to back per sample
+// (profiles/r05/m/): 512 x 86.6M 13.32 vs 13.74 ms, 384 x 86.6M 10.16 vs
+// 10.37, 256 x 86.6M 6.80 vs 6.92, 512 x 16.8M 2.44 vs 2.50, 1024 x 8.4M 2.44
+// vs 2.63; at 128 and 192 clients the two tie.  16-bit rows of 8M elements
+// and more only (below, the narrow packs run).
+constexpr int32_t kBF16WideFromClients = 256;
 
 // Tensors too small to fill the chip with 4,096-element tiles (configs 1-2,
 // LoRA-sized keys) use 256-element tiles of 64 lanes with 16 clients in flight
@@ -1089,6 +1102,10 @@ int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t
   if constexpr (!narrow_ok<OP>()) {  // 2- and 4-byte rows never reach it (narrow packs above)
     if (N < kTinyBelowElems && K >= kTinyFromClients)
       return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
+  }
+  if constexpr (std::is_same_v<OP, OpBF16Ref>) {
+    if (K >= kBF16WideFromClients && blocks >= kMid2BelowBlocks)
+      return launch_uvn<OP, 1, 8, true, 256, WS>(s, w, K, N, o, al, st, name);
   }
   if (blocks < kSmallBelowBlocks)
     return launch_uvn<OP, SmallCfg::U, SmallCfg::V, SmallCfg::NT, SmallCfg::BS, WS>(s, w, K, N, o, al, st, name);

@@ -91,3 +91,20 @@ def test_key_beyond_32_bit_ranges(N, dtype, cuda_device):
     gu.assert_same(got[idx].cpu(), exp, f"FedAvg_seq N={N} {dtype}")
     del got, ts, raw
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("offset", [0, 1], ids=["aligned", "offset1"])
+@pytest.mark.parametrize("K", [256, 300])
+def test_bf16_many_clients_wide_tiles(K, offset, cuda_device):
+    """bf16 reference chain from 256 clients over rows of 8M+ elements: the
+    eight-packs-per-lane tiles (and their ragged / unaligned edge path)."""
+    N = (8 << 20) + 12_345
+    g = torch.Generator(device=cuda_device).manual_seed(K + offset)
+    rows = torch.empty((K, N + 8), dtype=torch.bfloat16, device=cuda_device).normal_(0.0, 0.05, generator=g)
+    ns = [(i % 7) + 1 for i in range(K)]
+    raw = [(ns[i], OrderedDict(x=rows[i, offset:offset + N])) for i in range(K)]
+    cols = _columns(N, seed=K)
+    small = _gather(raw, cols)
+    got = FedMLAggOperator.agg(_Args("FedAvg", K), raw)["x"]
+    exp = orc.agg(_Args("FedAvg", K), small)["x"]
+    gu.assert_same(got[cols.to(cuda_device)].cpu(), exp, f"bf16 K={K} offset={offset}")
