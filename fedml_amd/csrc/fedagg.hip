@@ -992,12 +992,44 @@ template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; st
 // config 4 but 272 VGPRs, one wave per SIMD, and 5-8 % behind at K <= 128.)
 template <> struct Cfg<OpBF16Ref> { static constexpr int U = 1, V = 4, BS = 256; static constexpr bool NT = true; };
 // ... and from 256 clients, eight packs per lane (U1V8: 272 VGPRs, one wave
-// per SIMD).  tools/ab_backtoback.py, 10 launches back to back per sample
-// (profiles/r05/m/): 512 x 86.6M 13.32 vs 13.74 ms, 384 x 86.6M 10.16 vs
-// 10.37, 256 x 86.6M 6.80 vs 6.92, 512 x 16.8M 2.44 vs 2.50, 1024 x 8.4M 2.44
-// vs 2.63; at 128 and 192 clients the two tie.  16-bit rows of 8M elements
-// and more only (below, the narrow packs run).
+// per SIMD, so ONE 256-lane workgroup per CU) when its workgroups fill their
+// resident rounds: a U1V8 workgroup streams 16,384 elements of every client
+// (16.8 MB at 512 clients, ~0.6 ms), so a last round that keeps only part of
+// the CUs busy costs a large slice of the launch.  tools/ab_backtoback.py, 10
+// launches back to back per sample (profiles/r05/m/, r05/q/), U1V8 vs U1V4 at
+// 512 clients by rounds = workgroups / CUs: 86.6M (20.64 rounds) 13.32 vs
+// 13.74 ms, 33.6M (8.0) 4.92 vs 4.99, 25.2M (6.0) 3.73 vs 3.77, 16.8M (4.0)
+// 2.44 vs 2.50; but 60M (14.3) 9.50 vs 9.25, 43.3M (10.3) 6.94 vs 6.67, 21.6M
+// (5.16) 3.82 vs 3.40, 10.8M (2.58) 1.93 vs 1.76.  So U1V8 where rounds /
+// ceil(rounds) >= 0.97.  At 128 and 192 clients the two tie.  16-bit rows of
+// 8M elements and more only (below, the narrow packs run).
 constexpr int32_t kBF16WideFromClients = 256;
+// The bf16 -> fp32 partial of the client-axis split (OpBF16F32Out, no
+// roundings in the chain): U1V8 leads by more and tolerates a thinner last
+// round.  U1V8 vs U1V4 vs U4V4: 128 x 86.6M (20.64 rounds) 3.37 / 3.62 / 3.68
+// ms, 64 x 86.6M 1.75 / 1.93 / 1.97, 256 x 86.6M 6.71 / 6.94 / 7.00, 128 x
+// 43.3M (10.3) 1.70 / 1.78 / 1.82; 128 x 21.6M (5.16) 0.90 / 0.875 / 0.872.
+// So U1V8 from 32 clients where rounds / ceil(rounds) >= 0.9.
+constexpr int32_t kF32OutWideFromClients = 32;
+
+// CUs of the current device (cached per device ordinal).
+int device_cus() {
+  static std::atomic<int> cus[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cus[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
+// Fill of the last resident round when every CU holds one workgroup of
+// `elems_per_wg` elements: rounds / ceil(rounds).
+double round_fill(int64_t N, int64_t elems_per_wg) {
+  const double rounds = double((N + elems_per_wg - 1) / elems_per_wg) / device_cus();
+  return rounds / std::ceil(rounds);
+}
 
 // Tensors too small to fill the chip with 4,096-element tiles (configs 1-2,
 // LoRA-sized keys) use 256-element tiles of 64 lanes with 16 clients in flight
@@ -1103,8 +1135,10 @@ int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t
     if (N < kTinyBelowElems && K >= kTinyFromClients)
       return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
   }
-  if constexpr (std::is_same_v<OP, OpBF16Ref>) {
-    if (K >= kBF16WideFromClients && blocks >= kMid2BelowBlocks)
+  if constexpr (std::is_same_v<OP, OpBF16Ref> || std::is_same_v<OP, OpBF16F32Out>) {
+    constexpr bool ref = std::is_same_v<OP, OpBF16Ref>;
+    if (K >= (ref ? kBF16WideFromClients : kF32OutWideFromClients) && blocks >= kMid2BelowBlocks &&
+        round_fill(N, int64_t(256) * 8 * 8) >= (ref ? 0.97 : 0.9))
       return launch_uvn<OP, 1, 8, true, 256, WS>(s, w, K, N, o, al, st, name);
   }
   if (blocks < kSmallBelowBlocks)
@@ -1243,6 +1277,7 @@ using TinyFn = int (*)(const void* const*, const float*, int32_t, int64_t, void*
 struct TinyVariant {
   const char* name;
   TinyFn f32, bf16;
+  TinyFn bf16f32 = nullptr;  // bf16 rows, fp32 partial out (client-axis pre-reduction); wide tiles only
 };
 template <class OP, int U, int EL>
 int tiny_narrow_fn(const void* const* src, const float* w, int32_t K, int64_t N, void* out, hipStream_t st) {
@@ -1290,18 +1325,18 @@ int tiny_shipped_fn(const void* const* src, const float* w, int32_t K, int64_t N
 // wave per SIMD and slower everywhere in profiles/r03/tiny/, are no longer
 // instantiated)
 const TinyVariant kTinyVariants[] = {
-    {"shipped", tiny_shipped_fn<OpF32>, tiny_shipped_fn<OpBF16Ref>},
-    {"wide_U16", tiny_wide_fn<OpF32, 16>, tiny_wide_fn<OpBF16Ref, 16>},
-    {"U4V4", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16Ref, 4, 4, 256>},
+    {"shipped", tiny_shipped_fn<OpF32>, tiny_shipped_fn<OpBF16Ref>, tiny_shipped_fn<OpBF16F32Out>},
+    {"wide_U16", tiny_wide_fn<OpF32, 16>, tiny_wide_fn<OpBF16Ref, 16>, tiny_wide_fn<OpBF16F32Out, 16>},
+    {"U4V4", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16Ref, 4, 4, 256>, tiny_uv_fn<OpBF16F32Out, 4, 4, 256>},
     {"U4V4_lowhalf", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16RefLowHalf, 4, 4, 256>},
-    {"U1V4", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16Ref, 1, 4, 256>},
+    {"U1V4", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16Ref, 1, 4, 256>, tiny_uv_fn<OpBF16F32Out, 1, 4, 256>},
     {"U1V4_lowhalf", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16RefLowHalf, 1, 4, 256>},
-    {"U2V4", tiny_uv_fn<OpF32, 2, 4, 256>, tiny_uv_fn<OpBF16Ref, 2, 4, 256>},
-    {"U1V8", tiny_uv_fn<OpF32, 1, 8, 256>, tiny_uv_fn<OpBF16Ref, 1, 8, 256>},
-    {"U1V2", tiny_uv_fn<OpF32, 1, 2, 256>, tiny_uv_fn<OpBF16Ref, 1, 2, 256>},
-    {"U2V2", tiny_uv_fn<OpF32, 2, 2, 256>, tiny_uv_fn<OpBF16Ref, 2, 2, 256>},
-    {"U8V1", tiny_uv_fn<OpF32, 8, 1, 256>, tiny_uv_fn<OpBF16Ref, 8, 1, 256>},
-    {"U4V2", tiny_uv_fn<OpF32, 4, 2, 256>, tiny_uv_fn<OpBF16Ref, 4, 2, 256>},
+    {"U2V4", tiny_uv_fn<OpF32, 2, 4, 256>, tiny_uv_fn<OpBF16Ref, 2, 4, 256>, tiny_uv_fn<OpBF16F32Out, 2, 4, 256>},
+    {"U1V8", tiny_uv_fn<OpF32, 1, 8, 256>, tiny_uv_fn<OpBF16Ref, 1, 8, 256>, tiny_uv_fn<OpBF16F32Out, 1, 8, 256>},
+    {"U1V2", tiny_uv_fn<OpF32, 1, 2, 256>, tiny_uv_fn<OpBF16Ref, 1, 2, 256>, tiny_uv_fn<OpBF16F32Out, 1, 2, 256>},
+    {"U2V2", tiny_uv_fn<OpF32, 2, 2, 256>, tiny_uv_fn<OpBF16Ref, 2, 2, 256>, tiny_uv_fn<OpBF16F32Out, 2, 2, 256>},
+    {"U8V1", tiny_uv_fn<OpF32, 8, 1, 256>, tiny_uv_fn<OpBF16Ref, 8, 1, 256>, tiny_uv_fn<OpBF16F32Out, 8, 1, 256>},
+    {"U4V2", tiny_uv_fn<OpF32, 4, 2, 256>, tiny_uv_fn<OpBF16Ref, 4, 2, 256>, tiny_uv_fn<OpBF16F32Out, 4, 2, 256>},
     FEDAGG_TINY_NARROW(16, 1), FEDAGG_TINY_NARROW(32, 1), FEDAGG_TINY_NARROW(64, 1),
     FEDAGG_TINY_NARROW(16, 2), FEDAGG_TINY_NARROW(32, 2), FEDAGG_TINY_NARROW(64, 2),
     FEDAGG_TINY_NARROW(16, 4), FEDAGG_TINY_NARROW(32, 4),
@@ -2235,11 +2270,14 @@ int32_t fedagg_num_variants(void) { return kNumVariants; }
 int fedagg_wsum_tiny_variant(int32_t dtype, const void* const* d_src, const float* d_w, int32_t K, int64_t N,
                              void* d_out, int32_t variant, fedagg_stream_t stream) {
   if (variant < 0 || variant >= kNumTinyVariants) return set_error(FEDAGG_EINVAL, "bad variant");
-  if (dtype != FEDAGG_DT_F32 && dtype != FEDAGG_DT_BF16) return set_error(FEDAGG_EINVAL, "tiny variants: f32 or bf16");
+  if (dtype != FEDAGG_DT_F32 && dtype != FEDAGG_DT_BF16 && dtype != FEDAGG_TUNE_BF16_F32OUT)
+    return set_error(FEDAGG_EINVAL, "tiny variants: f32, bf16 or bf16 -> f32 partial");
   if (K < 1 || N < 0 || !d_src || !d_w || !d_out) return set_error(FEDAGG_EINVAL, "bad argument");
-  if (N == 0) return FEDAGG_OK;
   const TinyVariant& v = kTinyVariants[variant];
-  return (dtype == FEDAGG_DT_F32 ? v.f32 : v.bf16)(d_src, d_w, K, N, d_out, reinterpret_cast<hipStream_t>(stream));
+  const TinyFn f = dtype == FEDAGG_DT_F32 ? v.f32 : dtype == FEDAGG_DT_BF16 ? v.bf16 : v.bf16f32;
+  if (!f) return set_error(FEDAGG_EINVAL, "variant not built for this dtype");
+  if (N == 0) return FEDAGG_OK;
+  return f(d_src, d_w, K, N, d_out, reinterpret_cast<hipStream_t>(stream));
 }
 
 const char* fedagg_tiny_variant_name(int32_t variant) {

@@ -20,7 +20,9 @@ import torch  # noqa: E402
 
 from fedml_amd import _native as nat  # noqa: E402
 
-DT = {"f32": (0, torch.float32), "bf16": (1, torch.bfloat16)}
+# name -> (dtype code, row dtype, output dtype); bf16f32 = bf16 rows, fp32 partial out
+DT = {"f32": (0, torch.float32, torch.float32), "bf16": (1, torch.bfloat16, torch.bfloat16),
+      "bf16f32": (0x101, torch.bfloat16, torch.float32)}
 
 
 def main() -> None:
@@ -37,14 +39,14 @@ def main() -> None:
     lib = nat.lib()
     names = [lib.fedagg_tiny_variant_name(v).decode() for v in range(lib.fedagg_num_tiny_variants())]
     idx = [names.index(v) for v in a.variants]
-    code, dt = DT[a.dtype]
+    code, dt, odt = DT[a.dtype]
     K, N = a.K, a.N
     L = (N + 63) // 64 * 64
     rows = torch.empty((K, L), device=dev, dtype=dt).normal_(0.0, 0.05)
     ptrs = torch.tensor([rows[i].data_ptr() for i in range(K)], dtype=torch.int64, device=dev)
     w = torch.rand(K, device=dev)
     w /= w.sum()
-    outs = {v: torch.empty(L, device=dev, dtype=dt) for v in idx}
+    outs = {v: torch.empty(L, device=dev, dtype=odt) for v in idx}
     st = nat.stream_handle()
 
     def run(v):
@@ -54,7 +56,7 @@ def main() -> None:
     for v in idx:
         run(v)
     torch.cuda.synchronize()
-    ibits = torch.int16 if rows.element_size() == 2 else torch.int32
+    ibits = torch.int16 if outs[idx[0]].element_size() == 2 else torch.int32
     ref = outs[idx[0]][:N].view(ibits)
     for v in idx:
         assert torch.equal(outs[v][:N].view(ibits), ref), names[v]
@@ -69,7 +71,7 @@ def main() -> None:
             ev1.record()
             ev1.synchronize()
             times[v].append(ev0.elapsed_time(ev1) / a.launches)
-    nbytes = K * N * rows.element_size() + N * rows.element_size()
+    nbytes = K * N * rows.element_size() + N * outs[idx[0]].element_size()
     res = {names[v]: {"median_ms": statistics.median(t), "min_ms": min(t), "max_ms": max(t),
                       "GBps": nbytes / statistics.median(t) / 1e6} for v, t in times.items()}
     for n, r in res.items():
