@@ -1011,6 +1011,12 @@ constexpr int32_t kBF16WideFromClients = 256;
 // 43.3M (10.3) 1.70 / 1.78 / 1.82; 128 x 21.6M (5.16) 0.90 / 0.875 / 0.872.
 // So U1V8 from 32 clients where rounds / ceil(rounds) >= 0.9.
 constexpr int32_t kF32OutWideFromClients = 32;
+// The fp32-accumulated bf16 chain (acc_mode fp32, OpBF16Acc32) sits between
+// the two (profiles/r05/t/): U1V8 / U1V4 / U4V4 at 512 x 86.6M 13.12 / 13.60
+// / 14.00 ms, 64 x 86.6M 1.69 / 1.77 / 1.82, 128 x 86.6M 3.42 / 3.43 / 3.45,
+// 512 x 43.3M (10.3 rounds) 6.56 / 6.46 / 6.62, 512 x 21.6M 3.54 / 3.30 /
+// (mid tiles) 3.30.  U1V4 tiles, U1V8 from 32 clients at a fill >= 0.97.
+template <> struct Cfg<OpBF16Acc32> { static constexpr int U = 1, V = 4, BS = 256; static constexpr bool NT = true; };
 
 // CUs of the current device (cached per device ordinal).
 int device_cus() {
@@ -1135,10 +1141,12 @@ int launch_ws(const typename OP::in_t* const* s, const WS& w, int32_t K, int64_t
     if (N < kTinyBelowElems && K >= kTinyFromClients)
       return launch_uvn<OP, TinyCfg::U, TinyCfg::V, TinyCfg::NT, TinyCfg::BS, WS>(s, w, K, N, o, al, st, name);
   }
-  if constexpr (std::is_same_v<OP, OpBF16Ref> || std::is_same_v<OP, OpBF16F32Out>) {
+  if constexpr (std::is_same_v<OP, OpBF16Ref> || std::is_same_v<OP, OpBF16F32Out> ||
+                std::is_same_v<OP, OpBF16Acc32>) {
     constexpr bool ref = std::is_same_v<OP, OpBF16Ref>;
+    constexpr double min_fill = std::is_same_v<OP, OpBF16F32Out> ? 0.9 : 0.97;
     if (K >= (ref ? kBF16WideFromClients : kF32OutWideFromClients) && blocks >= kMid2BelowBlocks &&
-        round_fill(N, int64_t(256) * 8 * 8) >= (ref ? 0.97 : 0.9))
+        round_fill(N, int64_t(256) * 8 * 8) >= min_fill)
       return launch_uvn<OP, 1, 8, true, 256, WS>(s, w, K, N, o, al, st, name);
   }
   if (blocks < kSmallBelowBlocks)
@@ -1278,6 +1286,7 @@ struct TinyVariant {
   const char* name;
   TinyFn f32, bf16;
   TinyFn bf16f32 = nullptr;  // bf16 rows, fp32 partial out (client-axis pre-reduction); wide tiles only
+  TinyFn bf16acc32 = nullptr;  // bf16 rows, fp32 accumulation, bf16 out (acc_mode fp32); wide tiles only
 };
 template <class OP, int U, int EL>
 int tiny_narrow_fn(const void* const* src, const float* w, int32_t K, int64_t N, void* out, hipStream_t st) {
@@ -1325,18 +1334,18 @@ int tiny_shipped_fn(const void* const* src, const float* w, int32_t K, int64_t N
 // wave per SIMD and slower everywhere in profiles/r03/tiny/, are no longer
 // instantiated)
 const TinyVariant kTinyVariants[] = {
-    {"shipped", tiny_shipped_fn<OpF32>, tiny_shipped_fn<OpBF16Ref>, tiny_shipped_fn<OpBF16F32Out>},
-    {"wide_U16", tiny_wide_fn<OpF32, 16>, tiny_wide_fn<OpBF16Ref, 16>, tiny_wide_fn<OpBF16F32Out, 16>},
-    {"U4V4", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16Ref, 4, 4, 256>, tiny_uv_fn<OpBF16F32Out, 4, 4, 256>},
+    {"shipped", tiny_shipped_fn<OpF32>, tiny_shipped_fn<OpBF16Ref>, tiny_shipped_fn<OpBF16F32Out>, tiny_shipped_fn<OpBF16Acc32>},
+    {"wide_U16", tiny_wide_fn<OpF32, 16>, tiny_wide_fn<OpBF16Ref, 16>, tiny_wide_fn<OpBF16F32Out, 16>, tiny_wide_fn<OpBF16Acc32, 16>},
+    {"U4V4", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16Ref, 4, 4, 256>, tiny_uv_fn<OpBF16F32Out, 4, 4, 256>, tiny_uv_fn<OpBF16Acc32, 4, 4, 256>},
     {"U4V4_lowhalf", tiny_uv_fn<OpF32, 4, 4, 256>, tiny_uv_fn<OpBF16RefLowHalf, 4, 4, 256>},
-    {"U1V4", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16Ref, 1, 4, 256>, tiny_uv_fn<OpBF16F32Out, 1, 4, 256>},
+    {"U1V4", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16Ref, 1, 4, 256>, tiny_uv_fn<OpBF16F32Out, 1, 4, 256>, tiny_uv_fn<OpBF16Acc32, 1, 4, 256>},
     {"U1V4_lowhalf", tiny_uv_fn<OpF32, 1, 4, 256>, tiny_uv_fn<OpBF16RefLowHalf, 1, 4, 256>},
-    {"U2V4", tiny_uv_fn<OpF32, 2, 4, 256>, tiny_uv_fn<OpBF16Ref, 2, 4, 256>, tiny_uv_fn<OpBF16F32Out, 2, 4, 256>},
-    {"U1V8", tiny_uv_fn<OpF32, 1, 8, 256>, tiny_uv_fn<OpBF16Ref, 1, 8, 256>, tiny_uv_fn<OpBF16F32Out, 1, 8, 256>},
-    {"U1V2", tiny_uv_fn<OpF32, 1, 2, 256>, tiny_uv_fn<OpBF16Ref, 1, 2, 256>, tiny_uv_fn<OpBF16F32Out, 1, 2, 256>},
-    {"U2V2", tiny_uv_fn<OpF32, 2, 2, 256>, tiny_uv_fn<OpBF16Ref, 2, 2, 256>, tiny_uv_fn<OpBF16F32Out, 2, 2, 256>},
-    {"U8V1", tiny_uv_fn<OpF32, 8, 1, 256>, tiny_uv_fn<OpBF16Ref, 8, 1, 256>, tiny_uv_fn<OpBF16F32Out, 8, 1, 256>},
-    {"U4V2", tiny_uv_fn<OpF32, 4, 2, 256>, tiny_uv_fn<OpBF16Ref, 4, 2, 256>, tiny_uv_fn<OpBF16F32Out, 4, 2, 256>},
+    {"U2V4", tiny_uv_fn<OpF32, 2, 4, 256>, tiny_uv_fn<OpBF16Ref, 2, 4, 256>, tiny_uv_fn<OpBF16F32Out, 2, 4, 256>, tiny_uv_fn<OpBF16Acc32, 2, 4, 256>},
+    {"U1V8", tiny_uv_fn<OpF32, 1, 8, 256>, tiny_uv_fn<OpBF16Ref, 1, 8, 256>, tiny_uv_fn<OpBF16F32Out, 1, 8, 256>, tiny_uv_fn<OpBF16Acc32, 1, 8, 256>},
+    {"U1V2", tiny_uv_fn<OpF32, 1, 2, 256>, tiny_uv_fn<OpBF16Ref, 1, 2, 256>, tiny_uv_fn<OpBF16F32Out, 1, 2, 256>, tiny_uv_fn<OpBF16Acc32, 1, 2, 256>},
+    {"U2V2", tiny_uv_fn<OpF32, 2, 2, 256>, tiny_uv_fn<OpBF16Ref, 2, 2, 256>, tiny_uv_fn<OpBF16F32Out, 2, 2, 256>, tiny_uv_fn<OpBF16Acc32, 2, 2, 256>},
+    {"U8V1", tiny_uv_fn<OpF32, 8, 1, 256>, tiny_uv_fn<OpBF16Ref, 8, 1, 256>, tiny_uv_fn<OpBF16F32Out, 8, 1, 256>, tiny_uv_fn<OpBF16Acc32, 8, 1, 256>},
+    {"U4V2", tiny_uv_fn<OpF32, 4, 2, 256>, tiny_uv_fn<OpBF16Ref, 4, 2, 256>, tiny_uv_fn<OpBF16F32Out, 4, 2, 256>, tiny_uv_fn<OpBF16Acc32, 4, 2, 256>},
     FEDAGG_TINY_NARROW(16, 1), FEDAGG_TINY_NARROW(32, 1), FEDAGG_TINY_NARROW(64, 1),
     FEDAGG_TINY_NARROW(16, 2), FEDAGG_TINY_NARROW(32, 2), FEDAGG_TINY_NARROW(64, 2),
     FEDAGG_TINY_NARROW(16, 4), FEDAGG_TINY_NARROW(32, 4),
@@ -2270,11 +2279,15 @@ int32_t fedagg_num_variants(void) { return kNumVariants; }
 int fedagg_wsum_tiny_variant(int32_t dtype, const void* const* d_src, const float* d_w, int32_t K, int64_t N,
                              void* d_out, int32_t variant, fedagg_stream_t stream) {
   if (variant < 0 || variant >= kNumTinyVariants) return set_error(FEDAGG_EINVAL, "bad variant");
-  if (dtype != FEDAGG_DT_F32 && dtype != FEDAGG_DT_BF16 && dtype != FEDAGG_TUNE_BF16_F32OUT)
-    return set_error(FEDAGG_EINVAL, "tiny variants: f32, bf16 or bf16 -> f32 partial");
+  if (dtype != FEDAGG_DT_F32 && dtype != FEDAGG_DT_BF16 && dtype != FEDAGG_TUNE_BF16_F32OUT &&
+      dtype != FEDAGG_TUNE_BF16_ACC32)
+    return set_error(FEDAGG_EINVAL, "tiny variants: f32, bf16, bf16 -> f32 partial or bf16 fp32-accumulated");
   if (K < 1 || N < 0 || !d_src || !d_w || !d_out) return set_error(FEDAGG_EINVAL, "bad argument");
   const TinyVariant& v = kTinyVariants[variant];
-  const TinyFn f = dtype == FEDAGG_DT_F32 ? v.f32 : dtype == FEDAGG_DT_BF16 ? v.bf16 : v.bf16f32;
+  const TinyFn f = dtype == FEDAGG_DT_F32    ? v.f32
+                   : dtype == FEDAGG_DT_BF16 ? v.bf16
+                   : dtype == FEDAGG_TUNE_BF16_F32OUT ? v.bf16f32
+                                                      : v.bf16acc32;
   if (!f) return set_error(FEDAGG_EINVAL, "variant not built for this dtype");
   if (N == 0) return FEDAGG_OK;
   return f(d_src, d_w, K, N, d_out, reinterpret_cast<hipStream_t>(stream));

@@ -439,11 +439,14 @@ int32_t fedagg_num_variants(void);
 
 /* Tuning entry for many clients over small tensors (tools/tune_tiny.py) and
  * for the tile shapes of large rows (tools/ab_backtoback.py): dtype
- * FEDAGG_DT_F32, FEDAGG_DT_BF16 (reference chain) or FEDAGG_TUNE_BF16_F32OUT
- * (bf16 rows, fp32 partial out, as fedagg_wsum_bf16_f32out; wide tiles
- * only, FEDAGG_EINVAL for the others), pointers 16-byte aligned, d_w a
- * device array; variant indexes fedagg_tiny_variant_name(). */
+ * FEDAGG_DT_F32, FEDAGG_DT_BF16 (reference chain), FEDAGG_TUNE_BF16_F32OUT
+ * (bf16 rows, fp32 partial out, as fedagg_wsum_bf16_f32out) or
+ * FEDAGG_TUNE_BF16_ACC32 (bf16 rows, fp32 accumulation, FEDAGG_ACC_FP32);
+ * the last two for wide tiles only, FEDAGG_EINVAL for the others; pointers
+ * 16-byte aligned, d_w a device array; variant indexes
+ * fedagg_tiny_variant_name(). */
 #define FEDAGG_TUNE_BF16_F32OUT 0x101
+#define FEDAGG_TUNE_BF16_ACC32 0x102
 int fedagg_wsum_tiny_variant(int32_t dtype, const void* const* d_src,
                              const float* d_w, int32_t K, int64_t N,
                              void* d_out, int32_t variant,

@@ -93,18 +93,29 @@ def test_key_beyond_32_bit_ranges(N, dtype, cuda_device):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("acc", ["reference", "fp32"])
 @pytest.mark.parametrize("offset", [0, 1], ids=["aligned", "offset1"])
-@pytest.mark.parametrize("K", [256, 300])
-def test_bf16_many_clients_wide_tiles(K, offset, cuda_device):
-    """bf16 reference chain from 256 clients over rows of 8M+ elements: the
-    eight-packs-per-lane tiles (and their ragged / unaligned edge path)."""
-    N = (8 << 20) + 12_345
+@pytest.mark.parametrize("K,N", [(256, (8 << 20) - 12_345), (300, (8 << 20) - 12_345), (40, 8 << 20),
+                                 (40, (8 << 20) - 12_345)])
+def test_bf16_wide_tiles(K, N, offset, acc, cuda_device):
+    """bf16 over rows of 8M+ elements where the eight-packs-per-lane tiles
+    run (the reference chain from 256 clients, the fp32-accumulated chain from
+    32, when the last resident round is full enough: 8M - 12,345 and 8M
+    elements are 512 such workgroups, two full rounds on 256 CUs), their
+    ragged / unaligned edge path, and the four-pack tiles beside them.  "fp32" is fedml_amd's
+    fedagg_low_precision_acc mode, checked against oracle.wsum_acc32."""
     g = torch.Generator(device=cuda_device).manual_seed(K + offset)
     rows = torch.empty((K, N + 8), dtype=torch.bfloat16, device=cuda_device).normal_(0.0, 0.05, generator=g)
     ns = [(i % 7) + 1 for i in range(K)]
     raw = [(ns[i], OrderedDict(x=rows[i, offset:offset + N])) for i in range(K)]
     cols = _columns(N, seed=K)
     small = _gather(raw, cols)
-    got = FedMLAggOperator.agg(_Args("FedAvg", K), raw)["x"]
-    exp = orc.agg(_Args("FedAvg", K), small)["x"]
-    gu.assert_same(got[cols.to(cuda_device)].cpu(), exp, f"bf16 K={K} offset={offset}")
+    args = _Args("FedAvg", K)
+    args.fedagg_low_precision_acc = acc
+    got = FedMLAggOperator.agg(args, raw)["x"]
+    if acc == "reference":
+        exp = orc.agg(_Args("FedAvg", K), small)["x"]
+    else:
+        ws = [n / sum(ns) for n in ns]
+        exp = orc.wsum_acc32([d["x"] for _, d in small], ws)
+    gu.assert_same(got[cols.to(cuda_device)].cpu(), exp, f"bf16 K={K} N={N} offset={offset} acc={acc}")

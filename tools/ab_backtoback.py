@@ -22,7 +22,7 @@ from fedml_amd import _native as nat  # noqa: E402
 
 # name -> (dtype code, row dtype, output dtype); bf16f32 = bf16 rows, fp32 partial out
 DT = {"f32": (0, torch.float32, torch.float32), "bf16": (1, torch.bfloat16, torch.bfloat16),
-      "bf16f32": (0x101, torch.bfloat16, torch.float32)}
+      "bf16f32": (0x101, torch.bfloat16, torch.float32), "bf16acc32": (0x102, torch.bfloat16, torch.bfloat16)}
 
 
 def main() -> None:
