@@ -34,10 +34,18 @@ def main() -> None:
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--table", default="tiny", choices=["tiny", "f32"],
+                    help="tiny: fedagg_wsum_tiny_variant (any --dtype); f32: fedagg_wsum_f32_variant (the fp32 "
+                         "large-tile table: persistent, streaming, XCD forms)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = nat.lib()
-    names = [lib.fedagg_tiny_variant_name(v).decode() for v in range(lib.fedagg_num_tiny_variants())]
+    if a.table == "f32":
+        if a.dtype != "f32":
+            raise SystemExit("--table f32 takes --dtype f32")
+        names = [lib.fedagg_variant_name(v).decode() for v in range(lib.fedagg_num_variants())]
+    else:
+        names = [lib.fedagg_tiny_variant_name(v).decode() for v in range(lib.fedagg_num_tiny_variants())]
     idx = [names.index(v) for v in a.variants]
     code, dt, odt = DT[a.dtype]
     K, N = a.K, a.N
@@ -50,8 +58,11 @@ def main() -> None:
     st = nat.stream_handle()
 
     def run(v):
-        nat.check(lib.fedagg_wsum_tiny_variant(code, ptrs.data_ptr(), w.data_ptr(), K, N, outs[v].data_ptr(), v, st),
-                  names[v])
+        if a.table == "f32":
+            rc = lib.fedagg_wsum_f32_variant(ptrs.data_ptr(), w.data_ptr(), K, N, outs[v].data_ptr(), v, st)
+        else:
+            rc = lib.fedagg_wsum_tiny_variant(code, ptrs.data_ptr(), w.data_ptr(), K, N, outs[v].data_ptr(), v, st)
+        nat.check(rc, names[v])
 
     for v in idx:
         run(v)
