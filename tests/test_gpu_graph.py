@@ -43,3 +43,31 @@ def test_reduction_and_median_replay_from_a_graph(cuda_device):
     torch.cuda.synchronize()
     gu.assert_same(outs[torch.float32][:grp.length].cpu(), eager[torch.float32][:grp.length].cpu(), "wsum")
     gu.assert_same(med[:grp.length].cpu(), med_eager[:grp.length].cpu(), "median")
+
+
+@pytest.mark.parametrize("K,N,acc", [(256, (8 << 20) - 12_345, "reference"), (40, 8 << 20, "fp32"),
+                                     (40, 1 << 20, "reference")])
+def test_bf16_tiles_replay_from_a_graph(K, N, acc, cuda_device):
+    """The bf16 dispatch reads the device's CU count (tile shape by the fill
+    of the last resident round): captured launches replay bit for bit."""
+    from fedml_amd import kernels as kn
+
+    L = (N + 63) // 64 * 64  # 16-byte aligned rows: the launches below say FEDAGG_ALIGNED16
+    rows = torch.empty((K, L), dtype=torch.bfloat16, device=cuda_device).normal_(0.0, 0.05)
+    ptrs = torch.tensor([rows[i].data_ptr() for i in range(K)], dtype=torch.int64, device=cuda_device)
+    w = kn.weights_for([1.0 / K + 1e-4 * i for i in range(K)], torch.bfloat16, cuda_device)
+    mode = {"reference": kn.ACC_REFERENCE, "fp32": kn.ACC_FP32}[acc]
+    eager = torch.empty(N, dtype=torch.bfloat16, device=cuda_device)
+    kn.wsum_ptrs(torch.bfloat16, ptrs, w, K, N, eager, True, mode)
+    torch.cuda.synchronize()
+    out = torch.empty_like(eager)
+    graph = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(cuda_device)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            kn.wsum_ptrs(torch.bfloat16, ptrs, w, K, N, out, True, mode)
+    for _ in range(2):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), eager.view(torch.int16))
