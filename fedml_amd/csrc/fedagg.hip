@@ -988,8 +988,7 @@ template <class OP> struct Cfg { static constexpr int U = 4, V = 4, BS = 256; st
 // bf16 reference chain (round 5, after its packed rounding): one client per
 // step per lane.  tools/tune_tiny.py, interleaved, bit-identical
 // (profiles/r05/j/): 512 x 86.6M (config 4) 13.65 vs 14.04 ms for U4V4,
-// 128 x 86.6M 3.20 vs 3.31, 64 x 86.6M 1.60 vs 1.66.  (U1V8 is 0.6 % ahead at
-// config 4 but 272 VGPRs, one wave per SIMD, and 5-8 % behind at K <= 128.)
+// 128 x 86.6M 3.20 vs 3.31, 64 x 86.6M 1.60 vs 1.66.
 template <> struct Cfg<OpBF16Ref> { static constexpr int U = 1, V = 4, BS = 256; static constexpr bool NT = true; };
 // ... and from 256 clients, eight packs per lane (U1V8: 272 VGPRs, one wave
 // per SIMD, so ONE 256-lane workgroup per CU) when its workgroups fill their

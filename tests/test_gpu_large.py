@@ -105,17 +105,31 @@ def test_bf16_wide_tiles(K, N, offset, acc, cuda_device):
     ragged / unaligned edge path, and the four-pack tiles beside them.  "fp32" is fedml_amd's
     fedagg_low_precision_acc mode, checked against oracle.wsum_acc32."""
     g = torch.Generator(device=cuda_device).manual_seed(K + offset)
-    rows = torch.empty((K, N + 8), dtype=torch.bfloat16, device=cuda_device).normal_(0.0, 0.05, generator=g)
+    L = (N + 8 + 7) // 8 * 8  # 16-byte row stride: offset 0 is aligned for every client
+    rows = torch.empty((K, L), dtype=torch.bfloat16, device=cuda_device).normal_(0.0, 0.05, generator=g)
     ns = [(i % 7) + 1 for i in range(K)]
     raw = [(ns[i], OrderedDict(x=rows[i, offset:offset + N])) for i in range(K)]
     cols = _columns(N, seed=K)
     small = _gather(raw, cols)
     args = _Args("FedAvg", K)
     args.fedagg_low_precision_acc = acc
-    got = FedMLAggOperator.agg(args, raw)["x"]
+    got = FedMLAggOperator.agg(args, raw)["x"]  # device dicts: the multi-tensor launch
+    ws = [n / sum(ns) for n in ns]
     if acc == "reference":
         exp = orc.agg(_Args("FedAvg", K), small)["x"]
     else:
-        ws = [n / sum(ns) for n in ns]
         exp = orc.wsum_acc32([d["x"] for _, d in small], ws)
-    gu.assert_same(got[cols.to(cuda_device)].cpu(), exp, f"bf16 K={K} N={N} offset={offset} acc={acc}")
+    idx = cols.to(cuda_device)
+    gu.assert_same(got[idx].cpu(), exp, f"agg bf16 K={K} N={N} offset={offset} acc={acc}")
+    # the single-tensor entry (fedagg_wsum_bf16: launch_ws, where the tile
+    # shape is chosen by client count and last-round fill), aligned or not
+    from fedml_amd import kernels as kn
+
+    host_ptrs = [d["x"].data_ptr() for _, d in raw]
+    assert kn.aligned16(host_ptrs) == (offset == 0)
+    ptrs = torch.tensor(host_ptrs, dtype=torch.int64, device=cuda_device)
+    out = torch.empty(N, dtype=torch.bfloat16, device=cuda_device)
+    w = kn.weights_for(ws, torch.bfloat16, cuda_device)
+    kn.wsum_ptrs(torch.bfloat16, ptrs, w, K, N, out, kn.aligned16(host_ptrs),
+                 {"reference": kn.ACC_REFERENCE, "fp32": kn.ACC_FP32}[acc])
+    gu.assert_same(out[idx].cpu(), exp, f"wsum_ptrs bf16 K={K} N={N} offset={offset} acc={acc}")
