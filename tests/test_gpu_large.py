@@ -125,7 +125,8 @@ def test_bf16_wide_tiles(K, N, offset, acc, cuda_device):
     # shape is chosen by client count and last-round fill), aligned or not
     from fedml_amd import kernels as kn
 
-    host_ptrs = [d["x"].data_ptr() for _, d in raw]
+    # (not from raw: agg() rebinds client 0's dict to the result, as the reference does)
+    host_ptrs = [rows[i, offset:offset + N].data_ptr() for i in range(K)]
     assert kn.aligned16(host_ptrs) == (offset == 0)
     ptrs = torch.tensor(host_ptrs, dtype=torch.int64, device=cuda_device)
     out = torch.empty(N, dtype=torch.bfloat16, device=cuda_device)
