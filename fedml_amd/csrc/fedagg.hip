@@ -856,11 +856,13 @@ __global__ __launch_bounds__(BS) void reduce_kernel(Seg<OP> s, EPI epi, WS w, in
   reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, int64_t(blockIdx.x) * BS * V);
 }
 
-// Reduction fused with the server Adam epilogue (AdamEpi): the
-// prefetched optimizer operands sit in VGPRs across the client loop; cap the
-// kernel at 128 VGPRs so 4 waves per SIMD stay resident (the epilogue
-// otherwise lands at 130 and 3 waves; SgdEpi fits without the cap, and
-// spills with it).
+// Reduction fused with the server Adam / SGD epilogues (AdamEpi, SgdEpi):
+// the prefetched optimizer operands sit in VGPRs across the client loop; cap
+// the kernel at 128 VGPRs so 4 waves per SIMD stay resident (uncapped, Adam
+// lands at 130 and SGD at 142-166 VGPRs, 3 waves).  Capped, the SGD kernel
+// spills 6-16 VGPRs of its element-wise edge path to scratch, and still runs
+// config 5 in 0.166 against 0.182 ms (tools/ab_libs.py, back to back,
+// profiles/r05/ab/ab_cap.txt).
 template <class OP, int U, int V, bool NT, bool ALIGNED, int BS, class EPI, class WS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void reduce_fused_kernel(
     Seg<OP> s, EPI epi, WS w, int K) {
@@ -1935,9 +1937,9 @@ int fedagg_wsum_fedopt_sgd_f32(const float* const* d_src, const float* d_w, int3
     InlW<float> iw;
     if (!inline_weights<float>(d_w, K, &iw))
       return set_error(FEDAGG_EINVAL, "fedagg_wsum_fedopt_sgd_f32: FEDAGG_HOST_WEIGHTS needs K <= 256");
-    launch_fused<false>(s, epi, iw, K, aligned, st);
+    launch_fused<true>(s, epi, iw, K, aligned, st);
   } else {
-    launch_fused<false>(s, epi, PtrW<float>{d_w}, K, aligned, st);
+    launch_fused<true>(s, epi, PtrW<float>{d_w}, K, aligned, st);
   }
   return check_launch("fedagg_wsum_fedopt_sgd_f32");
 }
