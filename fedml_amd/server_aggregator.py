@@ -254,6 +254,26 @@ class MI355XServerAggregator(ServerAggregator):
         return self.model.state_dict()
 
     def set_model_params(self, model_parameters):
+        """load_state_dict (default_aggregator.py:25-27).  When the server
+        model lives in host memory and the averaged tensors on the GPU, the
+        copy goes buffer by buffer (fedml_amd.host_copy: one DMA per flat
+        result buffer straight into the model's tensors) instead of one
+        pageable D2H per key; the key set must be the model's, as with
+        load_state_dict's strict check."""
+        sd = self.model.state_dict()
+        if (isinstance(model_parameters, dict) and list(sd) == list(model_parameters)
+                and all(not t.is_cuda for t in sd.values())
+                and any(isinstance(t, torch.Tensor) and t.is_cuda for t in model_parameters.values())):
+            from .host_copy import to_host
+
+            host = to_host(model_parameters, into=sd)
+            # keys written in place are the model's own tensors; the rest
+            # (another dtype, e.g. int64 counters from float32 averages) take
+            # load_state_dict's conversion
+            rest = OrderedDict((k, v) for k, v in host.items() if v is not sd[k])
+            if rest:
+                self.model.load_state_dict(rest, strict=False)
+            return
         self.model.load_state_dict(model_parameters)
 
     def _test(self, test_data, device, args):

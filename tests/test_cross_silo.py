@@ -124,7 +124,9 @@ def test_server_test_tag_prediction_and_nwp():
         exp_acc = ((p > 0.5).int().eq(y).sum(-1) == 4).sum().item() / 20
         exp_loss = sum(torch.nn.functional.binary_cross_entropy(model(x[i:i + 7]), y[i:i + 7], reduction="sum").item()
                        * len(y[i:i + 7]) for i in range(0, 20, 7)) / 20
-    assert acc == exp_acc and abs(loss - exp_loss) < 1e-9
+    # (the summation order of torch's CPU BCE differs by host ISA: 6.7e-7 apart
+    # on a GPU box's host, bit-equal in the build container)
+    assert acc == exp_acc and abs(loss - exp_loss) < 1e-5
 
     A.dataset = "stackoverflow_nwp"
     emb = torch.nn.Sequential(torch.nn.Embedding(11, 5), torch.nn.Flatten(), torch.nn.Linear(15, 11))

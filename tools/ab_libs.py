@@ -65,6 +65,9 @@ def main():
     out3 = [torch.empty(L3, device=dev) for _ in libs]
     cases.append(("cfg3 FedAvg", lambda i: libs[i].fedagg_wsum_f32(p3.data_ptr(), w3.data_ptr(), K3, N3,
                                                                    out3[i].data_ptr(), 1, st)))
+    hw3 = (ctypes.c_float * K3)(*([1.0 / K3] * K3))
+    cases.append(("cfg3 FedAvg host-w", lambda i: libs[i].fedagg_wsum_f32(p3.data_ptr(), ctypes.addressof(hw3), K3,
+                                                                          N3, out3[i].data_ptr(), 3, st)))
     for name, fn in cases:
         for i in range(2):
             nat.check(fn(i), name)

@@ -12,8 +12,10 @@ so config 4's 512 x 173 MB needs 1.4 GB of host memory, not 89 GB):
              then check_whether_all_receive + aggregate() (the reduction over
              the device views; the result stays on the server device, as the
              reference's GPU server keeps it) and the copy of the averaged
-             model to the host for the broadcast (per-key .cpu()); arrival
-             GB/s, aggregate ms and round-end ms (aggregate + broadcast copy)
+             model to the host for the broadcast, per key (.cpu()) and by
+             buffer (fedml_amd.host_copy.to_host, checked bit for bit);
+             arrival GB/s, aggregate ms and round-end ms (aggregate +
+             broadcast copy)
   agg_call   FedMLAggOperator.agg(args, host_list): the reference's call
              shape with the whole round inside one call; GB/s of host inputs
   link       pinned / pageable H2D and D2H ceilings of this box (1 GiB)
@@ -37,6 +39,7 @@ import bench  # noqa: E402
 from fedml_amd import shapes  # noqa: E402
 from fedml_amd.agg_operator import FedMLAggOperator  # noqa: E402
 from fedml_amd.cross_silo import FedMLAggregator  # noqa: E402
+from fedml_amd.host_copy import to_host  # noqa: E402
 from fedml_amd.server_aggregator import MI355XServerAggregator  # noqa: E402
 from fedml_amd.synth import sample_nums  # noqa: E402
 
@@ -123,6 +126,10 @@ def main() -> None:
         host = OrderedDict((k, t.cpu()) for k, t in averaged.items())  # the broadcast's copy to the host
         t3 = time.perf_counter()
         assert all(not t.is_cuda for t in host.values())
+        host2 = to_host(averaged)  # the same copy, one DMA per result buffer (fedml_amd.host_copy)
+        t4 = time.perf_counter()
+        assert all(torch.equal(host[k].view(-1).view(torch.uint8), host2[k].view(-1).view(torch.uint8))
+                   for k in host)
         if r:
             rounds.append({"arrival_ms_median": round(statistics.median(per) * 1e3, 3),
                            "arrival_GBps": round(nbytes / statistics.median(per) / 1e9, 1),
@@ -130,11 +137,14 @@ def main() -> None:
                            "ingest_GBps": round(K * nbytes / (t1 - t0) / 1e9, 1),
                            "aggregate_ms": round((t2 - t1) * 1e3, 2),
                            "broadcast_d2h_ms": round((t3 - t2) * 1e3, 2),
-                           "round_end_ms": round((t3 - t1) * 1e3, 2)})
+                           "broadcast_to_host_ms": round((t4 - t3) * 1e3, 2),
+                           "round_end_ms": round((t3 - t1) * 1e3, 2),
+                           "round_end_to_host_ms": round((t2 - t1 + t4 - t3) * 1e3, 2)})
         print(a.config, "xsilo round", r, rounds[-1] if r else "(warm-up)", flush=True)
         time.sleep(0.2)  # the next round's arrivals, in which the result pool refills
     res["xsilo"] = {"rounds": rounds,
                     "round_end_ms_median": statistics.median(x["round_end_ms"] for x in rounds),
+                    "round_end_to_host_ms_median": statistics.median(x["round_end_to_host_ms"] for x in rounds),
                     "ingest_GBps_median": statistics.median(x["ingest_GBps"] for x in rounds)}
     del server, agg
     torch.cuda.empty_cache()
