@@ -15,6 +15,7 @@ before; the results are bit-identical to ``t.cpu()`` either way.
 """
 from __future__ import annotations
 
+import threading
 from collections import OrderedDict
 from typing import Dict, Optional
 
@@ -24,6 +25,7 @@ import torch
 from . import _native as nat
 
 _STAGE: Dict[torch.device, torch.Tensor] = {}  # pinned uint8 staging per device, grown on demand
+_LOCK = threading.Lock()  # one caller at a time uses a staging buffer
 _GATHER_THREADS = 15
 # a buffer whose keys cover less than this share of the span they sit in is
 # copied key by key (a few small views of a big buffer)
@@ -64,29 +66,36 @@ def to_host(state_dict, into: Optional[Dict[str, torch.Tensor]] = None) -> "Orde
             for k, t in zip(keys, ts):
                 out[k] = _one(t, into.get(k) if into is not None else None)
             continue
-        stage = _stage(dev, hi - lo)
-        base = ts[0].untyped_storage().data_ptr()
-        span = torch.empty(0, dtype=torch.uint8, device=dev)
-        span.set_(ts[0].untyped_storage(), lo - base, (hi - lo,))
-        with torch.cuda.device(dev):
-            stage[:hi - lo].copy_(span)  # one DMA, ordered after the producers on the current stream
-        dsts, srcs, nbs = [], [], []
-        sp = stage.data_ptr()
-        for k, t in zip(keys, ts):
-            dst = into.get(k) if into is not None else None
-            if not (isinstance(dst, torch.Tensor) and not dst.is_cuda and dst.is_contiguous()
-                    and dst.dtype == t.dtype and tuple(dst.shape) == tuple(t.shape)):
-                dst = torch.empty(t.shape, dtype=t.dtype)
-            out[k] = dst
-            dsts.append(dst.data_ptr())
-            srcs.append(sp + (t.data_ptr() - lo))
-            nbs.append(t.numel() * t.element_size())
-        d = np.asarray(dsts, dtype=np.int64)
-        s = np.asarray(srcs, dtype=np.uint64)
-        n = np.asarray(nbs, dtype=np.int64)
-        nat.check(nat.lib().fedagg_host_gather(d.ctypes.data, s.ctypes.data, n.ctypes.data, int(n.size),
-                                               _GATHER_THREADS), "host_gather")
+        with _LOCK:
+            _span_to_host(dev, ts, keys, lo, hi, into, out)
     return out
+
+
+def _span_to_host(dev, ts, keys, lo, hi, into, out) -> None:
+    """One buffer's covered byte span through the pinned staging, then the
+    native scatter into the per-key host tensors."""
+    stage = _stage(dev, hi - lo)
+    base = ts[0].untyped_storage().data_ptr()
+    span = torch.empty(0, dtype=torch.uint8, device=dev)
+    span.set_(ts[0].untyped_storage(), lo - base, (hi - lo,))
+    with torch.cuda.device(dev):
+        stage[:hi - lo].copy_(span)  # one DMA, ordered after the producers on the current stream
+    dsts, srcs, nbs = [], [], []
+    sp = stage.data_ptr()
+    for k, t in zip(keys, ts):
+        dst = into.get(k) if into is not None else None
+        if not (isinstance(dst, torch.Tensor) and not dst.is_cuda and dst.is_contiguous()
+                and dst.dtype == t.dtype and tuple(dst.shape) == tuple(t.shape)):
+            dst = torch.empty(t.shape, dtype=t.dtype)
+        out[k] = dst
+        dsts.append(dst.data_ptr())
+        srcs.append(sp + (t.data_ptr() - lo))
+        nbs.append(t.numel() * t.element_size())
+    d = np.asarray(dsts, dtype=np.int64)
+    s = np.asarray(srcs, dtype=np.uint64)
+    n = np.asarray(nbs, dtype=np.int64)
+    nat.check(nat.lib().fedagg_host_gather(d.ctypes.data, s.ctypes.data, n.ctypes.data, int(n.size),
+                                           _GATHER_THREADS), "host_gather")
 
 
 def _one(t: torch.Tensor, dst) -> torch.Tensor:
