@@ -147,6 +147,26 @@ def test_other_layout_moves_key_by_key(cuda_device):
         gu.assert_same(averaged[k].cpu(), exp[k], k)
 
 
+def test_same_numel_other_shape_is_not_rebound(cuda_device):
+    """The arrival's layout check compares shapes, not element counts: a key
+    whose shape differs from the bucket's (same numel) is not rebound to the
+    bucket's view (which would reshape the client's tensor); the update moves
+    key by key with its own shapes, as the reference moves it."""
+    server = _keyless_server(3, cuda_device)
+    mk = lambda s: OrderedDict(a=torch.randn(8, 4), b=torch.randn(6))  # noqa: E731
+    d0, d1 = mk(0), mk(1)
+    server.add_local_trained_result(0, d0, 2)
+    server.add_local_trained_result(1, d1, 3)
+    assert server.bucket is not None and tuple(d1["a"].shape) == (8, 4)
+    d2 = OrderedDict(a=torch.randn(4, 8), b=torch.randn(6))  # transposed shape, same 32 elements
+    host_a = d2["a"].clone()
+    server.add_local_trained_result(2, d2, 1)
+    assert d2["a"].is_cuda and tuple(d2["a"].shape) == (4, 8)
+    gu.assert_same(d2["a"].cpu(), host_a, "own shape kept")
+    d3 = OrderedDict(a=torch.randn(8, 4).numpy(), b=torch.randn(6))  # not a tensor: never rebound
+    assert server._same_layout(d3) is None
+
+
 def test_int32_key_moves_key_by_key(cuda_device):
     """A dtype the bucket would widen (int32) keeps the reference's per-key move."""
     K = 2
