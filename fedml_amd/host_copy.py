@@ -15,6 +15,7 @@ before; the results are bit-identical to ``t.cpu()`` either way.
 """
 from __future__ import annotations
 
+import os
 import threading
 from collections import OrderedDict
 from typing import Dict, Optional
@@ -26,6 +27,8 @@ from . import _native as nat
 
 _STAGE: Dict[torch.device, torch.Tensor] = {}  # pinned uint8 staging per device, grown on demand
 _LOCK = threading.Lock()  # one caller at a time uses a staging buffer
+_STREAMS: Dict[torch.device, "torch.cuda.Stream"] = {}  # D2H copy stream per device
+_CHUNK = 16 << 20  # bytes per D2H piece: the scatter of a piece overlaps the next pieces' DMA
 _GATHER_THREADS = 15
 # a buffer whose keys cover less than this share of the span they sit in is
 # copied key by key (a few small views of a big buffer)
@@ -71,16 +74,39 @@ def to_host(state_dict, into: Optional[Dict[str, torch.Tensor]] = None) -> "Orde
     return out
 
 
+def _copy_stream(dev: torch.device) -> "torch.cuda.Stream":
+    st = _STREAMS.get(dev)
+    if st is None:
+        st = _STREAMS[dev] = torch.cuda.Stream(dev)
+    return st
+
+
 def _span_to_host(dev, ts, keys, lo, hi, into, out) -> None:
     """One buffer's covered byte span through the pinned staging, then the
-    native scatter into the per-key host tensors."""
-    stage = _stage(dev, hi - lo)
+    native scatter into the per-key host tensors.  The span goes down in
+    _CHUNK pieces on a copy stream (after the producers queued on the
+    current stream), and the keys that end in a piece are scattered as soon
+    as it has landed, while the next pieces are still on the link."""
+    n = hi - lo
+    chunk = int(os.environ.get("FEDAGG_TO_HOST_CHUNK", _CHUNK)) or n  # tuning override (0: one piece)
+    stage = _stage(dev, n)
     base = ts[0].untyped_storage().data_ptr()
     span = torch.empty(0, dtype=torch.uint8, device=dev)
-    span.set_(ts[0].untyped_storage(), lo - base, (hi - lo,))
+    span.set_(ts[0].untyped_storage(), lo - base, (n,))
+    cuts = list(range(0, n, chunk)) + [n]
+    events = []
     with torch.cuda.device(dev):
-        stage[:hi - lo].copy_(span)  # one DMA, ordered after the producers on the current stream
-    dsts, srcs, nbs = [], [], []
+        cs = _copy_stream(dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                stage[a:b].copy_(span[a:b], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                events.append(ev)
+        # the span's memory may be freed and reused by the caller's stream only after the copies
+        span.record_stream(cs)
+    per_chunk = [([], [], []) for _ in events]
     sp = stage.data_ptr()
     for k, t in zip(keys, ts):
         dst = into.get(k) if into is not None else None
@@ -88,14 +114,21 @@ def _span_to_host(dev, ts, keys, lo, hi, into, out) -> None:
                 and dst.dtype == t.dtype and tuple(dst.shape) == tuple(t.shape)):
             dst = torch.empty(t.shape, dtype=t.dtype)
         out[k] = dst
-        dsts.append(dst.data_ptr())
-        srcs.append(sp + (t.data_ptr() - lo))
-        nbs.append(t.numel() * t.element_size())
-    d = np.asarray(dsts, dtype=np.int64)
-    s = np.asarray(srcs, dtype=np.uint64)
-    n = np.asarray(nbs, dtype=np.int64)
-    nat.check(nat.lib().fedagg_host_gather(d.ctypes.data, s.ctypes.data, n.ctypes.data, int(n.size),
-                                           _GATHER_THREADS), "host_gather")
+        nb = t.numel() * t.element_size()
+        off = t.data_ptr() - lo
+        d, s_, z = per_chunk[(off + nb - 1) // chunk]  # the piece holding the key's last byte
+        d.append(dst.data_ptr())
+        s_.append(sp + off)
+        z.append(nb)
+    for ev, (d, s_, z) in zip(events, per_chunk):
+        ev.synchronize()
+        if not z:
+            continue
+        da = np.asarray(d, dtype=np.int64)
+        sa = np.asarray(s_, dtype=np.uint64)
+        za = np.asarray(z, dtype=np.int64)
+        nat.check(nat.lib().fedagg_host_gather(da.ctypes.data, sa.ctypes.data, za.ctypes.data, int(za.size),
+                                               _GATHER_THREADS), "host_gather")
 
 
 def _one(t: torch.Tensor, dst) -> torch.Tensor:
