@@ -678,8 +678,9 @@ class ClientBucket:
                     cover = [pieces[p] for p in range(lo // _PIECE, (hi - 1) // _PIECE + 1) if p in pieces]
                     if cover:  # the copy stream is in order: the latest of them covers the others
                         cur.wait_event(max(cover, key=lambda se: se[0])[1])
-                kn.wsum_ptrs(dom, d_ptrs, w64 if dom == torch.float64 else w32, K, hi - lo, outs[dom][lo:hi], True,
-                             self.acc_mode)
+                if hi > lo:  # (a round of empty keys only: nothing to launch, empty results)
+                    kn.wsum_ptrs(dom, d_ptrs, w64 if dom == torch.float64 else w32, K, hi - lo, outs[dom][lo:hi],
+                                 True, self.acc_mode)
                 ev = torch.cuda.Event()
                 ev.record(cur)
                 self._d2h.wait_event(ev)

@@ -101,6 +101,8 @@ def wsum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, d_w: torch.Tensor, K: in
               out: torch.Tensor, aligned: bool, acc_mode: int = ACC_REFERENCE) -> None:
     """Weighted sum over K sources given as a device pointer table."""
     _require_cuda(out, "wsum")
+    if N == 0:  # empty keys: nothing to launch (their outputs may have no storage)
+        return
     lib = nat.lib()
     st = nat.stream_handle()
     flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0
@@ -182,6 +184,8 @@ def muldiv_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, pairs: Sequence, K: in
     table (the MPI simulation's term order).  Returns the uploaded weight
     records (keep them alive until the launch has run)."""
     _require_cuda(out, "muldiv")
+    if N == 0:
+        return None
     if dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64):
         raise TypeError(f"muldiv: unsupported dtype {dtype}")
     want = torch.float32 if dtype == torch.int64 else dtype
@@ -197,6 +201,8 @@ def muldiv_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, pairs: Sequence, K: in
 def sum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor, aligned: bool) -> None:
     """Unweighted sequential sum (FedAvg_seq / FedDyn)."""
     _require_cuda(out, "sum")
+    if N == 0:
+        return
     if dtype not in _DT_CODE:
         raise TypeError(f"sum: unsupported dtype {dtype}")
     flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0

@@ -1,0 +1,106 @@
+"""Random rounds through the drop-in against the oracle, on the GPU.
+
+Each case draws the optimizer branch (FedAvg, FedProx, FedAvg_seq, FedDyn),
+the client count (1 to 600), a handful of keys with random dtypes (f32, bf16,
+f16, f64, int64, int32, uint8, bool) and lengths around every tile-shape
+threshold of the dispatch (tiny / narrow / small / mid / wide tiles, 0, 1 and
+ragged tails), host or device residency, the accumulation mode, and now and
+then NaN / inf / -0.0 / denormal values.  FedMLAggOperator.agg must return
+the oracle's bits (agg_operator.py:33-63 restated in oracle/fedavg_oracle.py,
+pinned to the reference's fixtures), client 0's dict rebinding included.
+Seeded: a failure names its case and replays.
+"""
+from __future__ import annotations
+
+import copy
+import random
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+from fedml_amd.agg_operator import FedMLAggOperator
+from oracle import fedavg_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+_LENGTHS = [0, 1, 3, 31, 255, 256, 1023, 1024, 4095, 4096, 4097, 16383, 32767, 32768, 70001, 262_147,
+            (1 << 20) - 1, (1 << 20) + 3]
+_WEIGHTED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32, torch.uint8,
+             torch.bool]
+_SUMMED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64]
+_CASES = 160
+_ELEMS_PER_CASE = 24 << 20  # K x elements, so the oracle's numpy loop stays short
+
+
+class _Args:
+    def __init__(self, opt, acc):
+        self.federated_optimizer = opt
+        if acc:
+            self.fedagg_low_precision_acc = acc
+
+
+def _values(rnd: random.Random, g: torch.Generator, n: int, dt: torch.dtype, special: bool) -> torch.Tensor:
+    if dt == torch.bool:
+        return torch.randint(0, 2, (n,), generator=g).bool()
+    if dt == torch.uint8:
+        return torch.randint(0, 256, (n,), generator=g).to(torch.uint8)
+    if dt in (torch.int64, torch.int32):
+        return torch.randint(-100, 100, (n,), generator=g).to(dt)
+    t = (torch.randn(n, generator=g, dtype=torch.float64) * 0.05).to(dt)
+    if special and n:
+        picks = torch.randint(0, n, (min(n, 8),), generator=g)
+        vals = [float("nan"), float("inf"), -float("inf"), -0.0, 1e-40, -1e-42, 3e38]
+        for j, p in enumerate(picks.tolist()):
+            t[p] = vals[j % len(vals)]
+    return t
+
+
+def _case(seed: int):
+    rnd = random.Random(seed)
+    g = torch.Generator().manual_seed(seed)
+    opt = rnd.choice(["FedAvg"] * 6 + ["FedProx", "FedAvg_seq", "FedDyn"])
+    summed = opt in ("FedAvg_seq", "FedDyn")
+    K = rnd.choice([1, 2, 3, 5, 8, 16, 31, 48, 64, 128, 129, 256, 300, 513, 600])
+    nkeys = rnd.randint(1, 5)
+    keys = []
+    budget = _ELEMS_PER_CASE // K
+    for j in range(nkeys):
+        dt = rnd.choice(_SUMMED if summed else _WEIGHTED)
+        n = rnd.choice([x for x in _LENGTHS if x <= budget] or [1])
+        budget = max(1, budget - n)
+        shape = (n,) if n < 4 or rnd.random() < 0.5 else (n // 2, 2) if n % 2 == 0 else (n,)
+        keys.append((f"k{j}", shape, dt))
+    special = rnd.random() < 0.15
+    raw = []
+    for i in range(K):
+        d = OrderedDict((k, _values(rnd, g, int(np.prod(s)), dt, special).reshape(s)) for k, s, dt in keys)
+        n_i = rnd.choice([1, 7, 100, 1000, 3.5, 10 ** 12])
+        raw.append((n_i, d))
+    acc = rnd.choice([None, None, None, "fp32"]) if not summed else None
+    device = rnd.random() < 0.5
+    return opt, K, keys, raw, acc, device
+
+
+@pytest.mark.parametrize("seed", list(range(_CASES)))
+def test_random_round_matches_the_oracle(seed, cuda_device):
+    opt, K, keys, raw, acc, device = _case(seed)
+    what = f"seed {seed}: {opt} K={K} acc={acc} device={device} keys={[(k, s, str(d)) for k, s, d in keys]}"
+    host = copy.deepcopy(raw)
+    if device:
+        raw = [(n, OrderedDict((k, t.to(cuda_device)) for k, t in d.items())) for n, d in raw]
+    got = FedMLAggOperator.agg(_Args(opt, acc), raw)
+    exp_src = copy.deepcopy(host)
+    exp = orc.agg(_Args(opt, None), exp_src)
+    assert list(got) == list(exp), what
+    ws = [n / sum(n for n, _ in host) for n, _ in host]
+    for k, s, dt in keys:
+        e = exp[k]
+        if acc == "fp32" and dt in (torch.bfloat16, torch.float16):
+            e = orc.wsum_acc32([d[k] for _, d in host], ws)
+        a = got[k]
+        assert a.is_cuda == device, what
+        gu.assert_same(a.cpu(), e, f"{what} key {k}")
+    assert got is raw[0][1], what  # client 0's dict, keys rebound (agg_operator.py:36-44)
