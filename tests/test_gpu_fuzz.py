@@ -8,6 +8,8 @@ ragged tails), host or device residency, the accumulation mode, and now and
 then NaN / inf / -0.0 / denormal values.  FedMLAggOperator.agg must return
 the oracle's bits (agg_operator.py:33-63 restated in oracle/fedavg_oracle.py,
 pinned to the reference's fixtures), client 0's dict rebinding included.
+The same for the MPI simulation's term order (orc.mpi_fedavg) and for the
+SCAFFOLD / Mime 3-tuples, client 0's in-place control variates included.
 Seeded: a failure names its case and replays.
 """
 from __future__ import annotations
@@ -32,6 +34,7 @@ _WEIGHTED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.
              torch.bool]
 _SUMMED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64]
 _CASES = 160
+_CASES_3 = 120  # MPI order, SCAFFOLD / Mime tuples
 _ELEMS_PER_CASE = 24 << 20  # K x elements, so the oracle's numpy loop stays short
 
 
@@ -104,3 +107,75 @@ def test_random_round_matches_the_oracle(seed, cuda_device):
         assert a.is_cuda == device, what
         gu.assert_same(a.cpu(), e, f"{what} key {k}")
     assert got is raw[0][1], what  # client 0's dict, keys rebound (agg_operator.py:36-44)
+
+
+_MPI_DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64]
+
+
+@pytest.mark.parametrize("seed", list(range(_CASES_3)))
+def test_random_mpi_round_matches_the_oracle(seed, cuda_device):
+    """The MPI simulation's term order (FedAVGAggregator.py:99-116) through
+    fedml_amd.simulation.fedavg_mpi_aggregate, random shapes, dtypes, sample
+    counts (integers, floats, 10^15: int64 products wrap) and residency."""
+    from fedml_amd.simulation import fedavg_mpi_aggregate
+
+    rnd = random.Random(1000 + seed)
+    g = torch.Generator().manual_seed(1000 + seed)
+    K = rnd.choice([1, 2, 5, 17, 64, 130, 300])
+    budget = _ELEMS_PER_CASE // 2 // K
+    keys = []
+    for j in range(rnd.randint(1, 4)):
+        n = rnd.choice([x for x in _LENGTHS if x <= budget] or [1])
+        budget = max(1, budget - n)
+        keys.append((f"k{j}", (n,), rnd.choice(_MPI_DTYPES)))
+    special = rnd.random() < 0.15
+    raw = [(rnd.choice([1, 3, 250, 10 ** 15, 2.5, 7.25]),
+            OrderedDict((k, _values(rnd, g, s[0], dt, special)) for k, s, dt in keys)) for _ in range(K)]
+    device = rnd.random() < 0.5
+    what = f"mpi seed {seed}: K={K} device={device} keys={[(k, s, str(d)) for k, s, d in keys]}"
+    host = copy.deepcopy(raw)
+    if device:
+        raw = [(n, OrderedDict((k, t.to(cuda_device)) for k, t in d.items())) for n, d in raw]
+    got = fedavg_mpi_aggregate(raw)
+    exp = orc.mpi_fedavg(host)
+    assert list(got) == list(exp), what
+    for k in exp:
+        gu.assert_same(got[k].cpu(), exp[k], f"{what} key {k}")
+
+
+@pytest.mark.parametrize("seed", list(range(_CASES_3)))
+def test_random_scaffold_mime_round_matches_the_oracle(seed, cuda_device):
+    """SCAFFOLD and Mime (3-tuples, agg_operator.py:100-133) on the real
+    kernels: random dtypes and lengths, host or device, both results and the
+    in-place update of client 0's control-variate tensors (SCAFFOLD)."""
+    rnd = random.Random(2000 + seed)
+    g = torch.Generator().manual_seed(2000 + seed)
+    opt = rnd.choice(["SCAFFOLD", "Mime"])
+    K = rnd.choice([1, 2, 3, 8, 33, 130])
+    budget = _ELEMS_PER_CASE // 4 // K
+    keys = []
+    for j in range(rnd.randint(1, 4)):
+        n = rnd.choice([x for x in _LENGTHS if x <= budget] or [1])
+        budget = max(1, budget - n)
+        keys.append((f"k{j}", (n,), rnd.choice([torch.float32, torch.bfloat16, torch.float64, torch.int64])))
+    mk = lambda: OrderedDict((k, _values(rnd, g, s[0], dt, False)) for k, s, dt in keys)  # noqa: E731
+    raw = [(rnd.choice([1, 4, 9, 2.5]), mk(), mk()) for _ in range(K)]
+    device = rnd.random() < 0.5
+    what = f"{opt} seed {seed}: K={K} device={device} keys={[(k, s, str(d)) for k, s, d in keys]}"
+    host = copy.deepcopy(raw)
+    if device:
+        raw = [(n, OrderedDict((k, t.to(cuda_device)) for k, t in a.items()),
+                OrderedDict((k, t.to(cuda_device)) for k, t in b.items())) for n, a, b in raw]
+    c0_got, c0_exp = list(raw[0][2].values()), list(host[0][2].values())
+    args = _Args(opt, None)
+    args.client_num_per_round = K
+    args.client_num_in_total = 4 * K
+    got = FedMLAggOperator.agg(args, raw)
+    exp = orc.agg(args, host)
+    assert isinstance(got, tuple) and len(got) == len(exp), what
+    for gd, ed in zip(got, exp):
+        assert list(gd) == list(ed), what
+        for k in ed:
+            gu.assert_same(gd[k].cpu(), ed[k], f"{what} key {k}")
+    for j, (a, e) in enumerate(zip(c0_got, c0_exp)):  # client 0's own tensors (SCAFFOLD `+=` into them)
+        gu.assert_same(a.cpu(), e, f"{what} client-0 tensor {j}")
