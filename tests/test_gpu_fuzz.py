@@ -9,7 +9,9 @@ then NaN / inf / -0.0 / denormal values.  FedMLAggOperator.agg must return
 the oracle's bits (agg_operator.py:33-63 restated in oracle/fedavg_oracle.py,
 pinned to the reference's fixtures), client 0's dict rebinding included.
 The same for the MPI simulation's term order (orc.mpi_fedavg) and for the
-SCAFFOLD / Mime 3-tuples, client 0's in-place control variates included.
+SCAFFOLD / Mime 3-tuples, client 0's in-place control variates included,
+and for three-round FedOptServer runs (five fused optimizers, parameter keys
+interleaved with buffer keys), optimizer state included.
 Seeded: a failure names its case and replays.
 """
 from __future__ import annotations
@@ -179,3 +181,68 @@ def test_random_scaffold_mime_round_matches_the_oracle(seed, cuda_device):
             gu.assert_same(gd[k].cpu(), ed[k], f"{what} key {k}")
     for j, (a, e) in enumerate(zip(c0_got, c0_exp)):  # client 0's own tensors (SCAFFOLD `+=` into them)
         gu.assert_same(a.cpu(), e, f"{what} client-0 tensor {j}")
+
+
+_FEDOPT = [("sgd", 0.0), ("sgd", 0.9), ("adam", 0.0), ("adamw", 0.0), ("adagrad", 0.0), ("rmsprop", 0.0)]
+
+
+@pytest.mark.parametrize("seed", list(range(60)))
+def test_random_fedopt_rounds_match_the_oracle(seed, cuda_device):
+    """FedOptServer (FedOptAggregator.py:81-125, fedopt_api.py:121-130) over
+    three rounds: a random optimizer, learning rate and client count, fp32
+    parameter keys interleaved with fp32 / bf16 / int64 buffer keys (so the
+    fused runs split at random places), random sample counts.  Parameters,
+    buffers and optimizer state bit-exact against the oracle (IEEE sqrt)."""
+    from fedml_amd.fedopt import FedOptServer
+
+    rnd = random.Random(3000 + seed)
+    g = torch.Generator().manual_seed(3000 + seed)
+    opt, mom = rnd.choice(_FEDOPT)
+    lr = rnd.choice([1.0, 0.5, 0.1, 0.01, 3e-4])
+    K = rnd.choice([1, 2, 3, 7, 16, 40, 129])
+    budget = (8 << 20) // K
+    entries, names = [], []
+    for j in range(rnd.randint(1, 6)):
+        n = rnd.choice([x for x in _LENGTHS if 0 < x <= budget] or [1])
+        budget = max(1, budget - n)
+        kind = rnd.choice(["p", "p", "p", "f32", "bf16", "i64"])
+        dt = {"p": torch.float32, "f32": torch.float32, "bf16": torch.bfloat16, "i64": torch.int64}[kind]
+        entries.append((f"k{j}", n, dt))
+        if kind == "p":
+            names.append(f"k{j}")
+    init = OrderedDict((k, _values(rnd, g, n, dt, False)) for k, n, dt in entries)
+    what = f"fedopt seed {seed}: {opt} m={mom} lr={lr} K={K} keys={[(k, n, str(d), k in names) for k, n, d in entries]}"
+    srv = FedOptServer(init, names, K, opt, lr, mom, cuda_device)
+    prev, state = init, {}
+    for r in range(3):
+        raw = [(rnd.choice([1, 5, 64, 2.5]), OrderedDict(
+            (k, (t + _values(rnd, g, t.numel(), t.dtype, False) * 0.1).to(t.dtype) if t.is_floating_point()
+             else _values(rnd, g, t.numel(), t.dtype, False)) for k, t in prev.items())) for _ in range(K)]
+        for i, (n, d) in enumerate(raw):
+            srv.add_local_trained_result(i, d, n)
+        out = OrderedDict((k, t.cpu().clone()) for k, t in srv.aggregate().items())
+        host = copy.deepcopy(raw)
+        if opt == "sgd":
+            exp = orc.fedopt_round(prev, names, host, lr, mom, state)
+        elif opt in ("adam", "adamw"):
+            exp = orc.fedopt_adam_round(prev, names, host, lr, state, r + 1, sqrt="ieee",
+                                        weight_decay=0.01 if opt == "adamw" else 0.0)
+        elif opt == "adagrad":
+            exp = orc.fedopt_adagrad_round(prev, names, host, lr, state, sqrt="ieee")
+        else:
+            exp = orc.fedopt_rmsprop_round(prev, names, host, lr, state, sqrt="ieee")
+        assert list(out) == list(exp), what
+        for k in exp:
+            gu.assert_same(out[k], exp[k], f"{what} round {r} key {k}")
+        st = srv.optimizer_state()
+        for k in names:
+            if opt == "sgd" and mom:
+                gu.assert_same(st["momentum_buffer"][k].cpu().reshape(-1), torch.from_numpy(state[k]).reshape(-1),
+                               f"{what} round {r} momentum {k}")
+            elif opt in ("adam", "adamw"):
+                gu.assert_same(st["exp_avg"][k].cpu().reshape(-1), torch.from_numpy(state[k][0]), f"{what} m {k}")
+                gu.assert_same(st["exp_avg_sq"][k].cpu().reshape(-1), torch.from_numpy(state[k][1]), f"{what} v {k}")
+            elif opt in ("adagrad", "rmsprop"):
+                name = "sum" if opt == "adagrad" else "square_avg"
+                gu.assert_same(st[name][k].cpu().reshape(-1), torch.from_numpy(state[k]), f"{what} {name} {k}")
+        prev = out
