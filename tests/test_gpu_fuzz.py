@@ -11,7 +11,9 @@ pinned to the reference's fixtures), client 0's dict rebinding included.
 The same for the MPI simulation's term order (orc.mpi_fedavg) and for the
 SCAFFOLD / Mime 3-tuples, client 0's in-place control variates included,
 and for three-round FedOptServer runs (five fused optimizers, parameter keys
-interleaved with buffer keys), optimizer state included.
+interleaved with buffer keys), optimizer state included, and for
+three-round runs of the cross-silo mirror (arrival order, odd updates, the
+server model on the host or the GPU).
 Seeded: a failure names its case and replays.
 """
 from __future__ import annotations
@@ -246,3 +248,74 @@ def test_random_fedopt_rounds_match_the_oracle(seed, cuda_device):
                 name = "sum" if opt == "adagrad" else "square_avg"
                 gu.assert_same(st[name][k].cpu().reshape(-1), torch.from_numpy(state[k]), f"{what} {name} {k}")
         prev = out
+
+
+class _Holder(torch.nn.Module):
+    """A server model whose state dict is exactly the fuzz case's keys."""
+
+    def __init__(self, entries):
+        super().__init__()
+        for k, s, dt in entries:
+            self.register_buffer(k, torch.zeros(s, dtype=dt))
+
+
+@pytest.mark.parametrize("seed", list(range(60)))
+def test_random_cross_silo_rounds_match_the_oracle(seed, cuda_device):
+    """The cross-silo mirror (fedml_aggregator.py:58-106) over three rounds on
+    one server: random layout, client count and arrival order; now and then an
+    update with an extra key (moved key by key), a non-contiguous tensor, one
+    already on the GPU, or a value rebound after arrival (a hook); the server
+    model on the host (the buffer-wise D2H) or on the GPU.  Every round's
+    average and the model's state after set_model_params match the oracle."""
+    from fedml_amd.cross_silo import FedMLAggregator
+    from fedml_amd.server_aggregator import MI355XServerAggregator
+
+    rnd = random.Random(4000 + seed)
+    g = torch.Generator().manual_seed(4000 + seed)
+    opt = rnd.choice(["FedAvg", "FedAvg", "FedProx", "FedAvg_seq"])
+    K = rnd.choice([1, 2, 3, 6, 17, 40])
+    budget = (12 << 20) // K
+    entries = []
+    for j in range(rnd.randint(1, 6)):
+        n = rnd.choice([x for x in _LENGTHS if x <= budget] or [1])
+        budget = max(1, budget - n)
+        shape = (n,) if n < 4 or n % 2 else (2, n // 2)
+        entries.append((f"k{j}", shape, rnd.choice(_SUMMED)))
+    model = _Holder(entries)
+    on_gpu = rnd.random() < 0.4
+    if on_gpu:
+        model = model.to(cuda_device)
+    args = _Args(opt, None)
+    server = FedMLAggregator(None, None, 0, {}, {}, {}, K, cuda_device, args, MI355XServerAggregator(model, args))
+    what = f"cross-silo seed {seed}: {opt} K={K} model_on_gpu={on_gpu} keys={[(k, s, str(d)) for k, s, d in entries]}"
+    for r in range(3):
+        raw, quirks = [], []
+        for i in range(K):
+            d = OrderedDict((k, _values(rnd, g, int(np.prod(s)), dt, False).reshape(s)) for k, s, dt in entries)
+            q = rnd.choice(["plain"] * 8 + ["extra", "strided", "device", "hook"])
+            if q == "extra" and i > 0:
+                d["unused.extra"] = torch.ones(3)
+            elif q == "strided":
+                k, s, dt = rnd.choice(entries)
+                d[k] = torch.stack([d[k], d[k]], -1)[..., 0]  # same values, non-contiguous
+            quirks.append(q)
+            raw.append((rnd.choice([1, 3, 64, 2.5]), d))
+        host = copy.deepcopy(raw)
+        for i in rnd.sample(range(K), K):
+            n, d = raw[i]
+            if quirks[i] == "device":
+                d = OrderedDict((k, t.to(cuda_device)) for k, t in d.items())
+            server.add_local_trained_result(i, d, n)
+            if quirks[i] == "hook":
+                k = rnd.choice(entries)[0]
+                d[k] = d[k] * 2 if d[k].is_floating_point() else d[k] + 1
+                host[i][1][k] = host[i][1][k] * 2 if host[i][1][k].is_floating_point() else host[i][1][k] + 1
+        assert server.check_whether_all_receive(), what
+        exp = orc.agg(_Args(opt, None), host)
+        averaged, _, _ = server.aggregate()
+        tag = f"{what} round {r} quirks={quirks}"
+        for k in exp:
+            gu.assert_same(averaged[k].cpu(), exp[k], f"{tag} key {k}")
+        sd = model.state_dict()
+        for k, s, dt in entries:
+            gu.assert_same(sd[k].cpu(), torch.zeros(s, dtype=dt).copy_(exp[k]), f"{tag} model {k}")
