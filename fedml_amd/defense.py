@@ -148,17 +148,24 @@ def coordinate_wise_median(raw_client_grad_list: List[Tuple[float, "OrderedDict"
     dev = t0.device if t0.is_cuda else (torch.device(device) if device is not None else
                                         torch.device("cuda", torch.cuda.current_device()))
     dts = {dicts[0][k].dtype for k in wkeys}
-    # vectorize_weight's torch.cat promotes to one dtype: fp32 (with integer
-    # weights riding as fl32(v)), or a 16-bit model's own bf16 / f16
-    if dts <= {torch.float32, torch.int64, torch.int32, torch.bool} and torch.float32 in dts:
+    floats = dts & {torch.float32, torch.bfloat16, torch.float16}
+    ints = dts - floats
+    # vectorize_weight's torch.cat promotes to one dtype: fp32 when any key is
+    # fp32 or two float widths meet (bf16 + f16 -> fp32; the 16-bit keys widen
+    # exactly, integer weights ride as fl32(v)), or a 16-bit model's own bf16 /
+    # f16.  The median is one of its inputs, so selecting in the promoted
+    # dtype is exact.
+    if (torch.float32 in floats or len(floats) > 1) and ints <= {torch.int64, torch.int32, torch.bool}:
         row_dt = torch.float32
     elif dts in ({torch.bfloat16}, {torch.float16}):
         row_dt = next(iter(dts))
     else:
-        raise NotImplementedError("wise_median on the GPU takes fp32 weights (integer keys allowed), or all-bf16 "
-                                  f"/ all-f16 weights (got {sorted(map(str, dts))})")
+        raise NotImplementedError("wise_median on the GPU takes fp32 or mixed-width float weights (integer keys "
+                                  f"allowed), or all-bf16 / all-f16 weights (got {sorted(map(str, dts))})")
     with torch.cuda.device(dev):
-        layout = [(k, tuple(dicts[0][k].shape), dicts[0][k].dtype) for k in wkeys]
+        # 16-bit keys of a promoted model are declared fp32: put() widens them
+        layout = [(k, tuple(dicts[0][k].shape),
+                   row_dt if dicts[0][k].dtype in floats else dicts[0][k].dtype) for k in wkeys]
         bucket = ClientBucket(layout, K, dev)
         for i in range(K):
             bucket.put(i, {k: dicts[i][k] for k in wkeys}, 1)
