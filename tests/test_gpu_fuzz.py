@@ -14,7 +14,8 @@ and for three-round FedOptServer runs (five fused optimizers, parameter keys
 interleaved with buffer keys), optimizer state included, and for
 three-round runs of the cross-silo mirror (arrival order, odd updates, the
 server model on the host or the GPU), and for defended rounds (median,
-trimmed mean, Krum / multi-Krum, norm-diff clipping).
+trimmed mean, Krum / multi-Krum, norm-diff clipping), and with the round
+spread over 2-4 shards (args.fedagg_devices).
 Seeded: a failure names its case and replays.
 """
 from __future__ import annotations
@@ -266,7 +267,8 @@ def test_random_cross_silo_rounds_match_the_oracle(seed, cuda_device):
     one server: random layout, client count and arrival order; now and then an
     update with an extra key (moved key by key), a non-contiguous tensor, one
     already on the GPU, or a value rebound after arrival (a hook); the server
-    model on the host (the buffer-wise D2H) or on the GPU.  Every round's
+    model on the host (the buffer-wise D2H) or on the GPU; one to three
+    shards (args.fedagg_devices).  Every round's
     average and the model's state after set_model_params match the oracle."""
     from fedml_amd.cross_silo import FedMLAggregator
     from fedml_amd.server_aggregator import MI355XServerAggregator
@@ -287,8 +289,11 @@ def test_random_cross_silo_rounds_match_the_oracle(seed, cuda_device):
     if on_gpu:
         model = model.to(cuda_device)
     args = _Args(opt, None)
+    G = random.Random(seed + 99).choice([1, 1, 2, 3])  # shards of a MultiDeviceBucket, one GPU standing in
+    if G > 1:
+        args.fedagg_devices = [cuda_device] * G
     server = FedMLAggregator(None, None, 0, {}, {}, {}, K, cuda_device, args, MI355XServerAggregator(model, args))
-    what = f"cross-silo seed {seed}: {opt} K={K} model_on_gpu={on_gpu} keys={[(k, s, str(d)) for k, s, d in entries]}"
+    what = f"cross-silo seed {seed}: G={G} {opt} K={K} model_on_gpu={on_gpu} keys={[(k, s, str(d)) for k, s, d in entries]}"
     for r in range(3):
         raw, quirks = [], []
         for i in range(K):
@@ -396,3 +401,27 @@ def test_random_defended_round_matches_the_oracle(seed, cuda_device):
     assert list(got) == list(exp), what
     for k in exp:
         gu.assert_same(got[k].cpu(), exp[k].reshape(got[k].shape), f"{what} key {k}")
+
+
+@pytest.mark.parametrize("seed", list(range(40)))
+def test_random_multidevice_round_matches_the_oracle(seed, cuda_device):
+    """The same random rounds with args.fedagg_devices listing 2-4 shards (one
+    GPU standing in for several, as tests/test_gpu_multidev.py): whole keys
+    per shard, each reduced where it lives (fedml_amd.multidev)."""
+    opt, K, keys, raw, acc, device = _case(6000 + seed)
+    G = random.Random(seed).choice([2, 3, 4])
+    what = f"multidev seed {seed}: G={G} {opt} K={K} acc={acc} device={device} keys={[(k, s, str(d)) for k, s, d in keys]}"
+    host = copy.deepcopy(raw)
+    if device:
+        raw = [(n, OrderedDict((k, t.to(cuda_device)) for k, t in d.items())) for n, d in raw]
+    args = _Args(opt, acc)
+    args.fedagg_devices = [cuda_device] * G
+    got = FedMLAggOperator.agg(args, raw)
+    exp = orc.agg(_Args(opt, None), copy.deepcopy(host))
+    assert list(got) == list(exp), what
+    ws = [n / sum(n for n, _ in host) for n, _ in host]
+    for k, s, dt in keys:
+        e = exp[k]
+        if acc == "fp32" and dt in (torch.bfloat16, torch.float16):
+            e = orc.wsum_acc32([d[k] for _, d in host], ws)
+        gu.assert_same(got[k].cpu(), e, f"{what} key {k}")
