@@ -14,7 +14,8 @@ that are pure reductions over the client axis.
                 .view() raises RuntimeError — exactly what FedML does.
                 The median itself is fedagg_median (one launch over the
                 whole weight row; fp32 rows, or bf16 / f16 rows for 16-bit
-                models, whose torch.cat stays 16-bit).
+                models, whose torch.cat stays 16-bit; a mixed-width model's
+                16-bit keys are widened into fp32 rows, as torch.cat promotes).
 
 "trimmed_mean"  CoordinateWiseTrimmedMeanDefense.defend_before_aggregation
                 (coordinate_wise_trimmed_mean_defense.py:19-26 ->
@@ -132,6 +133,24 @@ def median_rows(d_ptrs: torch.Tensor, K: int, N: int, out: torch.Tensor, aligned
                                       nat.stream_handle()), "median")
 
 
+def median_row_dtype(dts) -> torch.dtype:
+    """The dtype of the median's rows for weight keys of dtypes `dts`:
+    vectorize_weight's torch.cat promotes to one dtype, fp32 when any key is
+    fp32 or two float widths meet (bf16 + f16 -> fp32; the 16-bit keys widen
+    exactly, integer weights ride as fl32(v)), or a 16-bit model's own bf16 /
+    f16.  The median is one of its inputs, so selecting in the promoted dtype
+    is exact.  Other mixes (all-integer, 16-bit floats with integers) raise."""
+    dts = set(dts)
+    floats = dts & {torch.float32, torch.bfloat16, torch.float16}
+    ints = dts - floats
+    if (torch.float32 in floats or len(floats) > 1) and ints <= {torch.int64, torch.int32, torch.bool}:
+        return torch.float32
+    if dts in ({torch.bfloat16}, {torch.float16}):
+        return next(iter(dts))
+    raise NotImplementedError("wise_median on the GPU takes fp32 or mixed-width float weights (integer keys "
+                              f"allowed), or all-bf16 / all-f16 weights (got {sorted(map(str, dts))})")
+
+
 def coordinate_wise_median(raw_client_grad_list: List[Tuple[float, "OrderedDict"]], device=None
                            ) -> "OrderedDict":
     """CoordinateWiseMedianDefense.defend_on_aggregation on the GPU."""
@@ -148,20 +167,8 @@ def coordinate_wise_median(raw_client_grad_list: List[Tuple[float, "OrderedDict"
     dev = t0.device if t0.is_cuda else (torch.device(device) if device is not None else
                                         torch.device("cuda", torch.cuda.current_device()))
     dts = {dicts[0][k].dtype for k in wkeys}
+    row_dt = median_row_dtype(dts)
     floats = dts & {torch.float32, torch.bfloat16, torch.float16}
-    ints = dts - floats
-    # vectorize_weight's torch.cat promotes to one dtype: fp32 when any key is
-    # fp32 or two float widths meet (bf16 + f16 -> fp32; the 16-bit keys widen
-    # exactly, integer weights ride as fl32(v)), or a 16-bit model's own bf16 /
-    # f16.  The median is one of its inputs, so selecting in the promoted
-    # dtype is exact.
-    if (torch.float32 in floats or len(floats) > 1) and ints <= {torch.int64, torch.int32, torch.bool}:
-        row_dt = torch.float32
-    elif dts in ({torch.bfloat16}, {torch.float16}):
-        row_dt = next(iter(dts))
-    else:
-        raise NotImplementedError("wise_median on the GPU takes fp32 or mixed-width float weights (integer keys "
-                                  f"allowed), or all-bf16 / all-f16 weights (got {sorted(map(str, dts))})")
     with torch.cuda.device(dev):
         # 16-bit keys of a promoted model are declared fp32: put() widens them
         layout = [(k, tuple(dicts[0][k].shape),

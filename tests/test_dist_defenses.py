@@ -377,3 +377,22 @@ def test_defenses_refuse_a_round_spread_over_gpus():
     dfn._one_device(d, ["a.weight"], "krum")  # one device: fine
     with pytest.raises(NotImplementedError, match="wise_median"):
         dfn.coordinate_wise_median([(1, d), (1, d)])
+
+
+def test_median_row_dtype_follows_torch_cat():
+    """The median's row dtype is torch.cat's promoted dtype for every mix of
+    weight-key dtypes it accepts; the mixes it refuses are the ones whose
+    promotion is not exact in fp32 rows (16-bit floats with integers) or has
+    no float at all."""
+    import itertools
+
+    pool = [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32, torch.bool]
+    for r in range(1, 4):
+        for dts in itertools.combinations(pool, r):
+            cat = torch.cat([torch.zeros(1, dtype=d) for d in dts]).dtype
+            floats = set(dts) & {torch.float32, torch.bfloat16, torch.float16}
+            if not floats or (floats <= {torch.bfloat16, torch.float16} and len(floats) == 1 and len(dts) > 1):
+                with pytest.raises(NotImplementedError, match="wise_median"):
+                    dfn.median_row_dtype(dts)
+                continue
+            assert dfn.median_row_dtype(dts) == cat, dts
