@@ -21,6 +21,7 @@ Seeded: a failure names its case and replays.
 from __future__ import annotations
 
 import copy
+import os
 import random
 from collections import OrderedDict
 
@@ -39,8 +40,10 @@ _LENGTHS = [0, 1, 3, 31, 255, 256, 1023, 1024, 4095, 4096, 4097, 16383, 32767, 3
 _WEIGHTED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32, torch.uint8,
              torch.bool]
 _SUMMED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64]
-_CASES = 160
-_CASES_3 = 120  # MPI order, SCAFFOLD / Mime tuples
+# FEDAGG_FUZZ_SCALE=n multiplies every case count (a longer campaign; new seeds come after the defaults)
+_SCALE = max(1, int(os.environ.get("FEDAGG_FUZZ_SCALE", "1")))
+_CASES = 160 * _SCALE
+_CASES_3 = 120 * _SCALE  # MPI order, SCAFFOLD / Mime tuples
 _ELEMS_PER_CASE = 24 << 20  # K x elements, so the oracle's numpy loop stays short
 
 
@@ -190,7 +193,7 @@ def test_random_scaffold_mime_round_matches_the_oracle(seed, cuda_device):
 _FEDOPT = [("sgd", 0.0), ("sgd", 0.9), ("adam", 0.0), ("adamw", 0.0), ("adagrad", 0.0), ("rmsprop", 0.0)]
 
 
-@pytest.mark.parametrize("seed", list(range(60)))
+@pytest.mark.parametrize("seed", list(range(60 * _SCALE)))
 def test_random_fedopt_rounds_match_the_oracle(seed, cuda_device):
     """FedOptServer (FedOptAggregator.py:81-125, fedopt_api.py:121-130) over
     three rounds: a random optimizer, learning rate and client count, fp32
@@ -261,7 +264,7 @@ class _Holder(torch.nn.Module):
             self.register_buffer(k, torch.zeros(s, dtype=dt))
 
 
-@pytest.mark.parametrize("seed", list(range(60)))
+@pytest.mark.parametrize("seed", list(range(60 * _SCALE)))
 def test_random_cross_silo_rounds_match_the_oracle(seed, cuda_device):
     """The cross-silo mirror (fedml_aggregator.py:58-106) over three rounds on
     one server: random layout, client count and arrival order; now and then an
@@ -336,7 +339,7 @@ class _DefArgs:
             setattr(self, k, v)
 
 
-@pytest.mark.parametrize("seed", list(range(60)))
+@pytest.mark.parametrize("seed", list(range(60 * _SCALE)))
 def test_random_defended_round_matches_the_oracle(seed, cuda_device):
     """The defenses on the hot path's kernels (fedml_defender.py:131-171):
     coordinate-wise median (mixed 16/32-bit weight keys, NaN now and then),
@@ -403,7 +406,7 @@ def test_random_defended_round_matches_the_oracle(seed, cuda_device):
         gu.assert_same(got[k].cpu(), exp[k].reshape(got[k].shape), f"{what} key {k}")
 
 
-@pytest.mark.parametrize("seed", list(range(40)))
+@pytest.mark.parametrize("seed", list(range(40 * _SCALE)))
 def test_random_multidevice_round_matches_the_oracle(seed, cuda_device):
     """The same random rounds with args.fedagg_devices listing 2-4 shards (one
     GPU standing in for several, as tests/test_gpu_multidev.py): whole keys
