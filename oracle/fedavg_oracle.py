@@ -618,10 +618,22 @@ def _is_weight_param(k: str) -> bool:
 def lower_median_cols(stack: np.ndarray) -> np.ndarray:
     """torch.median(x, dim=-1).values for x = stack.T ([M, K] -> [M]): element
     (K-1)//2 of each sorted column; a column with a NaN yields its first NaN
-    (ATen's median: find_if(isnan) before nth_element)."""
+    (ATen's median: find_if(isnan) before nth_element).
+
+    A zero median in a column holding both -0.0 and +0.0 takes its sign from
+    the IEEE total order (-0 < +0), as the GPU kernels do.  torch's
+    nth_element compares with `<`, so there the sign of that zero follows the
+    column's input order (np.sort's choice is arbitrary as well): PARITY
+    UNPINNED for that corner, the value (zero) is the same."""
     K = stack.shape[0]
+    r = (K - 1) // 2
     srt = np.sort(stack, axis=0)  # NaNs sort last; they are overridden below
-    med = srt[(K - 1) // 2].astype(stack.dtype)
+    med = srt[r].astype(stack.dtype)
+    zc = np.nonzero(med == 0)[0]
+    if zc.size:  # rank r falls among the column's zeros: -0 if it is within the negative zeros
+        sub = stack[:, zc]
+        below = (sub < 0).sum(axis=0) + ((sub == 0) & np.signbit(sub)).sum(axis=0)
+        med[zc] = np.where(r < below, -0.0, 0.0).astype(stack.dtype)
     isn = np.isnan(stack)
     anyn = isn.any(axis=0)
     if anyn.any():

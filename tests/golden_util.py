@@ -63,15 +63,18 @@ def assert_same(actual: torch.Tensor, expected: torch.Tensor, what: str = "") ->
     assert actual.dtype == expected.dtype, f"{what}: dtype {actual.dtype} != {expected.dtype}"
     assert tuple(actual.shape) == tuple(expected.shape), f"{what}: shape {actual.shape} != {expected.shape}"
     a, e = bits(actual).ravel(), bits(expected).ravel()
+    pos = np.arange(a.size)
     if actual.is_floating_point():
         an = torch.isnan(actual.detach().cpu().float()).numpy().ravel()
         en = torch.isnan(expected.float()).numpy().ravel()
         assert np.array_equal(an, en), f"{what}: NaN positions differ"
-        a, e = a[~an], e[~en]
+        a, e, pos = a[~an], e[~en], pos[~an]
     bad = np.nonzero(a != e)[0]
-    assert bad.size == 0, (f"{what}: {bad.size} of {a.size} elements differ; first at {bad[0]}: "
-                           f"got {actual.detach().cpu().reshape(-1)[bad[0]].item()!r} "
-                           f"want {expected.reshape(-1)[bad[0]].item()!r}")
+    if bad.size:
+        j = int(pos[bad[0]])  # the element's index in the tensor (NaNs were left out of a / e)
+        raise AssertionError(f"{what}: {bad.size} of {a.size} elements differ; first at {j}: "
+                             f"got {actual.detach().cpu().reshape(-1)[j].item()!r} "
+                             f"want {expected.reshape(-1)[j].item()!r}")
 
 
 def assert_groups(actual, meta, arrays, what="") -> None:
