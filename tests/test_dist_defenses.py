@@ -396,3 +396,15 @@ def test_median_row_dtype_follows_torch_cat():
                     dfn.median_row_dtype(dts)
                 continue
             assert dfn.median_row_dtype(dts) == cat, dts
+
+
+def test_oracle_median_zero_ties_take_the_total_order():
+    """The oracle's lower median picks -0.0 / +0.0 by the IEEE total order when
+    the rank falls among both zeros, whatever the input order."""
+    from oracle import fedavg_oracle as orc
+
+    cols = [([0.0, -0.0, 1.0], 0.0), ([-0.0, 0.0, 1.0], 0.0), ([0.0, -0.0, -1.0], -0.0), ([-1.0, 0.0, -0.0], -0.0),
+            ([-0.0, -0.0, 0.0, 0.0], -0.0), ([0.0, 0.0, -0.0, 2.0], 0.0), ([2.0, 1.0, 3.0], 2.0)]
+    for vals, want in cols:
+        got = orc.lower_median_cols(np.array(vals, dtype=np.float32).reshape(-1, 1))[0]
+        assert got == want and np.signbit(got) == np.signbit(want), (vals, got)

@@ -229,3 +229,33 @@ def test_median_16bit_lanes_first_nan_payload(dtype, K, N, cuda_device):
         assert int(o16[3]) & 0xffff == nan | 0x5
     exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
     gu.assert_same(out.cpu(), exp, f"median {dtype} K={K} N={N}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K", [2, 3, 64, 127, 128, 129, 300, 512, 1100])
+def test_median_signed_zero_ties_take_the_total_order(dtype, K, cuda_device):
+    """Columns whose lower median falls among a mix of -0.0 and +0.0: every
+    kernel family returns the zero of the IEEE total order (-0 < +0), which
+    the oracle restates (torch's nth_element leaves that sign to the column's
+    input order: DESIGN.md §5b, unpinned).  Columns vary the number of
+    negatives, negative zeros and positive zeros around the rank, in both
+    input orders, aligned (packed 16-bit kernels) and not."""
+    N = 1_031
+    g = torch.Generator().manual_seed(K)
+    rows = torch.zeros(K, 1_088, dtype=torch.float32)
+    for c in range(N):
+        n_neg = int(torch.randint(0, K // 2 + 1, (1,), generator=g))
+        n_nz = int(torch.randint(0, K - n_neg + 1, (1,), generator=g))
+        col = torch.cat([-torch.rand(n_neg, generator=g) - 0.5, torch.full((n_nz,), -0.0),
+                         torch.zeros(K - n_neg - n_nz), ])
+        col[n_neg + n_nz:][: max(0, K - n_neg - n_nz - K // 3)] = torch.rand(max(0, K - n_neg - n_nz - K // 3),
+                                                                             generator=g) + 0.5
+        rows[:, c] = col[torch.randperm(K, generator=g)] if c % 2 else col.flip(0)
+    rows = rows.to(dtype).to(cuda_device)[:, :N]
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(1_088, dtype=dtype, device=cuda_device)[:N]
+    dfn.median_rows(d_ptrs, K, N, out, aligned=True)
+    exp = torch.from_numpy(orc.lower_median_cols(rows.float().cpu().numpy())).to(dtype)
+    zeros = int((exp == 0).sum())
+    assert zeros > N // 10, zeros  # the case exercises the ties
+    gu.assert_same(out.cpu(), exp, f"median {dtype} K={K}")
