@@ -42,6 +42,8 @@ _WEIGHTED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.
 _SUMMED = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64]
 # FEDAGG_FUZZ_SCALE=n multiplies every case count (a longer campaign; new seeds come after the defaults)
 _SCALE = max(1, int(os.environ.get("FEDAGG_FUZZ_SCALE", "1")))
+# FEDAGG_FUZZ_SEED0=s starts every seed range at s (a campaign over fresh seeds)
+_SEED0 = int(os.environ.get("FEDAGG_FUZZ_SEED0", "0"))
 _CASES = 160 * _SCALE
 _CASES_3 = 120 * _SCALE  # MPI order, SCAFFOLD / Mime tuples
 _ELEMS_PER_CASE = 24 << 20  # K x elements, so the oracle's numpy loop stays short
@@ -96,7 +98,7 @@ def _case(seed: int):
     return opt, K, keys, raw, acc, device
 
 
-@pytest.mark.parametrize("seed", list(range(_CASES)))
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + _CASES)))
 def test_random_round_matches_the_oracle(seed, cuda_device):
     opt, K, keys, raw, acc, device = _case(seed)
     what = f"seed {seed}: {opt} K={K} acc={acc} device={device} keys={[(k, s, str(d)) for k, s, d in keys]}"
@@ -121,7 +123,7 @@ def test_random_round_matches_the_oracle(seed, cuda_device):
 _MPI_DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64]
 
 
-@pytest.mark.parametrize("seed", list(range(_CASES_3)))
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + _CASES_3)))
 def test_random_mpi_round_matches_the_oracle(seed, cuda_device):
     """The MPI simulation's term order (FedAVGAggregator.py:99-116) through
     fedml_amd.simulation.fedavg_mpi_aggregate, random shapes, dtypes, sample
@@ -152,7 +154,7 @@ def test_random_mpi_round_matches_the_oracle(seed, cuda_device):
         gu.assert_same(got[k].cpu(), exp[k], f"{what} key {k}")
 
 
-@pytest.mark.parametrize("seed", list(range(_CASES_3)))
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + _CASES_3)))
 def test_random_scaffold_mime_round_matches_the_oracle(seed, cuda_device):
     """SCAFFOLD and Mime (3-tuples, agg_operator.py:100-133) on the real
     kernels: random dtypes and lengths, host or device, both results and the
@@ -193,7 +195,7 @@ def test_random_scaffold_mime_round_matches_the_oracle(seed, cuda_device):
 _FEDOPT = [("sgd", 0.0), ("sgd", 0.9), ("adam", 0.0), ("adamw", 0.0), ("adagrad", 0.0), ("rmsprop", 0.0)]
 
 
-@pytest.mark.parametrize("seed", list(range(60 * _SCALE)))
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + 60 * _SCALE)))
 def test_random_fedopt_rounds_match_the_oracle(seed, cuda_device):
     """FedOptServer (FedOptAggregator.py:81-125, fedopt_api.py:121-130) over
     three rounds: a random optimizer, learning rate and client count, fp32
@@ -264,7 +266,7 @@ class _Holder(torch.nn.Module):
             self.register_buffer(k, torch.zeros(s, dtype=dt))
 
 
-@pytest.mark.parametrize("seed", list(range(60 * _SCALE)))
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + 60 * _SCALE)))
 def test_random_cross_silo_rounds_match_the_oracle(seed, cuda_device):
     """The cross-silo mirror (fedml_aggregator.py:58-106) over three rounds on
     one server: random layout, client count and arrival order; now and then an
@@ -339,7 +341,7 @@ class _DefArgs:
             setattr(self, k, v)
 
 
-@pytest.mark.parametrize("seed", list(range(60 * _SCALE)))
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + 60 * _SCALE)))
 def test_random_defended_round_matches_the_oracle(seed, cuda_device):
     """The defenses on the hot path's kernels (fedml_defender.py:131-171):
     coordinate-wise median (mixed 16/32-bit weight keys, NaN now and then),
@@ -406,7 +408,7 @@ def test_random_defended_round_matches_the_oracle(seed, cuda_device):
         gu.assert_same(got[k].cpu(), exp[k].reshape(got[k].shape), f"{what} key {k}")
 
 
-@pytest.mark.parametrize("seed", list(range(40 * _SCALE)))
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + 40 * _SCALE)))
 def test_random_multidevice_round_matches_the_oracle(seed, cuda_device):
     """The same random rounds with args.fedagg_devices listing 2-4 shards (one
     GPU standing in for several, as tests/test_gpu_multidev.py): whole keys
