@@ -15,7 +15,8 @@ interleaved with buffer keys), optimizer state included, and for
 three-round runs of the cross-silo mirror (arrival order, odd updates, the
 server model on the host or the GPU), and for defended rounds (median,
 trimmed mean, Krum / multi-Krum, norm-diff clipping), and with the round
-spread over 2-4 shards (args.fedagg_devices).
+spread over 2-4 shards (args.fedagg_devices), and with non-contiguous,
+unaligned and nn.Parameter client tensors.
 Seeded: a failure names its case and replays.
 """
 from __future__ import annotations
@@ -430,3 +431,41 @@ def test_random_multidevice_round_matches_the_oracle(seed, cuda_device):
         if acc == "fp32" and dt in (torch.bfloat16, torch.float16):
             e = orc.wsum_acc32([d[k] for _, d in host], ws)
         gu.assert_same(got[k].cpu(), e, f"{what} key {k}")
+
+
+def _odd(rnd: random.Random, t: torch.Tensor) -> torch.Tensor:
+    """The same values in an unusual tensor: non-contiguous, at an odd storage
+    offset (an unaligned pointer), or an nn.Parameter (a tensor subclass)."""
+    kind = rnd.choice(["strided", "offset", "param"])
+    if kind == "strided":
+        return torch.stack([t, t], -1)[..., 0]
+    if kind == "offset":
+        big = torch.empty(t.numel() + 3, dtype=t.dtype, device=t.device)
+        big[3:].copy_(t.reshape(-1))
+        return big[3:].view(t.shape)
+    if not t.is_floating_point():
+        return t
+    return torch.nn.Parameter(t.clone(), requires_grad=False)
+
+
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + 60 * _SCALE)))
+def test_random_round_with_odd_tensors_matches_the_oracle(seed, cuda_device):
+    """The random rounds again with a fifth of the client tensors replaced by
+    non-contiguous views, unaligned views or nn.Parameters (the native walker
+    declines those; the reference takes them as they are)."""
+    opt, K, keys, raw, acc, device = _case(7000 + seed)
+    rnd = random.Random(seed)
+    what = f"odd seed {seed}: {opt} K={K} acc={acc} device={device} keys={[(k, s, str(d)) for k, s, d in keys]}"
+    host = copy.deepcopy(raw)
+    if device:
+        raw = [(n, OrderedDict((k, t.to(cuda_device)) for k, t in d.items())) for n, d in raw]
+    raw = [(n, OrderedDict((k, _odd(rnd, t) if rnd.random() < 0.2 else t) for k, t in d.items())) for n, d in raw]
+    got = FedMLAggOperator.agg(_Args(opt, acc), raw)
+    exp = orc.agg(_Args(opt, None), copy.deepcopy(host))
+    assert list(got) == list(exp), what
+    ws = [n / sum(n for n, _ in host) for n, _ in host]
+    for k, s, dt in keys:
+        e = exp[k]
+        if acc == "fp32" and dt in (torch.bfloat16, torch.float16):
+            e = orc.wsum_acc32([d[k] for _, d in host], ws)
+        gu.assert_same(got[k].detach().cpu(), e, f"{what} key {k}")
