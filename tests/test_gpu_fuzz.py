@@ -16,7 +16,8 @@ three-round runs of the cross-silo mirror (arrival order, odd updates, the
 server model on the host or the GPU), and for defended rounds (median,
 trimmed mean, Krum / multi-Krum, norm-diff clipping), and with the round
 spread over 2-4 shards (args.fedagg_devices), and with non-contiguous,
-unaligned and nn.Parameter client tensors.
+unaligned and nn.Parameter client tensors, and ClientBucket rounds fed by
+put / device put / FAGG messages.
 Seeded: a failure names its case and replays.
 """
 from __future__ import annotations
@@ -469,3 +470,62 @@ def test_random_round_with_odd_tensors_matches_the_oracle(seed, cuda_device):
         if acc == "fp32" and dt in (torch.bfloat16, torch.float16):
             e = orc.wsum_acc32([d[k] for _, d in host], ws)
         gu.assert_same(got[k].detach().cpu(), e, f"{what} key {k}")
+
+
+@pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + 40 * _SCALE)))
+def test_random_bucket_rounds_match_the_oracle(seed, cuda_device):
+    """ClientBucket itself over three rounds on the same slots: each client
+    arrives in random order through put() (host dict), put() of a device
+    dict, or put_encoded() of a FAGG message (pageable or pinned), now and
+    then through reduce_to_host; the fp32 accumulation mode too.  FedAvg of
+    the slots matches the oracle (integer keys promoted into the fp32 rows,
+    as the reference's int64 * float gives float32)."""
+    from fedml_amd import wire
+    from fedml_amd.bucket import ClientBucket
+
+    rnd = random.Random(8000 + seed)
+    g = torch.Generator().manual_seed(8000 + seed)
+    K = rnd.choice([1, 2, 5, 16, 33, 100])
+    budget = (8 << 20) // K
+    entries = []
+    for j in range(rnd.randint(1, 5)):
+        n = rnd.choice([x for x in _LENGTHS if x <= budget] or [1])
+        budget = max(1, budget - n)
+        shape = (n,) if n < 4 or n % 2 else (n // 2, 2)
+        entries.append((f"k{j}", shape, rnd.choice([torch.float32, torch.bfloat16, torch.float16, torch.float64,
+                                                    torch.int64])))
+    acc = rnd.choice(["reference", "reference", "fp32"])
+    bucket = ClientBucket(entries, K, cuda_device, low_precision_acc=acc)
+    what = f"bucket seed {seed}: K={K} acc={acc} keys={[(k, s, str(d)) for k, s, d in entries]}"
+    for r in range(3):
+        raw = [(rnd.choice([1, 9, 250, 3.5]),
+                OrderedDict((k, _values(rnd, g, int(np.prod(s)), dt, rnd.random() < 0.1).reshape(s))
+                            for k, s, dt in entries)) for _ in range(K)]
+        hows = []
+        for i in rnd.sample(range(K), K):
+            n, d = raw[i]
+            how = rnd.choice(["put", "device", "wire", "wire_pinned"])
+            hows.append(how)
+            if how == "put":
+                bucket.put(i, d, n)
+            elif how == "device":
+                bucket.put(i, OrderedDict((k, t.to(cuda_device)) for k, t in d.items()), n)
+            else:
+                m = wire.encode(d, n)
+                if how == "wire_pinned":
+                    t = torch.empty(len(m), dtype=torch.uint8).pin_memory()
+                    t.numpy()[:] = np.frombuffer(m, dtype=np.uint8)
+                    m = t.numpy()
+                bucket.put_encoded(i, m)
+                bucket.wait_ingest()  # the receive buffer is reused by the next message
+        to_host = rnd.random() < 0.3
+        res = bucket.reduce_to_host(bucket.weights([n for n, _ in raw])) if to_host else bucket.aggregate()
+        exp = orc.agg(_Args("FedAvg", None), copy.deepcopy(raw))
+        ws = [n / sum(n for n, _ in raw) for n, _ in raw]
+        tag = f"{what} round {r} to_host={to_host}"
+        assert list(res) == list(exp), tag
+        for k, s, dt in entries:
+            e = exp[k]
+            if acc == "fp32" and dt in (torch.bfloat16, torch.float16):
+                e = orc.wsum_acc32([d[k] for _, d in raw], ws)
+            gu.assert_same(res[k].cpu(), e, f"{tag} key {k}")
