@@ -523,17 +523,20 @@ class ClientBucket:
                 if self._side is None:
                     self._side = torch.cuda.Stream(self.device)
                 self._side.wait_stream(cur)
+            # streams passed explicitly (no stream context per launch: ~6 us
+            # each, which a one-process round over G GPUs pays G times before
+            # the last device starts)
             for dt, g in self.groups.items():
                 if g.length == 0:
                     continue
                 ev = events.get(dt) if events else None
-                with torch.cuda.stream(cur if dt == dom else self._side):
-                    if ev is not None:
-                        ev[0].record()
-                    kn.wsum_ptrs(dt, g.d_ptrs if tables is None else tables[dt], w64 if dt == torch.float64 else w32,
-                                 K, g.length, outs[dt], True, self.acc_mode)
-                    if ev is not None:
-                        ev[1].record()
+                s = cur if dt == dom else self._side
+                if ev is not None:
+                    ev[0].record(s)
+                kn.wsum_ptrs(dt, g.d_ptrs if tables is None else tables[dt], w64 if dt == torch.float64 else w32,
+                             K, g.length, outs[dt], True, self.acc_mode, s.cuda_stream)
+                if ev is not None:
+                    ev[1].record(s)
             if minor:
                 cur.wait_stream(self._side)
 

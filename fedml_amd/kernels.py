@@ -8,10 +8,11 @@ non-CUDA tensors raise.
 """
 from __future__ import annotations
 
+import array
 import ctypes
 import functools
 import operator
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -71,11 +72,26 @@ class HostWeights:
         return ctypes.addressof(self.buf)
 
 
+_LAST_HOST_W: dict = {}  # per weight dtype: (values' bytes, HostWeights) of the last ones built
+
+
 def weights_for(values: Sequence[float], dtype: torch.dtype, device: torch.device):
-    """Kernel-argument weights when K allows, else a device array."""
+    """Kernel-argument weights when K allows, else a device array.
+
+    The last HostWeights built is reused for the same values (keyed by their
+    exact fp64 bytes, so -0.0 and NaN payloads are told apart): a round over
+    G shards or several dtype groups builds it once.  The launch copies the
+    values into the kernel arguments, and nothing writes a HostWeights after
+    construction, so sharing one is safe."""
     wdt = torch.float64 if dtype == torch.float64 else torch.float32
     if len(values) <= INLINE_MAX_K:
-        return HostWeights(values, wdt)
+        key = array.array("d", values).tobytes()
+        last = _LAST_HOST_W.get(wdt)
+        if last is not None and last[0] == key:
+            return last[1]
+        hw = HostWeights(values, wdt)
+        _LAST_HOST_W[wdt] = (key, hw)
+        return hw
     return upload_f64(values, device) if wdt == torch.float64 else upload_f32(values, device)
 
 
@@ -98,13 +114,14 @@ def wsum_rlr_ptrs(d_ptrs: torch.Tensor, d_w, K: int, N: int, threshold: float, o
 
 
 def wsum_ptrs(dtype: torch.dtype, d_ptrs: torch.Tensor, d_w: torch.Tensor, K: int, N: int,
-              out: torch.Tensor, aligned: bool, acc_mode: int = ACC_REFERENCE) -> None:
-    """Weighted sum over K sources given as a device pointer table."""
+              out: torch.Tensor, aligned: bool, acc_mode: int = ACC_REFERENCE, stream: Optional[int] = None) -> None:
+    """Weighted sum over K sources given as a device pointer table; on the
+    current stream, or on the raw hipStream_t `stream`."""
     _require_cuda(out, "wsum")
     if N == 0:  # empty keys: nothing to launch (their outputs may have no storage)
         return
     lib = nat.lib()
-    st = nat.stream_handle()
+    st = stream if stream is not None else nat.stream_handle()
     flags = nat.FEDAGG_ALIGNED16 if aligned and (out.data_ptr() & 15) == 0 else 0
     if isinstance(d_w, HostWeights):
         flags |= nat.FEDAGG_HOST_WEIGHTS
