@@ -31,9 +31,18 @@ def _require_cuda(t: torch.Tensor, what: str) -> None:
         raise nat.FedAggNativeError(f"{what}: expected a device tensor, got {t.device} (no CPU fallback)")
 
 
+_CUDA: list = []  # torch.cuda.is_available(), asked once (it reads the environment on every call)
+
+
+def _cuda_ok() -> bool:
+    if not _CUDA:
+        _CUDA.append(torch.cuda.is_available())
+    return _CUDA[0]
+
+
 def upload_i64(values: Sequence[int], device: torch.device) -> torch.Tensor:
     arr = np.asarray(values, dtype=np.int64)  # ~2x faster than torch.tensor(list) on 40k pointers
-    if torch.cuda.is_available():
+    if _cuda_ok():
         host = torch.empty(arr.shape, dtype=torch.int64, pin_memory=True)
         host.numpy()[...] = arr
     else:
@@ -43,14 +52,14 @@ def upload_i64(values: Sequence[int], device: torch.device) -> torch.Tensor:
 
 def upload_f32(values: Sequence[float], device: torch.device) -> torch.Tensor:
     host = torch.tensor([float(v) for v in values], dtype=torch.float32)
-    if torch.cuda.is_available():
+    if _cuda_ok():
         host = host.pin_memory()
     return host.to(device, non_blocking=True)
 
 
 def upload_f64(values: Sequence[float], device: torch.device) -> torch.Tensor:
     host = torch.tensor([float(v) for v in values], dtype=torch.float64)
-    if torch.cuda.is_available():
+    if _cuda_ok():
         host = host.pin_memory()
     return host.to(device, non_blocking=True)
 
