@@ -17,10 +17,7 @@ Every config keeps BASELINE.json's client count (4 / 32 / 128 / 512 / 64;
                           keys dealt to ranks by bytes, the same partition as
                           the in-process fedml_amd.multidev bucket) and
                           reduces them in the reference order: no exchange,
-                          bit-exact with one GPU.  The same run then measures
-                          the client axis below on the same clients and nests
-                          it under "exchange" (north_star's RCCL
-                          reduce-scatter over xGMI; --no-exchange skips it).
+                          bit-exact with one GPU.  Nested legs follow (below).
   --mode client           every rank holds its K/N clients' whole updates,
                           computes an fp32 partial and joins one chunked RCCL
                           reduce-scatter (timed separately on the comm stream).
@@ -32,10 +29,37 @@ Every config keeps BASELINE.json's client count (4 / 32 / 128 / 512 / 64;
         --master-port 29500 bench.py --gpus 8
     python bench.py --gpus 8              # the same: bench.py spawns the 8 ranks itself
 
-In --mode param every multi-GPU line also nests "inprocess": rank 0 alone
-drives all N GPUs from ONE process through fedml_amd.multidev.MultiDeviceBucket
-(the only multi-GPU mode FedML's single server process can use), same clients,
-per-device kernel GB/s and roofline fraction (--no-inprocess skips it).
+Nested legs of a multi-GPU --mode param FedAvg line (each its own JSON object):
+
+  exchange      north_star's client axis on the same clients: fp32 partials +
+                the chunked RCCL reduce-scatter over xGMI (--no-exchange skips)
+  inprocess     rank 0 alone drives all N GPUs through one
+                fedml_amd.multidev.MultiDeviceBucket (the mode FedML's single
+                server process uses; --no-inprocess skips)
+  cfg4          at N >= 4: BASELINE config 4 (512 x ViT-B/16 bf16) on the
+                parameter axis, the client axis (fp32 partial reduce-scatter)
+                and in one process
+  cfg5          at N = 8: BASELINE config 5 (64 x Llama-2-7B LoRA) FedAvg fused
+                with the SGD server step (lr 1.0, momentum 0.9) through
+                ShardedFedOpt (client axis + RCCL) and MultiDeviceFedOptServer
+                (one process)
+  (--nest overrides which config legs run: auto, none, cfg4, cfg5, cfg4,cfg5)
+
+Robustness of the multi-GPU run: every rank meets the
+others only through the rendezvous TCP store (`Coord`: barriers with a
+deadline, timings gathered as JSON), so the exchange-free headline needs
+neither RCCL nor gloo; the process group (120 s timeout) is used by the
+nested client-axis legs alone, and RCCL creates its communicator at their
+first collective.  Before that collective every rank posts "ok" or its
+failure (`Leg.ready`); a leg any rank failed is abandoned by all of them, and
+its object carries the error.  Rank 0 starts a nested leg only while the job
+budget (--budget-s, default 480 s of the driver's 600 s) leaves that leg's
+reserve, else the object says "skipped: budget".  A watchdog thread on every
+rank prints whatever line rank 0 has at budget + 60 s and ends the process,
+so even a collective that never returns costs the nested object, not the
+line.  FEDAGG_BENCH_FAIL / FEDAGG_BENCH_HANG ("<leg>:<rank>,...") inject a
+failure or a hang into a leg's handshake (tests/test_bench_legs.py, with
+--probe-cpu: the same orchestration with host stand-in reductions on gloo).
 
 Prints ONE JSON line on rank 0 (contract in the task statement); at N = 1 the
 cpu_baseline leg times the reference's own CPU loop (oracle/cpu_baseline.py)
@@ -47,14 +71,19 @@ cycles per wave64 instruction per SIMD are set against the kernel time.
 """
 from __future__ import annotations
 
-import argparse
-import json
-import os
-import sys
 import time
 
-import torch
-import torch.distributed as dist
+T_START = time.monotonic()  # the job budget counts from here, before torch loads
+
+import argparse  # noqa: E402
+import datetime  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+import sys  # noqa: E402
+import threading  # noqa: E402
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -76,6 +105,8 @@ SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
 CLOCK_GHZ = 2.4
 VALU_HALF_RATE_CYCLES = 4  # min/max/med3/DPP wave64 issue cost per SIMD (profiles/r03/median_rsel/valu_rate_probe*.txt)
 LSA_PRIME, LSA_QBITS = 2 ** 15 - 19, 10  # the reference's example LightSecAgg config (fedml_config.yaml:58-59)
+PG_TIMEOUT_S = 120.0  # process group and store timeout (RCCL's default, 10 min, outlasts the driver's limit)
+WATCHDOG_GRACE_S = 60.0  # the watchdog fires this long after --budget-s
 
 CONFIGS = {
     "cfg1": dict(model="lr_mnist", K=4, desc="FedAvg 4 clients x LogisticRegression MNIST (7,850 params) fp32"),
@@ -85,6 +116,10 @@ CONFIGS = {
     "cfg4": dict(model="vit_b16", K=512, desc="FedAvg 512 clients x ViT-B/16 (86,567,656) bf16"),
     "cfg5": dict(model="llama2_7b_lora", K=64, desc="FedAvg 64 clients x Llama-2-7B LoRA r=8 q/v fp32"),
 }
+
+# seconds of job budget a nested leg must find left before rank 0 starts it
+LEG_RESERVE_S = {"exchange": 45.0, "inprocess": 45.0, "cfg4/param": 60.0, "cfg4/exchange": 90.0,
+                 "cfg4/inprocess": 90.0, "cfg5/sharded_fedopt": 45.0, "cfg5/inprocess_fedopt": 45.0}
 
 
 def parse(argv=None):
@@ -104,9 +139,9 @@ def parse(argv=None):
     ap.add_argument("--acc", default="reference", choices=["reference", "fp32"],
                     help="bf16/f16 accumulation: torch's per-op chain (bit-exact) or fp32")
     ap.add_argument("--fedopt", nargs="?", const="sgd", default=None,
-                    choices=["sgd", "adam", "adamw", "adagrad", "rmsprop"],
+                    choices=["sgd", "adam", "adamw", "adagrad", "rmsprop", "adamax", "nadam", "radam", "adadelta"],
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
-                         "or Adam / Adagrad lr=1.0 with torch defaults)")
+                         "or the other optimizers at lr=1.0 with torch defaults)")
     ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa", "krum", "dist2", "clip",
                                                        "rlr", "mpi"],
                     help="1 GPU: the reduction measured (median = the wise_median defense kernel; secagg = "
@@ -129,7 +164,15 @@ def parse(argv=None):
     ap.add_argument("--no-inprocess", action="store_true",
                     help="multi-GPU --mode param: skip the nested one-process measurement (MultiDeviceBucket over "
                          "the N GPUs, the mode FedML's single server process uses)")
+    ap.add_argument("--nest", default="auto",
+                    help="multi-GPU --mode param: the nested config legs: auto (cfg4 at N >= 4, cfg5 at N = 8), "
+                         "none, or a comma list of cfg4 / cfg5")
+    ap.add_argument("--budget-s", type=float, default=480.0,
+                    help="multi-GPU: job seconds (from process start) within which nested legs may start; the "
+                         "watchdog prints the line and ends every rank 60 s later")
+    ap.add_argument("--watchdog-s", type=float, default=None, help=argparse.SUPPRESS)  # default: budget + 60 s
     ap.add_argument("--spawn-probe", action="store_true", help=argparse.SUPPRESS)  # CPU test of the self-launch
+    ap.add_argument("--probe-cpu", action="store_true", help=argparse.SUPPRESS)  # CPU test of the orchestration
     return ap.parse_args(argv)
 
 
@@ -141,13 +184,15 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv, probe: bool = False) -> int:
+def spawn_ranks(n: int, argv, probe: bool = False, grace_s: float = 60.0) -> int:
     """`python bench.py --gpus N` without torch.distributed.run: start N
     worker processes of this script, one per GPU, with torchrun's environment
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* on 127.0.0.1), wait for them and
     return the first failing exit code (0 if all succeed).  The parent never
     touches the GPU (no HIP call before or after the spawn: the workers start
-    as fresh processes, not forks), and rank 0 prints the JSON line."""
+    as fresh processes, not forks), and rank 0 prints the JSON line.  Once
+    rank 0 has exited cleanly (its line is out), ranks still running after
+    ``grace_s`` are terminated and do not change the exit code."""
     import signal
     import subprocess
 
@@ -166,6 +211,7 @@ def spawn_ranks(n: int, argv, probe: bool = False) -> int:
 
     old = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
+    rank0_done = None
     try:
         for r in range(n):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
@@ -179,9 +225,16 @@ def spawn_ranks(n: int, argv, probe: bool = False) -> int:
                 if code is None:
                     continue
                 live.remove(p)
-                if code != 0 and rc == 0:
+                if p is procs[0] and code == 0:
+                    rank0_done = time.monotonic()
+                if code != 0 and rc == 0 and rank0_done is None:
                     rc = code
-                    stop_all()  # a rank died: the others would wait in a collective forever
+                    stop_all()  # a rank died: the others would wait for it until their deadlines
+            if live and rank0_done is not None and time.monotonic() - rank0_done > grace_s:
+                stop_all()  # the line is out; a rank that has not followed in grace_s is stuck
+                for p in live:
+                    p.wait()
+                live = []
             time.sleep(0.05)
     finally:
         stop_all()
@@ -193,6 +246,265 @@ def spawn_ranks(n: int, argv, probe: bool = False) -> int:
         print(json.dumps({"probe": "parent", "cuda_initialized": torch.cuda.is_initialized(),
                           "exit_codes": [p.returncode for p in procs]}), flush=True)
     return rc
+
+
+# ---- host-only coordination of the ranks -------------------------------------------------------------------------
+
+
+class Coord:
+    """Host-only coordination of the bench's ranks through the rendezvous TCP
+    store: barriers with a deadline, and small JSON values gathered from
+    every rank.  Nothing here touches the GPU or a collective backend, so the
+    exchange-free measurements depend on neither RCCL nor gloo, and a waiting
+    rank leaves no spinning kernel on its GPU.  Every name is used once per
+    run (keys are never reused).  The first deadline that passes marks the
+    coordination broken: later nested legs are skipped, not waited for."""
+
+    def __init__(self, world: int, rank: int, store=None, timeout_s: float = PG_TIMEOUT_S):
+        self.world, self.rank, self.store, self.timeout_s = world, rank, store, timeout_s
+        self.broken = None
+        self._used = set()
+
+    def _key(self, name: str) -> str:
+        if name in self._used:
+            raise ValueError(f"coordination name {name!r} used twice")
+        self._used.add(name)
+        return "bench/" + name
+
+    def _deadline(self, timeout_s):
+        return time.monotonic() + (self.timeout_s if timeout_s is None else timeout_s)
+
+    def _timeout(self, what: str) -> TimeoutError:
+        self.broken = self.broken or what
+        return TimeoutError(what)
+
+    def barrier(self, name: str, timeout_s=None) -> None:
+        if self.world == 1:
+            return
+        key = self._key(name)
+        self.store.add(key, 1)
+        deadline = self._deadline(timeout_s)
+        while True:
+            n = self.store.add(key, 0)
+            if n >= self.world:
+                return
+            if time.monotonic() > deadline:
+                raise self._timeout(f"barrier {name!r}: {n} of {self.world} ranks arrived in time")
+            time.sleep(0.005)
+
+    def post(self, name: str, value) -> None:
+        """This rank's value under ``name`` (collect() reads every rank's)."""
+        if self.world > 1:
+            self.store.set(f"bench/{name}/{self.rank}", json.dumps(value))
+
+    def collect(self, name: str, timeout_s=None, abort_key=None) -> list:
+        """Every rank's posted value under ``name``, in rank order.  abort_key:
+        a store key whose appearance ends the wait with LegAborted (a rank
+        that failed mid-leg posts it)."""
+        if self.world == 1:
+            raise ValueError("collect() needs ranks")
+        self._key(name)
+        keys = [f"bench/{name}/{r}" for r in range(self.world)]
+        deadline = self._deadline(timeout_s)
+        while not self.store.check(keys):
+            if abort_key is not None and self.store.check([abort_key]):
+                raise LegAborted(self.store.get(abort_key).decode())
+            if time.monotonic() > deadline:
+                have = [r for r, k in enumerate(keys) if self.store.check([k])]
+                raise self._timeout(f"{name!r}: only ranks {have} of {self.world} posted in time")
+            time.sleep(0.005)
+        return [json.loads(self.store.get(k)) for k in keys]
+
+    def allgather(self, name: str, value, timeout_s=None, abort_key=None) -> list:
+        if self.world == 1:
+            return [value]
+        self.post(name, value)
+        return self.collect(name, timeout_s, abort_key)
+
+    def from_rank0(self, name: str, value, timeout_s=None):
+        """Rank 0's value, on every rank (rank 0 decides, the others follow)."""
+        if self.world == 1:
+            return value
+        key = self._key(name)
+        if self.rank == 0:
+            self.store.set(key, json.dumps(value))
+            return value
+        deadline = self._deadline(timeout_s)
+        while not self.store.check([key]):
+            if time.monotonic() > deadline:
+                raise self._timeout(f"{name!r}: rank 0 did not decide in time")
+            time.sleep(0.005)
+        return json.loads(self.store.get(key))
+
+
+SOLO = Coord(1, 0)
+
+
+def host_barrier(tag: str, world: int, timeout_s: float = PG_TIMEOUT_S) -> None:
+    """A host-only barrier on the default process group's store, with a
+    deadline (TimeoutError)."""
+    store = dist.distributed_c10d._get_default_store()
+    Coord(world, dist.get_rank(), store).barrier(tag, timeout_s)
+
+
+class LegAborted(RuntimeError):
+    """A leg abandoned by this rank because another rank failed in it."""
+
+
+def _injected(kind: str, name: str, rank: int) -> bool:
+    """FEDAGG_BENCH_<kind> = "<leg>:<rank>,...": the test hooks."""
+    for item in os.environ.get(f"FEDAGG_BENCH_{kind}", "").split(","):
+        leg, _, r = item.strip().rpartition(":")
+        if leg == name and r.isdigit() and int(r) == rank:
+            return True
+    return False
+
+
+class Leg:
+    """One measurement of the run as the ranks see it: coordination names
+    under the leg's name, the readiness handshake before its first
+    collective, and the abort key a failing rank posts."""
+
+    def __init__(self, coord: Coord, name: str):
+        self.coord, self.name = coord, name
+        self.abort_key = f"bench/{name}/abort"
+        self._posted = False
+
+    @property
+    def rank(self) -> int:
+        return self.coord.rank
+
+    @property
+    def world(self) -> int:
+        return self.coord.world
+
+    def barrier(self, tag: str, timeout_s=None) -> None:
+        self.coord.barrier(f"{self.name}/{tag}", timeout_s)
+
+    def allgather(self, tag: str, value, timeout_s=None) -> list:
+        return self.coord.allgather(f"{self.name}/{tag}", value, timeout_s, self.abort_key)
+
+    def ready(self) -> None:
+        """Handshake before the leg's first collective: every rank posts "ok"
+        once its rows are allocated and filled, or its failure (``fail``).
+        If any rank failed, every rank abandons the leg here, before anyone
+        enters the collective that would wait for the failed rank."""
+        if _injected("FAIL", self.name, self.rank):
+            raise RuntimeError(f"injected failure (FEDAGG_BENCH_FAIL) in {self.name} on rank {self.rank}")
+        if self.world > 1:
+            self._posted = True
+            states = self.coord.allgather(f"{self.name}/ready", "ok")
+            bad = [f"rank {r}: {s}" for r, s in enumerate(states) if s != "ok"]
+            if bad:
+                raise LegAborted("; ".join(bad) + " -- every rank skipped the leg's collective")
+        if _injected("HANG", self.name, self.rank):  # a rank lost inside the collective phase
+            while True:
+                time.sleep(3600)
+
+    def fail(self, msg: str) -> None:
+        """This rank failed in the leg: answer the handshake (if not yet) and
+        post the abort key, so no rank waits for it."""
+        if self.world == 1:
+            return
+        if not self._posted:
+            self._posted = True
+            self.coord.post(f"{self.name}/ready", f"failed: {msg}")
+        self.coord.store.set(self.abort_key, f"rank {self.rank}: {msg}")
+
+
+class Budget:
+    def __init__(self, total_s: float):
+        self.total_s = total_s
+
+    def left(self) -> float:
+        return self.total_s - (time.monotonic() - T_START)
+
+
+class Report:
+    """The line being built (rank 0), printed exactly once: normally at the
+    end of main, or by the watchdog with what is there."""
+
+    def __init__(self):
+        self.line = None
+        self.leg = None
+        self._lock = threading.Lock()
+        self._printed = False
+
+    def emit(self, extra=None) -> bool:
+        with self._lock:
+            if self._printed or self.line is None:
+                return False
+            if extra:
+                self.line.update(extra)
+            print(json.dumps(self.line), flush=True)
+            self._printed = True
+            return True
+
+
+REPORT = Report()
+
+
+def start_watchdog(rank: int, budget: Budget, at_s=None) -> threading.Timer:
+    """After budget + grace, rank 0 prints the line as it stands (the running
+    leg marked) and every rank ends: a collective that never returns must
+    not cost the line or outlast the driver's limit."""
+    def fire():
+        running = REPORT.leg
+        if rank == 0:
+            REPORT.emit({"watchdog": f"fired at {time.monotonic() - T_START:.0f} s; still running: {running}"})
+        sys.stdout.flush()
+        sys.stderr.write(f"bench rank {rank}: watchdog fired during {running}\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    at = budget.total_s + WATCHDOG_GRACE_S if at_s is None else at_s  # seconds from the job's start
+    t = threading.Timer(max(1.0, at - (time.monotonic() - T_START)), fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def run_leg(coord: Coord, budget: Budget, name: str, fn, reserve_s: float, rank0_only: bool = False,
+            cleanup=None) -> dict:
+    """One nested leg on every rank: rank 0 decides from the budget whether it
+    starts; ``fn(leg)`` runs (on rank 0 alone if rank0_only, the others
+    waiting at the end barrier); an exception becomes the leg's "error" and
+    is posted so no rank waits for this one.  Every rank leaves together."""
+    REPORT.leg = name
+    if coord.broken:
+        return {"skipped": f"coordination lost earlier ({coord.broken})"}
+    left = budget.left()
+    go = "run" if left >= reserve_s else f"budget: {left:.0f} s of the job budget left, the leg reserves {reserve_s:.0f} s"
+    try:
+        go = coord.from_rank0(f"{name}/go", go)
+    except TimeoutError as e:
+        return {"skipped": str(e)}
+    if go != "run":
+        return {"skipped": go}
+    leg = Leg(coord if not rank0_only else SOLO, name)
+    out = {}
+    try:
+        if not rank0_only or coord.rank == 0:
+            out = fn(leg)
+    except LegAborted as e:
+        out = {"error": f"rank {coord.rank} abandoned the leg: {e}"}
+    except Exception as e:  # noqa: BLE001 -- the headline stands; the leg reports what it hit
+        msg = f"{type(e).__name__}: {e}"
+        if not rank0_only:
+            leg.fail(msg)
+        out = {"error": f"rank {coord.rank}: {msg}"}
+    finally:
+        if cleanup is not None:
+            cleanup()
+    try:
+        coord.barrier(f"{name}/end", max(PG_TIMEOUT_S, budget.left() + WATCHDOG_GRACE_S) if rank0_only else None)
+    except TimeoutError as e:
+        out.setdefault("error", str(e))
+    REPORT.leg = None
+    return out
+
+
+# ---- workload ------------------------------------------------------------------------------------------------------
 
 
 def plan_clients(config: str, world: int, rank: int, mode: str, clients_total=None, weak: bool = False,
@@ -242,6 +554,20 @@ def fill_rows(rows: torch.Tensor, length: int, seed: int, round_idx: int = 0) ->
         rows[i, :length].copy_(base + 0.01 * eps)
         rows[i, length:].zero_()
     del base, eps
+
+
+def fill_bucket(bucket, seed_base: int) -> None:
+    with torch.cuda.device(bucket.device):
+        for gi, (dt, g) in enumerate(bucket.groups.items()):
+            fill_rows(g.rows, g.length, seed=seed_base + gi, round_idx=3)
+
+
+def model_entries(config: str):
+    return shapes.MODELS[CONFIGS[config]["model"]]()
+
+
+def elements_per_client(entries) -> int:
+    return sum(sum(g.numels) for g in RowLayout(entries).groups.values())
 
 
 CPU_SAMPLE_BYTES = 13_400_000_000  # cpu_baseline: client bytes copied to the host (config 3 = 13.2 GB, all of it)
@@ -350,6 +676,159 @@ def load_median_valu(config: str, mode: str, world: int, variant: str, clients: 
         return None
 
 
+# ---- timing ---------------------------------------------------------------------------------------------------------
+
+
+class HostEvent:
+    """torch.cuda.Event's timing interface on the host clock (--probe-cpu)."""
+
+    def __init__(self, enable_timing=True):
+        self.t = None
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end) -> float:
+        return (end.t - self.t) * 1e3
+
+
+def _cuda_event():
+    return torch.cuda.Event(enable_timing=True)
+
+
+def run_timed(step, n_launch: int, steps: int, warmup: int, leg: Leg, per_chunk: bool, timed_comm: bool,
+              sync=None, event=None):
+    """W untimed steps, then K timed steps between a host barrier (the
+    rendezvous store) + synchronize on both sides.  Returns this rank's
+    (elapsed s; kernel ms per step from the events on the launch stream;
+    comm-stream ms per step or None); ``over_ranks`` combines them."""
+    sync = sync or torch.cuda.synchronize
+    event = event or _cuda_event
+
+    def new_events(n):
+        return [[event(), event()] for _ in range(n)]
+
+    for _ in range(warmup):
+        step()
+    evs = [new_events(n_launch) for _ in range(steps)]
+    cevs = [new_events(n_launch) for _ in range(steps)] if timed_comm else [None] * steps
+    sync()
+    leg.barrier("start")
+    t0 = time.perf_counter()
+    for s in range(steps):
+        # the client-axis steps take one (start, end) pair per chunk; the rest one pair
+        step(evs[s] if per_chunk else evs[s][0], cevs[s])
+    sync()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(e0.elapsed_time(e1) for ev in evs for e0, e1 in ev) / steps  # per step
+    comm_ms = sum(e0.elapsed_time(e1) for ev in cevs for e0, e1 in ev) / steps if timed_comm else None
+    return elapsed, kern_ms, comm_ms
+
+
+def over_ranks(leg: Leg, elapsed: float, achieved: float, hbm: float, comm_ms):
+    """Through the store: the MAX elapsed over ranks, the slowest rank's kernel
+    rate, the sum of the ranks' HBM rates and the mean comm-stream time."""
+    rows = leg.allgather("timing", [elapsed, achieved, hbm, comm_ms])
+    comm = [r[3] for r in rows if r[3] is not None]
+    return (max(r[0] for r in rows), min(r[1] for r in rows), sum(r[2] for r in rows),
+            sum(comm) / len(comm) if comm else None)
+
+
+# ---- nested legs (GPU) ---------------------------------------------------------------------------------------------
+
+
+def leg_steps(a):
+    """Steps of a nested collective leg: the run's, or 3 + 1 on gloo (a
+    host-staged rehearsal whose reduce-scatter costs ~0.1-1 s per step)."""
+    return (min(a.steps, 3), min(a.warmup, 1)) if a.backend == "gloo" else (a.steps, a.warmup)
+
+
+def measure_param(a, config: str, leg: Leg, dev) -> dict:
+    """A config's parameter axis over the ranks: this rank's whole keys
+    (multidev.shard_plan) of all K clients, reduced in the reference order;
+    no collective, bit-exact with one GPU."""
+    from fedml_amd.synth import sample_nums
+
+    world, rank = leg.world, leg.rank
+    entries = model_entries(config)
+    K = CONFIGS[config]["K"]
+    plan = multidev.shard_plan(entries, world)
+    if len(plan) < world:
+        return {"skipped": f"{config} has data in {len(plan)} keys: too few for {world} ranks"}
+    bucket = ClientBucket(plan[rank], K, dev, low_precision_acc=a.acc)
+    fill_bucket(bucket, 1000 * rank)
+    ns = sample_nums(K, seed=1)
+    w = bucket.weights(ns)
+    outs = bucket.new_outputs()
+    dom = bucket.dominant_dtype()
+
+    def step(ev=None, cev=None):
+        bucket.reduce_into(outs, w, events={dom: ev} if ev is not None else None)
+
+    torch.cuda.synchronize()
+    leg.ready()
+    elapsed, kern_ms, _ = run_timed(step, 1, a.steps, a.warmup, leg, False, False)
+    gd = bucket.groups[dom]
+    dom_bytes = K * gd.length * gd.rows.element_size() + gd.length * torch.empty((), dtype=gd.out_dtype).element_size()
+    achieved = dom_bytes / (kern_ms / 1e3) / 1e9
+    hbm = bucket.algorithmic_bytes() / (elapsed / a.steps) / 1e9
+    elapsed, achieved, hbm, _ = over_ranks(leg, elapsed, achieved, hbm, None)
+    n_elems = elements_per_client(entries)
+    return {"mode": "param", "workload": CONFIGS[config]["desc"], "world_size": world, "clients_total": K,
+            "value": K * n_elems / (elapsed / a.steps), "unit": "client-params/s",
+            "ms_per_step": elapsed / a.steps * 1e3, "kernel_gbps_slowest_rank": round(achieved, 1),
+            "frac_slowest_rank": round(achieved / HBM_PEAK_GBPS, 4), "aggregate_gbps": round(hbm, 1),
+            "aggregate_frac_of_n_peaks": round(hbm / (world * HBM_PEAK_GBPS), 4),
+            "parity": "bit-exact with one GPU (whole keys per rank, reference client order)"}
+
+
+def measure_client_axis(a, config: str, leg: Leg, dev) -> dict:
+    """north_star's client-axis mode on a config's round (its K clients and
+    sample counts): this rank's K/world clients' whole updates, the fp32
+    partial and the chunked RCCL reduce-scatter over xGMI; 16-bit models
+    round once after the exchange."""
+    from fedml_amd.synth import sample_nums
+
+    world, rank = leg.world, leg.rank
+    K_total = CONFIGS[config]["K"] if config != a.config or a.clients_total is None else a.clients_total
+    entries = model_entries(config)
+    if K_total < world:
+        return {"mode": "client", "skipped": f"{K_total} clients cannot cover {world} ranks on the client axis"}
+    _, K_c, first_c = plan_clients(config, world, rank, "client", K_total)
+    ns_all = sample_nums(K_total, seed=1)
+    total_n = sum(ns_all)
+    w = [n / total_n for n in ns_all[first_c:first_c + K_c]]
+    bucket = ClientBucket(entries, K_c, dev, low_precision_acc=a.acc)
+    fill_bucket(bucket, 1000 * rank)
+    torch.cuda.synchronize()
+    dom_dt = bucket.dominant_dtype()
+    step, n_launch, dom_bytes, xgmi_bytes = client_axis_step(bucket, dom_dt, w, a.chunks, world)
+    backend = dist.get_backend()
+    timed_comm = backend == "nccl"
+    steps, warmup = leg_steps(a)
+    leg.ready()  # every rank's rows are filled: only now does anyone enter the collective
+    elapsed, kern_ms, comm_ms = run_timed(step, n_launch, steps, warmup, leg, True, timed_comm)
+    achieved = dom_bytes / (kern_ms / 1e3) / 1e9
+    hbm_all = dom_bytes / (elapsed / steps) / 1e9
+    elapsed, achieved, hbm_all, comm_ms = over_ranks(leg, elapsed, achieved, hbm_all, comm_ms)
+    ms = elapsed / steps * 1e3
+    n_elems = elements_per_client(entries)
+    rehearsal = backend != "nccl"
+    return {"mode": "client", "workload": CONFIGS[config]["desc"], "backend": backend, "world_size": world,
+            "collective": "reduce_scatter_tensor (RCCL over xGMI)" if not rehearsal else
+            "reduce_scatter_tensor (gloo, host-staged: a rehearsal, not a measurement)",
+            "clients_total": K_total, "clients_per_gpu": K_c, "chunks": n_launch, "steps": steps,
+            "value": K_total * n_elems / (elapsed / steps), "unit": "client-params/s",
+            "ms_per_step": ms, "kernel_ms_per_step": round(kern_ms, 4),
+            "kernel_gbps_slowest_rank": round(achieved, 1), "frac_slowest_rank": round(achieved / HBM_PEAK_GBPS, 4),
+            "aggregate_gbps": round(hbm_all, 1), "xgmi_bytes_per_rank_per_step": xgmi_bytes,
+            "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
+            "parity": "fp32 partials summed across GPUs: |d| <= 2(K + log2 G + 1) 2^-24 sum|w_i p_i| vs one GPU "
+                      "(ClientAxisAggregator.tolerance; tests/test_sharded_gloo.py)",
+            "note": "comm_ms: mean over ranks of the chunks' reduce-scatter time on the comm stream (overlapping "
+                    "the next chunk's reduction)"}
+
+
 def client_axis_step(bucket, dom_dt, w_local, chunks: int, world: int):
     """The client-axis step over this rank's bucket: per dtype group the fp32
     partial of its clients (global weights) and the chunked reduce-scatter,
@@ -371,134 +850,36 @@ def client_axis_step(bucket, dom_dt, w_local, chunks: int, world: int):
     return step, len(aggs[dom_dt].bounds), dom_bytes, xgmi_bytes
 
 
-def run_timed(step, n_launch: int, steps: int, warmup: int, world: int, per_chunk: bool, timed_comm: bool):
-    """W untimed steps, then K timed steps between barrier + synchronize on
-    both sides.  Returns (elapsed s, MAX over ranks; kernel ms per step from
-    the HIP events on the launch stream; comm-stream ms per step or None)."""
-    def new_events(n):
-        return [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(n)]
-
-    for _ in range(warmup):
-        step()
-    evs = [new_events(n_launch) for _ in range(steps)]
-    cevs = [new_events(n_launch) for _ in range(steps)] if timed_comm else [None] * steps
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(steps):
-        # the client-axis steps take one (start, end) pair per chunk; the rest one pair
-        step(evs[s] if per_chunk else evs[s][0], cevs[s])
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], device=torch.cuda.current_device(), dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_ms = sum(e0.elapsed_time(e1) for ev in evs for e0, e1 in ev) / steps  # per step
-    comm_ms = sum(e0.elapsed_time(e1) for ev in cevs for e0, e1 in ev) / steps if timed_comm else None
-    return elapsed, kern_ms, comm_ms
+def _inprocess_devices(world: int):
+    n_dev = torch.cuda.device_count()
+    return [torch.device("cuda", i % n_dev) for i in range(world)]
 
 
-def reduce_rates(achieved: float, hbm_all: float, comm_ms, world: int, dev):
-    """Over ranks: the slowest rank's kernel rate, the sum of the ranks' HBM
-    rates and the mean comm-stream time."""
-    t = torch.tensor([achieved], device=dev, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)  # slowest rank's kernel
-    achieved = float(t.item())
-    t = torch.tensor([hbm_all, comm_ms or 0.0], device=dev, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    hbm_all = float(t[0].item())
-    if comm_ms is not None:
-        comm_ms = float(t[1].item()) / world
-    return achieved, hbm_all, comm_ms
+def _sync_devices(devices) -> None:
+    for i in sorted({d.index for d in devices}):
+        torch.cuda.synchronize(i)
 
 
-def measure_client_axis(a, entries, n_elems: int, K_total: int, world: int, rank: int, dev) -> dict:
-    """north_star's client-axis mode on the same round (the same K_total
-    clients and sample counts): this rank's K_total/world clients' whole
-    updates, the fp32 partial and the chunked RCCL reduce-scatter over xGMI.
-    Runs after the headline in the same processes; returns the "exchange"
-    object of the JSON line."""
-    from fedml_amd.synth import sample_nums
-
-    if K_total < world:
-        return {"mode": "client", "skipped": f"{K_total} clients cannot cover {world} ranks on the client axis"}
-    _, K_c, first_c = plan_clients(a.config, world, rank, "client", K_total)
-    ns_all = sample_nums(K_total, seed=1)
-    total_n = sum(ns_all)
-    w = [n / total_n for n in ns_all[first_c:first_c + K_c]]
-    bucket = ClientBucket(entries, K_c, dev, low_precision_acc=a.acc)
-    for gi, (dt, g) in enumerate(bucket.groups.items()):
-        fill_rows(g.rows, g.length, seed=1000 * rank + gi, round_idx=3)
-    torch.cuda.synchronize()
-    dom_dt = max(bucket.groups.items(), key=lambda kv: kv[1].length * kv[1].rows.element_size())[0]
-    step, n_launch, dom_bytes, xgmi_bytes = client_axis_step(bucket, dom_dt, w, a.chunks, world)
-    backend = dist.get_backend()
-    timed_comm = backend == "nccl"
-    elapsed, kern_ms, comm_ms = run_timed(step, n_launch, a.steps, a.warmup, world, True, timed_comm)
-    achieved = dom_bytes / (kern_ms / 1e3) / 1e9
-    hbm_all = dom_bytes / (elapsed / a.steps) / 1e9
-    achieved, hbm_all, comm_ms = reduce_rates(achieved, hbm_all, comm_ms, world, dev)
-    ms = elapsed / a.steps * 1e3
-    out = {"mode": "client", "backend": backend, "world_size": world,
-           "collective": "reduce_scatter_tensor (RCCL over xGMI)" if backend == "nccl" else
-           "reduce_scatter_tensor (gloo, host-staged: a rehearsal, not a measurement)",
-           "clients_total": K_total, "clients_per_gpu": K_c, "chunks": n_launch,
-           "value": K_total * n_elems / (elapsed / a.steps), "unit": "client-params/s",
-           "ms_per_step": ms, "kernel_ms_per_step": round(kern_ms, 4),
-           "kernel_gbps_slowest_rank": round(achieved, 1), "aggregate_gbps": round(hbm_all, 1),
-           "xgmi_bytes_per_rank_per_step": xgmi_bytes,
-           "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
-           "parity": "fp32 partials summed across GPUs: |d| <= 2(K + log2 G + 1) 2^-24 sum|w_i p_i| vs one GPU "
-                     "(ClientAxisAggregator.tolerance; tests/test_sharded_gloo.py)",
-           "note": "same clients as the headline; comm_ms: mean over ranks of the chunks' reduce-scatter time on "
-                   "the comm stream (overlapping the next chunk's reduction)"}
-    del step, bucket
-    torch.cuda.empty_cache()
-    return out
-
-
-def host_barrier(tag: str, world: int) -> None:
-    """A barrier on the host only, through the rendezvous TCP store: around
-    the one-process measurement an RCCL barrier would leave a spinning kernel
-    on every waiting rank's GPU while rank 0 reduces there."""
-    store = dist.distributed_c10d._get_default_store()
-    store.add(tag, 1)
-    while store.add(tag, 0) < world:
-        time.sleep(0.005)
-
-
-def measure_inprocess(a, entries, n_elems: int, K_total: int, world: int) -> dict:
+def measure_inprocess(a, config: str, world: int) -> dict:
     """The multi-GPU mode FedML's server can use: ONE process (the server is
     one process, python/fedml/__init__.py:330-348) driving `world` GPUs
     through fedml_amd.multidev.MultiDeviceBucket: whole keys per device, every
-    device reducing its keys of all K_total clients in the reference order (no
+    device reducing its keys of all K clients in the reference order (no
     exchange, bit-exact with one GPU; cross_silo/server/fedml_aggregator.py:
     58-67 feeds it).  Device-resident rows, the same clients and weights as
-    the headline; runs on rank 0 while the other ranks wait at a barrier with
-    their rows freed (host_barrier).  Returns the "inprocess" object of the
-    JSON line."""
+    the parameter axis; runs on rank 0 while the other ranks wait at a host
+    barrier with their rows freed."""
     from fedml_amd.synth import sample_nums
 
-    n_dev = torch.cuda.device_count()
-    devices = [torch.device("cuda", i % n_dev) for i in range(world)]
-    mb = multidev.MultiDeviceBucket(entries, K_total, devices, low_precision_acc=a.acc)
+    entries = model_entries(config)
+    K_total = CONFIGS[config]["K"] if config != a.config or a.clients_total is None else a.clients_total
+    mb = multidev.MultiDeviceBucket(entries, K_total, _inprocess_devices(world), low_precision_acc=a.acc)
     for s, b in enumerate(mb.shards):
-        with torch.cuda.device(b.device):
-            for gi, (dt, g) in enumerate(b.groups.items()):
-                fill_rows(g.rows, g.length, seed=5000 + 100 * s + gi, round_idx=3)
+        fill_bucket(b, 5000 + 100 * s)
     ns = sample_nums(K_total, seed=1)
     w = mb.weights(ns)
     outs = [b.new_outputs() for b in mb.shards]
     doms = [b.dominant_dtype() for b in mb.shards]
-    used = sorted({d.index for d in mb.devices})
-
-    def sync_all():
-        for i in used:
-            torch.cuda.synchronize(i)
 
     def step(evs=None):
         for s, b in enumerate(mb.shards):  # every device's launches queued before any is waited for
@@ -513,11 +894,11 @@ def measure_inprocess(a, entries, n_elems: int, K_total: int, world: int) -> dic
             with torch.cuda.device(b.device):
                 per.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
         evs.append(per)
-    sync_all()
+    _sync_devices(mb.devices)
     t0 = time.perf_counter()
     for s in range(a.steps):
         step(evs[s])
-    sync_all()
+    _sync_devices(mb.devices)
     elapsed = time.perf_counter() - t0
     per_dev = []
     total_bytes = 0
@@ -532,52 +913,217 @@ def measure_inprocess(a, entries, n_elems: int, K_total: int, world: int) -> dic
                         "kernel_ms_per_step": round(kern_ms, 4), "gbps": round(gbps, 1),
                         "frac": round(gbps / HBM_PEAK_GBPS, 4)})
     ms = elapsed / a.steps * 1e3
+    used = {d.index for d in mb.devices}
     shared = len(used) < len(mb.shards)
-    out = {"mode": "one process, G GPUs (fedml_amd.multidev.MultiDeviceBucket)", "devices": len(mb.shards),
-           "distinct_gpus": len(used), "clients_total": K_total,
-           "value": K_total * n_elems / (elapsed / a.steps), "unit": "client-params/s", "ms_per_step": ms,
-           "slowest_device_kernel_ms": max(d["kernel_ms_per_step"] for d in per_dev),
-           "per_device": per_dev, "aggregate_gbps": round(total_bytes / (elapsed / a.steps) / 1e9, 1),
-           "aggregate_frac_of_n_peaks": round(total_bytes / (elapsed / a.steps) / 1e9 / (len(used) * HBM_PEAK_GBPS),
-                                              4),
-           "shard_balance": round(max(mb.shard_bytes()) / (sum(mb.shard_bytes()) / len(mb.shards)), 4),
-           "parity": "bit-exact with one GPU (whole keys per device, reference client order; "
-                     "tests/test_gpu_multidev.py)",
-           "note": ("shards share one GPU here: a rehearsal of the launch pattern, not a multi-GPU rate"
-                    if shared else "device-resident rows; reduce_to_host (D2H) excluded, as in the headline")}
-    del mb, outs
-    torch.cuda.empty_cache()
-    return out
+    n_elems = elements_per_client(entries)
+    return {"mode": "one process, G GPUs (fedml_amd.multidev.MultiDeviceBucket)", "workload": CONFIGS[config]["desc"],
+            "devices": len(mb.shards), "distinct_gpus": len(used), "clients_total": K_total,
+            "value": K_total * n_elems / (elapsed / a.steps), "unit": "client-params/s", "ms_per_step": ms,
+            "slowest_device_kernel_ms": max(d["kernel_ms_per_step"] for d in per_dev),
+            "per_device": per_dev, "aggregate_gbps": round(total_bytes / (elapsed / a.steps) / 1e9, 1),
+            "aggregate_frac_of_n_peaks": round(total_bytes / (elapsed / a.steps) / 1e9 / (len(used) * HBM_PEAK_GBPS),
+                                               4),
+            "shard_balance": round(max(mb.shard_bytes()) / (sum(mb.shard_bytes()) / len(mb.shards)), 4),
+            "parity": "bit-exact with one GPU (whole keys per device, reference client order; "
+                      "tests/test_gpu_multidev.py)",
+            "note": ("shards share one GPU here: a rehearsal of the launch pattern, not a multi-GPU rate"
+                     if shared else "device-resident rows; reduce_to_host (D2H) excluded, as in the headline")}
 
 
-def main():
-    a = parse()
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # launched as `python bench.py --gpus N`: become torchrun ourselves
-        raise SystemExit(spawn_ranks(a.gpus, sys.argv[1:], probe=a.spawn_probe))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus > 1 and world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one process per GPU (or drop WORLD_SIZE "
-                         "and let bench.py spawn them)")
-    if a.spawn_probe:
-        print(json.dumps({"probe": "rank", "rank": rank, "local_rank": local, "world": world,
-                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
-                          "cuda_initialized": torch.cuda.is_initialized()}), flush=True)
-        return
-    dev = torch.device("cuda", local % torch.cuda.device_count())
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+CFG5_STEP = ("sgd", 1.0, 0.9)  # config 5's server step in the nested legs: SGD lr 1.0 momentum 0.9
 
+
+def measure_sharded_fedopt(a, config: str, leg: Leg, dev) -> dict:
+    """Config 5 over the ranks' client axis: ShardedFedOpt (fp32 partial,
+    chunked RCCL reduce-scatter, then the fused SGD + momentum step on each
+    rank's 1/G shard with sharded optimizer state)."""
+    from fedml_amd.sharded import ShardedFedOpt, buffer_ranges
+    from fedml_amd.synth import sample_nums
+
+    world, rank = leg.world, leg.rank
+    entries = model_entries(config)
+    K_total = CONFIGS[config]["K"]
+    if K_total < world:
+        return {"skipped": f"{K_total} clients cannot cover {world} ranks on the client axis"}
+    _, K_c, first_c = plan_clients(config, world, rank, "client", K_total)
+    ns_all = sample_nums(K_total, seed=1)
+    total_n = sum(ns_all)
+    w = [n / total_n for n in ns_all[first_c:first_c + K_c]]
+    bucket = ClientBucket(entries, K_c, dev)
+    if set(bucket.groups) != {torch.float32}:
+        return {"skipped": f"{config}: the sharded FedOpt leg takes an fp32 model"}
+    fill_bucket(bucket, 1000 * rank)
+    gd = bucket.groups[torch.float32]
+    init = torch.zeros(gd.length, dtype=torch.float32, device=dev)
+    opt_name, lr, mom = CFG5_STEP
+    opt = ShardedFedOpt(gd.rows, gd.length, init, opt_name, lr, mom, chunks=a.chunks,
+                        buffers=buffer_ranges(bucket, shapes.param_names(entries)))
+    torch.cuda.synchronize()
+    steps, warmup = leg_steps(a)
+    leg.ready()
+    opt.aggregate(w)  # the first step (no momentum read) before timing
+
+    def step(ev=None, cev=None):
+        opt.aggregate(w, events=ev, comm_events=cev)
+
+    timed_comm = dist.get_backend() == "nccl"
+    n_launch = len(opt.agg.bounds)
+    elapsed, kern_ms, comm_ms = run_timed(step, n_launch, steps, warmup, leg, True, timed_comm)
+    dom_bytes = K_c * gd.length * 4 + gd.length * 4  # rows in, fp32 partial out (the step itself is 1/G of a pass)
+    achieved = dom_bytes / (kern_ms / 1e3) / 1e9
+    hbm = dom_bytes / (elapsed / steps) / 1e9
+    elapsed, achieved, hbm, comm_ms = over_ranks(leg, elapsed, achieved, hbm, comm_ms)
+    xgmi = (world - 1) * opt.agg.piece * n_launch * 4
+    n_elems = elements_per_client(entries)
+    return {"mode": "client axis + sharded server step (fedml_amd.sharded.ShardedFedOpt)",
+            "workload": CONFIGS[config]["desc"], "server_step": "SGD lr=1.0 momentum=0.9, each rank's 1/G shard",
+            "backend": dist.get_backend(), "world_size": world, "clients_total": K_total, "clients_per_gpu": K_c,
+            "steps": steps, "value": K_total * n_elems / (elapsed / steps), "unit": "client-params/s",
+            "ms_per_step": elapsed / steps * 1e3, "kernel_ms_per_step": round(kern_ms, 4),
+            "kernel_gbps_slowest_rank": round(achieved, 1), "frac_slowest_rank": round(achieved / HBM_PEAK_GBPS, 4),
+            "xgmi_bytes_per_rank_per_step": xgmi,
+            "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
+            "parity": "the client-axis tolerance for the average, then the one-GPU fused step "
+                      "(tests/test_gpu_multirank.py, tests/test_sharded_gloo.py)"}
+
+
+def measure_inprocess_fedopt(a, config: str, world: int) -> dict:
+    """Config 5 in ONE server process over `world` GPUs:
+    MultiDeviceFedOptServer (whole keys per device, each device's FedAvg
+    fused with the SGD + momentum step, bit-exact with one GPU)."""
+    from collections import OrderedDict
+
+    from fedml_amd.fedopt import MultiDeviceFedOptServer
+    from fedml_amd.synth import sample_nums
+
+    entries = model_entries(config)
+    K = CONFIGS[config]["K"]
+    devices = _inprocess_devices(world)
+    init = OrderedDict((k, torch.zeros(s, dtype=d)) for k, s, d in entries)
+    opt_name, lr, mom = CFG5_STEP
+    server = MultiDeviceFedOptServer(init, shapes.param_names(entries), K, opt_name, lr, mom, devices)
+    for s, srv in enumerate(server.servers):
+        fill_bucket(srv.bucket, 7000 + 100 * s)
+    for i, n in enumerate(sample_nums(K, seed=1)):
+        server.sample_num_dict[i] = n
+    server.aggregate()  # the first step (no momentum read) before timing
+    for _ in range(a.warmup):
+        server.aggregate()
+    evs = []
+    for _ in range(a.steps):
+        per = []
+        for srv in server.servers:
+            with torch.cuda.device(srv.device):
+                per.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        evs.append(per)
+    _sync_devices(server.devices)
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        server.aggregate(device_events=evs[s])
+    _sync_devices(server.devices)
+    elapsed = time.perf_counter() - t0
+    per_dev = []
+    for s, srv in enumerate(server.servers):
+        kern_ms = sum(ev[s][0].elapsed_time(ev[s][1]) for ev in evs) / a.steps
+        b = srv.algorithmic_bytes()
+        per_dev.append({"device": str(srv.device), "keys": len(srv.bucket.entries), "alg_bytes_per_step": b,
+                        "kernel_ms_per_step": round(kern_ms, 4), "gbps": round(b / (kern_ms / 1e3) / 1e9, 1),
+                        "frac": round(b / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)})
+    total = server.algorithmic_bytes()
+    used = {d.index for d in server.devices}
+    n_elems = elements_per_client(entries)
+    return {"mode": "one process, G GPUs (fedml_amd.fedopt.MultiDeviceFedOptServer)",
+            "workload": CONFIGS[config]["desc"], "server_step": "SGD lr=1.0 momentum=0.9 fused into the reduction",
+            "devices": len(server.servers), "distinct_gpus": len(used), "clients_total": K,
+            "value": K * n_elems / (elapsed / a.steps), "unit": "client-params/s",
+            "ms_per_step": elapsed / a.steps * 1e3, "per_device": per_dev,
+            "aggregate_gbps": round(total / (elapsed / a.steps) / 1e9, 1),
+            "aggregate_frac_of_n_peaks": round(total / (elapsed / a.steps) / 1e9 / (len(used) * HBM_PEAK_GBPS), 4),
+            "parity": "bit-exact with one GPU (tests/test_gpu_multidev_fedopt.py)",
+            "note": ("shards share one GPU here: a rehearsal of the launch pattern, not a multi-GPU rate"
+                     if len(used) < len(server.servers) else "device-resident rows and state")}
+
+
+def _free_device_memory() -> None:
+    if torch.cuda.is_initialized():
+        for i in range(torch.cuda.device_count()):
+            torch.cuda.synchronize(i)
+        torch.cuda.empty_cache()
+
+
+# ---- nested legs (--probe-cpu: host stand-ins, same orchestration) ---------------------------------------------------
+
+
+PROBE_K, PROBE_N = 8, 4096
+
+
+def _probe_rows(K: int, seed: int) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(K, PROBE_N, generator=g)
+
+
+def _probe_step(fn):
+    """A stand-in step recording its events on the host clock."""
+    def step(ev=None, cev=None):
+        if ev is not None:
+            ev[0].record()
+        fn()
+        if ev is not None:
+            ev[1].record()
+    return step
+
+
+def _probe_reducer(rows, weights, out):
+    acc = torch.zeros(rows.shape[1], dtype=torch.float32)
+    for i, wi in enumerate(weights):
+        acc += rows[i].float() * wi
+    out.copy_(acc)
+
+
+def probe_param(a, config: str, leg: Leg, dev) -> dict:
+    from fedml_amd.sharded import ParamAxisAggregator
+
+    rows = _probe_rows(PROBE_K, 10 + leg.rank)
+    agg = ParamAxisAggregator(rows, PROBE_N, reducer=_probe_reducer)
+    w = [1.0 / PROBE_K] * PROBE_K
+    leg.ready()
+    elapsed, kern_ms, _ = run_timed(_probe_step(lambda: agg.aggregate(w)), 1, a.steps, a.warmup, leg, False,
+                                    False, sync=lambda: None, event=HostEvent)
+    elapsed, achieved, hbm, _ = over_ranks(leg, elapsed, 0.0, 0.0, None)
+    return {"mode": "param", "probe": True, "ms_per_step": elapsed / a.steps * 1e3}
+
+
+def probe_client_axis(a, config: str, leg: Leg, dev) -> dict:
+    rows = _probe_rows(PROBE_K // leg.world, 20 + leg.rank)
+    agg = ClientAxisAggregator(rows, PROBE_N, chunks=2, reducer=_probe_reducer)
+    w = [1.0 / PROBE_K] * rows.shape[0]
+    steps, warmup = leg_steps(a)
+    leg.ready()
+    elapsed, _, _ = run_timed(_probe_step(lambda: agg.aggregate(w)), 1, steps, warmup, leg, False, False,
+                              sync=lambda: None, event=HostEvent)
+    elapsed, _, _, _ = over_ranks(leg, elapsed, 0.0, 0.0, None)
+    return {"mode": "client", "probe": True, "backend": dist.get_backend(), "ms_per_step": elapsed / steps * 1e3}
+
+
+def probe_inprocess(a, config: str, world: int) -> dict:
+    rows = _probe_rows(PROBE_K, 30)
+    out = torch.empty(PROBE_N)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        _probe_reducer(rows, [1.0 / PROBE_K] * PROBE_K, out)
+    return {"mode": "one process", "probe": True, "devices": world,
+            "ms_per_step": (time.perf_counter() - t0) / a.steps * 1e3}
+
+
+# ---- the headline ---------------------------------------------------------------------------------------------------
+
+
+def measure_headline(a, world: int, rank: int, dev, coord: Coord):
+    """The line's own measurement (the contract's K timed steps).  Returns
+    (line, the bucket and local sample counts for the CPU baseline)."""
     cfg = CONFIGS[a.config]
-    entries = shapes.MODELS[cfg["model"]]()
-    full_layout = RowLayout(entries)
-    n_elems = sum(sum(g.numels) for g in full_layout.groups.values())  # per client, the whole model
+    entries = model_entries(a.config)
+    n_elems = elements_per_client(entries)  # per client, the whole model
     mode = a.mode if world > 1 else "single"
     weak = a.weak and world > 1
     # this rank's clients: all of them (single / param axis) or its share (client axis)
@@ -596,6 +1142,7 @@ def main():
     ns_local = ns_all[first:first + K_loc]
     total_n = sum(ns_all)
     w_local = [n / total_n for n in ns_local]  # global weights of this rank's clients
+    leg = Leg(coord, "headline")
 
     server = None
     sharded_opt = None
@@ -646,6 +1193,7 @@ def main():
             sharded_opt.aggregate(w_local, events=ev, comm_events=cev)
 
         n_launch = len(sharded_opt.agg.bounds)
+        leg.ready()
         sharded_opt.aggregate(w_local)  # first step (no state read) before timing
         dom_bytes = K_loc * gd.length * 4 + gd.length * 4  # rows in, fp32 partial out (the step is 1/G of a pass)
         xgmi_bytes = (world - 1) * sharded_opt.agg.piece * len(sharded_opt.agg.bounds) * 4
@@ -814,13 +1362,14 @@ def main():
             gd.length * torch.empty((), dtype=gd.out_dtype).element_size()
     else:  # client axis: this rank's clients' partial + chunked RCCL reduce-scatter
         step, n_launch, dom_bytes, xgmi_bytes = client_axis_step(bucket, dom_dt, w_local, a.chunks, world)
+        leg.ready()
 
     timed_comm = mode == "client" and world > 1 and a.backend == "nccl"
-    elapsed, kern_ms, comm_ms = run_timed(step, n_launch, a.steps, a.warmup, world, mode == "client", timed_comm)
+    elapsed, kern_ms, comm_ms = run_timed(step, n_launch, a.steps, a.warmup, leg, mode == "client", timed_comm)
     achieved = dom_bytes / (kern_ms / 1e3) / 1e9  # GB/s (GFLOP/s for the exact-difference krum kernel)
     hbm_all = dom_bytes / (elapsed / a.steps) / 1e9  # this rank's algorithmic bytes over the step time
     if world > 1:
-        achieved, hbm_all, comm_ms = reduce_rates(achieved, hbm_all, comm_ms, world, dev)
+        elapsed, achieved, hbm_all, comm_ms = over_ranks(leg, elapsed, achieved, hbm_all, comm_ms)
 
     ms_per_step = elapsed / a.steps * 1e3
     gram_op = a.op == "krum" and (a.pair_distance == "gram" or (a.pair_distance == "auto" and K <= 128))
@@ -856,10 +1405,7 @@ def main():
             "elements_per_client": n_elems,
             "layout": "ClientBucket rows [K, L] per dtype, 256-B aligned rows",
             "low_precision_acc": a.acc,
-            "server_step": ({"sgd": "SGD lr=1.0 momentum=0.9", "adam": "Adam lr=1.0 betas=(0.9,0.999)",
-                             "adagrad": "Adagrad lr=1.0 eps=1e-10",
-                             "adamw": "AdamW lr=1.0 weight_decay=0.01",
-                             "rmsprop": "RMSprop lr=1.0 alpha=0.99"}[a.fedopt]
+            "server_step": (SERVER_STEP_DESC[a.fedopt]
                             + (" fused" if server is not None else
                                f", on each rank's 1/{world} shard after the reduce-scatter, sharded state")
                             if a.fedopt else None),
@@ -885,10 +1431,7 @@ def main():
                         "mpi": "reduce_kernel<OpF32MulDiv> (fl(fl(p n_i) / N))"}[a.op]
                        if a.op in ("secagg", "lsa", "krum", "dist2", "clip", "rlr", "mpi") else
                        median_kernel_name(K, dom_dt) if a.op == "median" else
-                       ({"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
-                         "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>"}
-                        .get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>"))
-                       + " (FedAvg+server step fused)"
+                       SERVER_STEP_KERNEL.get(a.fedopt, "reduce_kernel<OpF32,SgdEpi>") + " (FedAvg+server step fused)"
                        if server is not None else
                        f"reduce_kernel<OpF32> x{n_launch}/step + shard step" if sharded_opt is not None else
                        f"reduce_kernel<{'OpF32' if dom_dt == torch.float32 else dom_dt}> x{n_launch}/step"),
@@ -927,35 +1470,143 @@ def main():
                                 "comm_ms_per_step": round(comm_ms, 4) if comm_ms is not None else None,
                                 "note": "comm_ms: mean over ranks of the chunks' reduce-scatter time on the comm "
                                         "stream (overlapping the next chunk's reduction)"}
-        elif mode == "param" and a.op == "fedavg" and not a.fedopt:
-            # the headline is the exchange-free parameter axis of N processes;
-            # two more measurements on the same clients follow, each after this
-            # rank's rows are freed
-            del step, outs, gd, groups, bucket
-            torch.cuda.empty_cache()
+    keep = (bucket, ns_local) if world == 1 and a.op == "fedavg" and not a.no_cpu_baseline else None
+    return line, keep
+
+
+SERVER_STEP_DESC = {"sgd": "SGD lr=1.0 momentum=0.9", "adam": "Adam lr=1.0 betas=(0.9,0.999)",
+                    "adagrad": "Adagrad lr=1.0 eps=1e-10", "adamw": "AdamW lr=1.0 weight_decay=0.01",
+                    "rmsprop": "RMSprop lr=1.0 alpha=0.99", "adamax": "Adamax lr=1.0 betas=(0.9,0.999)",
+                    "nadam": "NAdam lr=1.0 momentum_decay=4e-3", "radam": "RAdam lr=1.0 betas=(0.9,0.999)",
+                    "adadelta": "Adadelta lr=1.0 rho=0.9 eps=1e-6"}
+SERVER_STEP_KERNEL = {"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
+                      "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>",
+                      "adamax": "reduce_fused_kernel<OpF32,AdamaxEpi>", "nadam": "reduce_fused_kernel<OpF32,NAdamEpi>",
+                      "radam": "reduce_fused_kernel<OpF32,RAdamEpi>",
+                      "adadelta": "reduce_fused_kernel<OpF32,AdadeltaEpi>"}
+
+
+def probe_headline(a, world: int, rank: int, coord: Coord):
+    """--probe-cpu: the multi-rank orchestration with a host stand-in for the
+    parameter-axis reduction (gloo, no GPU).  Not a measurement."""
+    d = probe_param(a, a.config, Leg(coord, "headline"), None)
+    line = {"metric": METRIC, "value": PROBE_K * PROBE_N / (d["ms_per_step"] / 1e3), "unit": "client-params/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": d["ms_per_step"],
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "probe", "probe": "cpu orchestration probe: host stand-in reductions over gloo, not a measurement",
+            "config": {"workload": "probe", "parallelism": f"parameter-axis x{world}"}, "roofline": None,
+            "cpu_baseline": None}
+    return line, None
+
+
+def nested_configs(a, world: int):
+    """The config legs nested in this run (--nest, default by N)."""
+    if a.nest == "none":
+        return []
+    if a.nest == "auto":
+        want = (["cfg4"] if world >= 4 else []) + (["cfg5"] if world >= 8 else [])
+    else:
+        want = [c.strip() for c in a.nest.split(",") if c.strip()]
+        bad = [c for c in want if c not in ("cfg4", "cfg5")]
+        if bad:
+            raise SystemExit(f"--nest: {bad} (cfg4 / cfg5, auto or none)")
+    return [c for c in want if c != a.config]
+
+
+def run_nested(a, world: int, rank: int, dev, coord: Coord, budget: Budget, line: dict) -> None:
+    """The nested legs of a multi-GPU --mode param FedAvg line, each into its
+    own object of ``line`` (which the watchdog prints as it stands)."""
+    probe = a.probe_cpu
+    cleanup = (lambda: None) if probe else _free_device_memory
+    client_fn = probe_client_axis if probe else measure_client_axis
+    inproc_fn = probe_inprocess if probe else measure_inprocess
+    param_fn = probe_param if probe else measure_param
+    sfo_fn = probe_client_axis if probe else measure_sharded_fedopt
+    ifo_fn = probe_inprocess if probe else measure_inprocess_fedopt
+
+    def leg(key, name, fn, rank0_only=False):
+        res = run_leg(coord, budget, name, fn, LEG_RESERVE_S.get(name, 45.0), rank0_only, cleanup)
+        tgt = line
+        for part in key[:-1]:
+            tgt = tgt.setdefault(part, {})
+        tgt[key[-1]] = res
+
+    cleanup()
+    if not a.no_exchange:
+        leg(("exchange",), "exchange", lambda lg: client_fn(a, a.config, lg, dev))
+    if not a.no_inprocess:
+        leg(("inprocess",), "inprocess", lambda lg: inproc_fn(a, a.config, world), rank0_only=True)
+    for cfg in nested_configs(a, world):
+        if cfg == "cfg4":
+            leg(("cfg4", "param"), "cfg4/param", lambda lg: param_fn(a, "cfg4", lg, dev))
             if not a.no_exchange:
-                # north_star's client axis + RCCL reduce-scatter over xGMI
-                try:
-                    line["exchange"] = measure_client_axis(a, entries, n_elems, K_total, world, rank, dev)
-                except Exception as e:  # the headline above stands; report what the nested run hit
-                    line["exchange"] = {"mode": "client", "error": f"{type(e).__name__}: {e}"}
+                leg(("cfg4", "exchange"), "cfg4/exchange", lambda lg: client_fn(a, "cfg4", lg, dev))
             if not a.no_inprocess:
-                # FedML's server is ONE process: rank 0 alone drives all N
-                # GPUs through the multi-device bucket while the others wait
-                torch.cuda.synchronize()
-                host_barrier("inprocess_start", world)
-                if rank == 0:
-                    try:
-                        line["inprocess"] = measure_inprocess(a, entries, n_elems, K_total, world)
-                    except Exception as e:
-                        line["inprocess"] = {"error": f"{type(e).__name__}: {e}"}
-                host_barrier("inprocess_end", world)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.op == "fedavg":  # the reference's FedAvg loop
-        line["cpu_baseline"] = cpu_baseline(bucket, ns_local, a.cpu_reps)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+                leg(("cfg4", "inprocess"), "cfg4/inprocess", lambda lg: inproc_fn(a, "cfg4", world), rank0_only=True)
+        elif cfg == "cfg5":
+            if not a.no_exchange:
+                leg(("cfg5", "sharded_fedopt"), "cfg5/sharded_fedopt", lambda lg: sfo_fn(a, "cfg5", lg, dev))
+            if not a.no_inprocess:
+                leg(("cfg5", "inprocess_fedopt"), "cfg5/inprocess_fedopt", lambda lg: ifo_fn(a, "cfg5", world),
+                    rank0_only=True)
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launched as `python bench.py --gpus N`: become torchrun ourselves
+        raise SystemExit(spawn_ranks(a.gpus, sys.argv[1:], probe=a.spawn_probe))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus > 1 and world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one process per GPU (or drop WORLD_SIZE "
+                         "and let bench.py spawn them)")
+    if a.spawn_probe:
+        print(json.dumps({"probe": "rank", "rank": rank, "local_rank": local, "world": world,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
+                          "cuda_initialized": torch.cuda.is_initialized()}), flush=True)
+        return
+    budget = Budget(a.budget_s)
+    dev = None
+    if not a.probe_cpu:
+        dev = torch.device("cuda", local % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+    coord = SOLO
     if world > 1:
-        dist.destroy_process_group()
+        start_watchdog(rank, budget, a.watchdog_s)
+        timeout = datetime.timedelta(seconds=PG_TIMEOUT_S)
+        # no device_id: RCCL builds its communicator at the first collective
+        # (a nested client-axis leg), so the exchange-free headline needs only
+        # the rendezvous store
+        backend = "gloo" if a.probe_cpu or a.backend == "gloo" else "nccl"
+        dist.init_process_group(backend, timeout=timeout)
+        coord = Coord(world, rank, dist.distributed_c10d._get_default_store())
+    keep = None
+    try:
+        if a.probe_cpu:
+            if world == 1:
+                raise SystemExit("--probe-cpu rehearses the multi-rank orchestration: --gpus >= 2")
+            line, keep = probe_headline(a, world, rank, coord)
+        else:
+            line, keep = measure_headline(a, world, rank, dev, coord)
+        if rank == 0:
+            REPORT.line = line
+        if world > 1 and a.mode == "param" and a.op == "fedavg" and not a.fedopt:
+            try:
+                run_nested(a, world, rank, dev, coord, budget, line)
+            except Exception as e:  # noqa: BLE001 -- the headline stands whatever the nested legs hit
+                line["nested_error"] = f"{type(e).__name__}: {e}"
+        if keep is not None and rank == 0:  # the reference's FedAvg loop on the host
+            line["cpu_baseline"] = cpu_baseline(keep[0], keep[1], a.cpu_reps)
+        REPORT.emit()
+    finally:
+        if world > 1 and dist.is_initialized():
+            try:
+                coord.barrier("exit", timeout_s=30.0)
+            except (TimeoutError, RuntimeError):
+                pass
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -377,11 +377,13 @@ class MultiDeviceFedOptServer:
                 s.flag_client_model_uploaded_dict[idx] = False
         return True
 
-    def aggregate(self, events=None) -> "OrderedDict[str, torch.Tensor]":
+    def aggregate(self, events=None, device_events=None) -> "OrderedDict[str, torch.Tensor]":
         """Every device's launches are enqueued on its own current stream
-        (events, if given, around the first device's fp32 launches)."""
+        (events, if given, around the first device's fp32 launches;
+        device_events[i] around device i's)."""
         for i, s in enumerate(self.servers):
-            s.aggregate(events=events if i == 0 else None)
+            ev = device_events[i] if device_events is not None else (events if i == 0 else None)
+            s.aggregate(events=ev)
         return self.get_global_model_params()
 
     def get_global_model_params(self) -> "OrderedDict[str, torch.Tensor]":
