@@ -139,7 +139,8 @@ def parse(argv=None):
     ap.add_argument("--acc", default="reference", choices=["reference", "fp32"],
                     help="bf16/f16 accumulation: torch's per-op chain (bit-exact) or fp32")
     ap.add_argument("--fedopt", nargs="?", const="sgd", default=None,
-                    choices=["sgd", "adam", "adamw", "adagrad", "rmsprop", "adamax", "nadam", "radam", "adadelta"],
+                    choices=["sgd", "adam", "adamw", "adagrad", "rmsprop", "adamax", "nadam", "radam", "adadelta",
+                             "asgd", "rprop"],
                     help="1 GPU: FedOpt server step fused into the reduction (config 5: SGD lr=1.0 momentum 0.9, "
                          "or the other optimizers at lr=1.0 with torch defaults)")
     ap.add_argument("--op", default="fedavg", choices=["fedavg", "median", "secagg", "lsa", "krum", "dist2", "clip",
@@ -1478,12 +1479,12 @@ SERVER_STEP_DESC = {"sgd": "SGD lr=1.0 momentum=0.9", "adam": "Adam lr=1.0 betas
                     "adagrad": "Adagrad lr=1.0 eps=1e-10", "adamw": "AdamW lr=1.0 weight_decay=0.01",
                     "rmsprop": "RMSprop lr=1.0 alpha=0.99", "adamax": "Adamax lr=1.0 betas=(0.9,0.999)",
                     "nadam": "NAdam lr=1.0 momentum_decay=4e-3", "radam": "RAdam lr=1.0 betas=(0.9,0.999)",
-                    "adadelta": "Adadelta lr=1.0 rho=0.9 eps=1e-6"}
+                    "adadelta": "Adadelta lr=1.0 rho=0.9 eps=1e-6", "asgd": "ASGD lr=1.0 lambd=1e-4 alpha=0.75",
+                    "rprop": "Rprop lr=1.0 etas=(0.5,1.2)"}
 SERVER_STEP_KERNEL = {"adam": "reduce_fused_kernel<OpF32,AdamEpi>", "adamw": "reduce_fused_kernel<OpF32,AdamEpi>",
                       "adagrad": "reduce_kernel<OpF32,AdagradEpi>", "rmsprop": "reduce_kernel<OpF32,AdagradEpi>",
-                      "adamax": "reduce_fused_kernel<OpF32,AdamaxEpi>", "nadam": "reduce_fused_kernel<OpF32,NAdamEpi>",
-                      "radam": "reduce_fused_kernel<OpF32,RAdamEpi>",
-                      "adadelta": "reduce_fused_kernel<OpF32,AdadeltaEpi>"}
+                      **{o: f"reduce_fused_kernel<OpF32,OptRepoEpi<{c}>>" for o, c in
+                         (("adamax", 1), ("nadam", 2), ("radam", 3), ("adadelta", 4), ("asgd", 5), ("rprop", 6))}}
 
 
 def probe_headline(a, world: int, rank: int, coord: Coord):

@@ -26,6 +26,8 @@ FEDAGG_ACC_FP32 = 1
 DT_F32, DT_BF16, DT_F16, DT_F64, DT_I64, DT_I32 = 0, 1, 2, 3, 4, 5
 DIST_CHUNK, PAIR_CHUNK = 1024, 256  # FEDAGG_DIST_CHUNK / FEDAGG_PAIR_CHUNK
 WORK_DIST2, WORK_PAIRDIST2, WORK_PAIRGRAM = 0, 1, 2
+# FEDAGG_OPT_*: the OptRepo optimizers of fedagg_wsum_fedopt_optrepo_f32
+OPT_CODES = {"adamax": 1, "nadam": 2, "radam": 3, "adadelta": 4, "asgd": 5, "rprop": 6}
 
 # Every symbol include/fedagg.h declares, with its ctypes signature.
 _P = ctypes.c_void_p
@@ -55,6 +57,8 @@ SIGNATURES = {
     "fedagg_wsum_fedopt_adamw_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _P, _P, _F, _I32, _U32, _P]),
     "fedagg_wsum_fedopt_rmsprop_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _P, _F, ctypes.c_double, _F, _U32,
                                                       _P]),
+    "fedagg_optrepo_scalars": (ctypes.c_int, [_I32, ctypes.c_double, _I64, _P, _P]),
+    "fedagg_wsum_fedopt_optrepo_f32": (ctypes.c_int, [_I32, _P, _P, _I32, _I64, _P, _P, _P, _P, _U32, _P]),
     "fedagg_wsum_rlr_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _P, _U32, _P]),
     "fedagg_median_f32": (ctypes.c_int, [_P, _I32, _I64, _P, _U32, _P]),
     "fedagg_median": (ctypes.c_int, [_I32, _P, _I32, _I64, _P, _U32, _P]),
@@ -64,6 +68,7 @@ SIGNATURES = {
     "fedagg_host_gather": (ctypes.c_int, [_P, _P, _P, _I32, _I32]),
     "fedagg_host_unpack": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32]),
     "fedagg_host_round_f32": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P]),
+    "fedagg_device_round_f32": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P]),
     "fedagg_robust_work_len": (_I64, [_I32, _I32, _I64]),
     "fedagg_dist2_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _I64, _P]),
     "fedagg_pairdist2_f32": (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P, _I64, _P]),
@@ -72,12 +77,6 @@ SIGNATURES = {
     "fedagg_scale_diff_f32": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P]),
     "fedagg_last_error": (ctypes.c_char_p, []),
     "fedagg_version": (_I32, []),
-    "fedagg_wsum_f32_variant": (ctypes.c_int, [_P, _P, _I32, _I64, _P, _I32, _P]),
-    "fedagg_variant_name": (ctypes.c_char_p, [_I32]),
-    "fedagg_num_variants": (_I32, []),
-    "fedagg_wsum_tiny_variant": (ctypes.c_int, [_I32, _P, _P, _I32, _I64, _P, _I32, _P]),
-    "fedagg_tiny_variant_name": (ctypes.c_char_p, [_I32]),
-    "fedagg_num_tiny_variants": (_I32, []),
 }
 
 

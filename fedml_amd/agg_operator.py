@@ -361,6 +361,33 @@ def _reduce_host_round(w, dicts, keys, weights) -> "OrderedDict[str, torch.Tenso
     return OrderedDict(zip(keys, outs))
 
 
+_DEVICE_ROUND_FN: "int | None" = None
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _reduce_device_round(w, dicts, keys, weights) -> "OrderedDict[str, torch.Tensor] | None":
+    """Small device rounds of fp32 / int64 keys (config 1 on a `using_gpu`
+    server): ONE native call validates the K dicts, allocates the outputs and
+    launches fedagg_device_round_f32 with every pointer and weight in the
+    kernel arguments, on the device's current stream; no uploads, plans or
+    stream lookups in Python.  None when the walker declines (more than 16
+    keys or 128 client tensors, other dtypes, unaligned or non-contiguous
+    tensors, several devices)."""
+    global _DEVICE_ROUND_FN
+    if _RAW_STREAM is None or not hasattr(w, "device_round"):
+        return None
+    if _DEVICE_ROUND_FN is None:
+        import ctypes
+
+        _DEVICE_ROUND_FN = ctypes.cast(nat.lib().fedagg_device_round_f32, ctypes.c_void_p).value
+    got = w.device_round(dicts, keys, weights, _DEVICE_ROUND_FN, _RAW_STREAM)
+    if got is None:
+        return None
+    rc, outs = got
+    nat.check(rc, "fedagg_device_round_f32")
+    return OrderedDict(zip(keys, outs))
+
+
 _BATCH_MAX_BYTES = 256 << 20  # host rounds up to this size stage every client in one pack + one H2D
 _ROW_ESZ = {nat.DT_F32: 4, nat.DT_BF16: 2, nat.DT_F16: 2, nat.DT_F64: 8, nat.DT_I64: 8}
 
@@ -481,6 +508,10 @@ def weighted_reduce(dicts: Sequence["OrderedDict"], keys: Sequence[str], weights
             res = _reduce_resident(w, dicts, keys, weights, acc_mode)
             if res is not None:
                 return res
+            if len(keys) <= 16 and len(keys) * len(dicts) <= 128:
+                res = _reduce_device_round(w, dicts, keys, weights)
+                if res is not None:
+                    return res
         res = _reduce_device_walked(w, dicts, keys, weights, acc_mode)
         if res is not None:
             return res
@@ -638,11 +669,39 @@ def _reads_running_sum(ts: Sequence[torch.Tensor]) -> List[int]:
         if lo < hi0 and lo0 < hi:
             if (lo, hi) == (lo0, hi0) and t.stride() == t0.stride() and t.shape == t0.shape:
                 pos.append(j)
-            else:
+            elif _shares_elements(t0, t):
                 raise NotImplementedError(
                     f"client {j}'s tensor partly overlaps client 0's: the reference's in-place sum would read a "
                     "mix of running and original values, which fedml_amd does not reproduce")
+            # else: interleaved views of one buffer that share no element (e.g.
+            # clients holding different columns of one matrix) -- independent
     return pos
+
+
+_OVERLAP_CHECK_MAX = 1 << 24  # elements: larger interleaved views are refused rather than enumerated
+
+
+def _shares_elements(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Do two views whose byte extents overlap share an element?  Exact for
+    views of one storage with element-aligned offsets (their element index
+    sets are compared); anything else counts as sharing."""
+    if a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr() or a.element_size() != b.element_size():
+        return True
+    if a.numel() + b.numel() > _OVERLAP_CHECK_MAX:
+        return True
+    esz = a.element_size()
+    base = a.untyped_storage().data_ptr()
+    if (a.data_ptr() - base) % esz or (b.data_ptr() - base) % esz:
+        return True
+
+    def elements(t):
+        off = (t.data_ptr() - base) // esz
+        idx = torch.zeros((), dtype=torch.int64)
+        for n, st in zip(t.shape, t.stride()):
+            idx = idx.unsqueeze(-1) + torch.arange(n, dtype=torch.int64) * st
+        return (idx.reshape(-1) + off).numpy()
+
+    return bool(np.intersect1d(elements(a), elements(b)).size)
 
 
 def sequential_sum_inplace(dicts: Sequence["OrderedDict"], keys: Sequence[str], args) -> None:

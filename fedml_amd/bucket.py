@@ -533,6 +533,11 @@ class ClientBucket:
                 s = cur if dt == dom else self._side
                 if ev is not None:
                     ev[0].record(s)
+                if tables is not None:
+                    # a cached table may be read on another stream than the one
+                    # it was uploaded on: evicted later, its block must wait for
+                    # this launch too
+                    tables[dt].record_stream(s)
                 kn.wsum_ptrs(dt, g.d_ptrs if tables is None else tables[dt], w64 if dt == torch.float64 else w32,
                              K, g.length, outs[dt], True, self.acc_mode, s.cuda_stream)
                 if ev is not None:

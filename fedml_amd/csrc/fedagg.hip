@@ -601,6 +601,126 @@ struct AdagradEpi {
   }
 };
 
+// The other elementwise optimizers FedML's OptRepo can name
+// (sp/fedopt/optrepo.py:10: torch.optim's direct Optimizer subclasses), each
+// as FedOptAPI builds it (lr only, torch defaults; fedopt_api.py:78-85) and
+// fused onto the fp32 average like AdamEpi.  Per element, following torch
+// 2.10's single-tensor CPU paths op by op (one rounding per torch op, the
+// fused ones as fmaf; fedagg_optrepo_scalars computes the host scalars):
+//
+//   Adamax   (adamax.py:265-303)   m = lerp(m, g, w1); u = max(u*b2, |g| + eps)  (NaN wins);
+//                                  p = p + (s*m)/u
+//   NAdam    (nadam.py:330-379)    m = lerp; v = fma(c2*g, g, v*b2); d = sqrt(v/bc2) + eps;
+//                                  p = p + (s1*g)/d; p = p + (s2*m)/d
+//   RAdam    (radam.py:301-360)    m, v as NAdam; x = (m/bc1)*lr; rectified steps (rho_t > 5):
+//                                  x = (x * ((1/(sqrt(v) + eps)) * bc2s)) * rect; p = p - x
+//   Adadelta (adadelta.py:281-302) sq = fma(c*g, g, sq*rho); d = sqrt(acc + eps) / sqrt(sq + eps) * g;
+//                                  acc = fma(c*d, d, acc*rho); p = fma(d, -lr, p)
+//   ASGD     (asgd.py:247-275)     p = fma(g, -eta, p*decay); ax = p (mu == 1) or ax + (p - ax)*mu
+//   Rprop    (rprop.py:257-291)    f = {1.2, 0.5, 1}[sign(g*prev)]; ss = clamp(ss*f, 1e-6, 50);
+//                                  g' = f == 0.5 ? 0 : g; p = fma(-sign(g'), ss, p); prev = g'
+//
+// state0 / state1 are the optimizer's two per-element buffers (Adamax:
+// exp_avg / exp_inf; NAdam, RAdam: exp_avg / exp_avg_sq; Adadelta:
+// square_avg / acc_delta; ASGD: ax / unused; Rprop: prev / step_size), in
+// the state torch creates before its first step.  p_old and state0 are
+// prefetched before the client loop, state1 is read in the epilogue (the
+// 128-VGPR cap of reduce_fused_kernel, as for Adam).
+enum : int32_t { kOptAdamax = 1, kOptNAdam = 2, kOptRAdam = 3, kOptAdadelta = 4, kOptASGD = 5, kOptRprop = 6 };
+
+__device__ __forceinline__ float lerp_fma(float m, float g, float w) {  // torch's vectorised lerp_
+  const float d = g - m;
+  return __builtin_fabsf(w) < 0.5f ? __builtin_fmaf(w, d, m) : __builtin_fmaf(w - 1.0f, d, g);
+}
+// torch.sign: (0 < x) - (x < 0), so +0 for ±0 AND for NaN (the robust-LR sign
+// sum of a column holding a NaN still counts the other clients' signs)
+__device__ __forceinline__ float sign_of(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+__device__ __forceinline__ float max_nan(float a, float b) {  // torch.maximum: a NaN operand wins
+  return (a != a || b != b) ? __builtin_nanf("") : __builtin_fmaxf(a, b);
+}
+
+template <int OPT>
+struct OptRepoEpi {
+  float* p;
+  float* s0;
+  float* s1;
+  float k[9];  // fedagg_optrepo_scalars' out9, per optimizer
+  static constexpr int E = 4;
+  static constexpr bool kS0 = OPT != kOptASGD;  // ASGD reads ax only while mu != 1
+  struct Pre {
+    Pack<float, 4> p, a;
+  };
+  __device__ __forceinline__ Pre pre(int64_t off) const {
+    Pre r;
+    r.p = load_pack<float, true>(p + off);
+    r.a = {};
+    if (kS0 || k[3] != 1.0f) r.a = load_pack<float, true>(s0 + off);
+    return r;
+  }
+  __device__ __forceinline__ float step1(float po, float avg, float* a0, float* a1) const {
+    const float g = po - avg;
+    if constexpr (OPT == kOptAdamax) {
+      *a0 = lerp_fma(*a0, g, k[0]);
+      *a1 = max_nan(*a1 * k[1], __builtin_fabsf(g) + k[2]);
+      return po + (k[3] * *a0) / *a1;
+    } else if constexpr (OPT == kOptNAdam) {
+      *a0 = lerp_fma(*a0, g, k[0]);
+      *a1 = __builtin_fmaf(k[2] * g, g, *a1 * k[1]);
+      const float d = __builtin_sqrtf(*a1 / k[3]) + k[4];
+      const float p1 = po + (k[5] * g) / d;
+      return p1 + (k[6] * *a0) / d;
+    } else if constexpr (OPT == kOptRAdam) {
+      *a0 = lerp_fma(*a0, g, k[0]);
+      *a1 = __builtin_fmaf(k[2] * g, g, *a1 * k[1]);
+      float x = (*a0 / k[3]) * k[4];
+      if (k[5] != 0.0f) {
+        const float ad = (1.0f / (__builtin_sqrtf(*a1) + k[6])) * k[7];
+        x = (x * ad) * k[8];
+      }
+      return po - x;
+    } else if constexpr (OPT == kOptAdadelta) {
+      *a0 = __builtin_fmaf(k[1] * g, g, *a0 * k[0]);
+      const float sd = __builtin_sqrtf(*a0 + k[2]);
+      const float d = (__builtin_sqrtf(*a1 + k[2]) / sd) * g;
+      *a1 = __builtin_fmaf(k[1] * d, d, *a1 * k[0]);
+      return __builtin_fmaf(d, k[3], po);
+    } else if constexpr (OPT == kOptASGD) {
+      const float pn = __builtin_fmaf(g, k[1], po * k[0]);
+      *a0 = k[3] == 1.0f ? pn : *a0 + (pn - *a0) * k[2];
+      return pn;
+    } else {  // kOptRprop
+      const float sg = sign_of(g * *a0);
+      const float f = sg > 0.f ? k[0] : (sg < 0.f ? k[1] : 1.0f);
+      const float ss = *a1 * f;
+      *a1 = ss != ss ? ss : __builtin_fminf(__builtin_fmaxf(ss, k[2]), k[3]);
+      const float g2 = f == k[1] ? 0.0f : g;
+      *a0 = g2;
+      return __builtin_fmaf(-sign_of(g2), *a1, po);
+    }
+  }
+  __device__ __forceinline__ void pack(int64_t off, const float (&acc)[E], const Pre& pr) const {
+    float po[E], ao[E], bo[E];
+    Pack<float, 4> b = {};
+    if constexpr (OPT != kOptASGD) b = load_pack<float, true>(s1 + off);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      ao[e] = pr.a.v[e];
+      bo[e] = b.v[e];
+      po[e] = step1(pr.p.v[e], acc[e], &ao[e], &bo[e]);
+    }
+    store_pack<float, E>(p + off, po);
+    store_pack<float, E>(s0 + off, ao);
+    if constexpr (OPT != kOptASGD) store_pack<float, E>(s1 + off, bo);
+  }
+  __device__ __forceinline__ void one(int64_t e, float a) const {
+    float a0 = (kS0 || k[3] != 1.0f) ? s0[e] : 0.f;
+    float a1 = OPT != kOptASGD ? s1[e] : 0.f;
+    p[e] = step1(p[e], a, &a0, &a1);
+    s0[e] = a0;
+    if constexpr (OPT != kOptASGD) s1[e] = a1;
+  }
+};
+
 // LightSecAgg model reconstruction epilogue
 // (cross_silo/lightsecagg/lsa_fedml_aggregator.py:139-166 with
 // core/mpc/lightsecagg.py:157-182): on the wrapping int64 client sum
@@ -644,9 +764,6 @@ struct LsaEpi {
 struct RlrAcc {
   float a, s;
 };
-// torch.sign: (0 < x) - (x < 0), so +0 for ±0 AND for NaN (the sign sum of a
-// column holding a NaN still counts the other clients' signs)
-__device__ __forceinline__ float sign_of(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 struct OpF32Rlr {
   using in_t = float; using out_t = float; using acc_t = RlrAcc; using w_t = float;
   static __device__ __forceinline__ acc_t first(in_t x, w_t w) { return {x * w, sign_of(x)}; }
@@ -870,6 +987,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void re
   reduce_block<OP, U, V, NT, ALIGNED, BS>(s, epi, w, K, int64_t(blockIdx.x) * BS * V);
 }
 
+#ifdef FEDAGG_TUNING
 // XCD-contiguous tile order (tuning variant): workgroups are dispatched to the
 // 8 XCDs round-robin, so block b runs on XCD b % 8; this remap gives each XCD
 // one contiguous range of tiles instead of every eighth tile (a bijection for
@@ -889,6 +1007,8 @@ __global__ __launch_bounds__(BS) void reduce_persistent_kernel(Seg<OP> s, StoreE
   for (int64_t b = blockIdx.x; b < tiles; b += gridDim.x)
     reduce_block<OP, U, V, NT, true, BS>(s, epi, w, K, b * BS * V);
 }
+
+#endif  // FEDAGG_TUNING
 
 // Multi-tensor form: blockIdx -> (segment, block within segment) by binary
 // search over the prefix of per-segment block counts (wave-uniform, s_load).
@@ -1223,6 +1343,14 @@ int launch(const void* const* src, const void* w, int32_t K, int64_t N, void* ou
 }
 
 // ---------------------------------------------------------------------------
+// Tuning build only (tools/build_tuning.py compiles this file with
+// -DFEDAGG_TUNING into tools/_build/libfedagg_tuning.so): the A/B tables the
+// shipped tile shapes were chosen from.  The product library carries none of it.
+#ifdef FEDAGG_TUNING
+#define FEDAGG_TUNE_BF16_F32OUT 0x101  // bf16 rows, fp32 partial out
+#define FEDAGG_TUNE_BF16_ACC32 0x102   // bf16 rows, fp32 accumulation
+
+// ---------------------------------------------------------------------------
 // Tuning table for the fp32 kernel (fedagg_wsum_f32_variant).
 
 struct Variant {
@@ -1354,6 +1482,7 @@ const TinyVariant kTinyVariants[] = {
 };
 #undef FEDAGG_TINY_NARROW
 constexpr int kNumTinyVariants = sizeof(kTinyVariants) / sizeof(kTinyVariants[0]);
+#endif  // FEDAGG_TUNING
 
 // ---------------------------------------------------------------------------
 // fp32 -> bf16 / f16 rounding of a reduced shard (the client-axis multi-GPU
@@ -1567,7 +1696,7 @@ int check_ranges(int32_t n, const void* a, const void* b, const int64_t* offs, c
     if (nbytes[i] < 0 || offs[i] < 0) return set_error(FEDAGG_EINVAL, std::string(what) + ": negative size");
   return FEDAGG_OK;
 }
-}  // namespace
+// (the anonymous namespace continues: the small-round machinery below is internal too)
 
 // ---------------------------------------------------------------------------
 // One small host-resident round, host to host (fedagg_host_round_f32).
@@ -1636,6 +1765,82 @@ __global__ __launch_bounds__(kRoundBlock) void host_round_kernel(const float* __
       __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// One small round of device tensors in one launch (fedagg_device_round_f32).
+//
+// A GPU server (`using_gpu`) hands FedMLAggOperator.agg device tensors; at
+// config 1 (4 clients x 2 keys, 31 KB) the reduction is a few microseconds and
+// the pointer-table and weight uploads, output allocation and per-key launches
+// around it decide the time.  Here every client pointer, output pointer, key
+// length and weight travels in the kernel arguments (no upload at all) and one
+// launch covers every key: a workgroup owns 1,024 consecutive elements of one
+// key (4 per lane, 16-byte loads), keys looked up by a wave-uniform scan of
+// their first-block prefix.  Same arithmetic as every FedAvg kernel:
+// acc = x_0*w_0; acc = acc + x_i*w_i; int64 keys as fl32(v) (torch's int64 *
+// float promotion) into fp32 outputs.
+constexpr int kDevRoundMaxKeys = 16;
+constexpr int kDevRoundMaxPtrs = 128;
+constexpr int kDevRoundBlock = 256;
+constexpr int kDevRoundElems = kDevRoundBlock * 4;
+
+struct DevRoundArgs {
+  const void* src[kDevRoundMaxPtrs];  // [T][K]
+  float* out[kDevRoundMaxKeys];
+  int64_t numel[kDevRoundMaxKeys];
+  int64_t block0[kDevRoundMaxKeys + 1];  // first workgroup of key t; block0[T] = grid
+  float w[kDevRoundMaxPtrs];
+  int32_t code[kDevRoundMaxKeys];
+  int32_t T, K;
+};
+
+template <class T>
+__device__ __forceinline__ float dr_load(const void* p, int64_t e) {
+  if constexpr (std::is_same<T, float>::value)
+    return reinterpret_cast<const float*>(p)[e];
+  else
+    return static_cast<float>(reinterpret_cast<const int64_t*>(p)[e]);
+}
+
+template <class T>
+__device__ __forceinline__ void dr_key(const DevRoundArgs& a, int t, int64_t e, int64_t n) {
+  const void* const* src = a.src + t * a.K;
+  if (e + 4 <= n && std::is_same<T, float>::value) {
+    float4 acc;
+    {
+      const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src[0]) + e);
+      const float w0 = a.w[0];
+      acc = make_float4(x.x * w0, x.y * w0, x.z * w0, x.w * w0);
+    }
+    for (int i = 1; i < a.K; ++i) {
+      const float4 x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src[i]) + e);
+      const float wi = a.w[i];
+      acc.x = acc.x + x.x * wi;
+      acc.y = acc.y + x.y * wi;
+      acc.z = acc.z + x.z * wi;
+      acc.w = acc.w + x.w * wi;
+    }
+    *reinterpret_cast<float4*>(a.out[t] + e) = acc;
+    return;
+  }
+  for (int64_t j = e; j < e + 4 && j < n; ++j) {
+    float acc = dr_load<T>(src[0], j) * a.w[0];
+    for (int i = 1; i < a.K; ++i) acc = acc + dr_load<T>(src[i], j) * a.w[i];
+    a.out[t][j] = acc;
+  }
+}
+
+__global__ __launch_bounds__(kDevRoundBlock) void device_round_kernel(const DevRoundArgs a) {
+  int t = 0;
+  while (t + 1 < a.T && int64_t(blockIdx.x) >= a.block0[t + 1]) ++t;  // wave-uniform
+  const int64_t e = (int64_t(blockIdx.x) - a.block0[t]) * kDevRoundElems + int64_t(threadIdx.x) * 4;
+  const int64_t n = a.numel[t];
+  if (e >= n) return;
+  if (a.code[t] == FEDAGG_DT_F32)
+    dr_key<float>(a, t, e, n);
+  else
+    dr_key<int64_t>(a, t, e, n);
 }
 
 // A persistent pool for the host copies of a round (spawning threads per call
@@ -1749,7 +1954,6 @@ void split_rows(int64_t bytes, int n, const F& fn) {  // fn(i) for i in [0, n), 
 // C ABI
 // ===========================================================================
 
-namespace {
 // FedAvg fused with a server-optimizer epilogue (SgdEpi / AdamEpi): the tile
 // configuration by size, as launch_ws picks it for plain FedAvg.  FUSED_CAP
 // selects reduce_fused_kernel (capped at 128 VGPRs for Adam's operands).
@@ -2093,6 +2297,103 @@ int fedagg_wsum_fedopt_rmsprop_f32(const float* const* d_src, const float* d_w, 
   return check_launch("fedagg_wsum_fedopt_rmsprop_f32");
 }
 
+int fedagg_optrepo_scalars(int32_t opt, double lr, int64_t step, float* carry2, float* out9) {
+  if (!out9 || step < 1) return set_error(FEDAGG_EINVAL, "fedagg_optrepo_scalars: step must be >= 1");
+  for (int i = 0; i < 9; ++i) out9[i] = 0.0f;
+  // torch's double-precision scalar chains (Python's ** is C pow()); every
+  // value a CPU kernel receives as a Python float is rounded to fp32 here
+  const double t = double(step);
+  const double b1 = 0.9, b2 = 0.999;
+  switch (opt) {
+    case kOptAdamax: {
+      const double clr = lr / (1.0 - std::pow(b1, t));
+      out9[0] = float(1.0 - b1); out9[1] = float(b2); out9[2] = float(1e-8); out9[3] = float(-clr);
+      return FEDAGG_OK;
+    }
+    case kOptNAdam: {
+      if (!carry2) return set_error(FEDAGG_EINVAL, "fedagg_optrepo_scalars: NAdam needs carry2 (mu_product)");
+      const double md = 4e-3;
+      const double mu = b1 * (1.0 - 0.5 * std::pow(0.96, t * md));
+      const double mu_next = b1 * (1.0 - 0.5 * std::pow(0.96, (t + 1.0) * md));
+      carry2[0] = carry2[0] * float(mu);  // mu_product *= mu: an fp32 state tensor
+      const double mp = double(carry2[0]);
+      const double mp_next = mp * mu_next;
+      out9[0] = float(1.0 - b1); out9[1] = float(b2); out9[2] = float(1.0 - b2);
+      out9[3] = float(1.0 - std::pow(b2, t)); out9[4] = float(1e-8);
+      out9[5] = float(-lr * (1.0 - mu) / (1.0 - mp));
+      out9[6] = float(-lr * mu_next / (1.0 - mp_next));
+      return FEDAGG_OK;
+    }
+    case kOptRAdam: {
+      const double bc1 = 1.0 - std::pow(b1, t), bc2 = 1.0 - std::pow(b2, t);
+      const double rho_inf = 2.0 / (1.0 - b2) - 1.0;
+      const double rho_t = rho_inf - 2.0 * t * std::pow(b2, t) / bc2;
+      out9[0] = float(1.0 - b1); out9[1] = float(b2); out9[2] = float(1.0 - b2);
+      out9[3] = float(bc1); out9[4] = float(lr); out9[6] = float(1e-8);
+      if (rho_t > 5.0) {
+        out9[5] = 1.0f;
+        out9[7] = float(std::pow(bc2, 0.5));
+        out9[8] = float(std::pow((rho_t - 4.0) * (rho_t - 2.0) * rho_inf / ((rho_inf - 4.0) * (rho_inf - 2.0) * rho_t),
+                                 0.5));
+      }
+      return FEDAGG_OK;
+    }
+    case kOptAdadelta:
+      out9[0] = float(0.9); out9[1] = float(1.0 - 0.9); out9[2] = float(1e-6); out9[3] = float(-lr);
+      return FEDAGG_OK;
+    case kOptASGD: {
+      if (!carry2) return set_error(FEDAGG_EINVAL, "fedagg_optrepo_scalars: ASGD needs carry2 (eta, mu)");
+      const double lambd = 1e-4, alpha = 0.75, t0 = 1e6;
+      const double eta = double(carry2[0]);
+      out9[0] = float(1.0 - lambd * eta); out9[1] = float(-eta); out9[2] = carry2[1];
+      out9[3] = carry2[1] == 1.0f ? 1.0f : 0.0f;
+      carry2[0] = float(lr / std::pow(1.0 + lambd * lr * t, alpha));  // eta.copy_(...), after the step
+      carry2[1] = float(1.0 / std::max(1.0, t - t0));
+      return FEDAGG_OK;
+    }
+    case kOptRprop:
+      out9[0] = float(1.2); out9[1] = float(0.5); out9[2] = float(1e-6); out9[3] = float(50.0);
+      return FEDAGG_OK;
+    default:
+      return set_error(FEDAGG_EINVAL, "fedagg_optrepo_scalars: unknown optimizer code");
+  }
+}
+
+int fedagg_wsum_fedopt_optrepo_f32(int32_t opt, const float* const* d_src, const float* d_w, int32_t K, int64_t N,
+                                   float* d_param, float* d_state0, float* d_state1, const float* scalars9,
+                                   uint32_t flags, fedagg_stream_t stream) {
+  const char* name = "fedagg_wsum_fedopt_optrepo_f32";
+  if (K < 1 || N < 0) return set_error(FEDAGG_EINVAL, std::string(name) + ": K must be >= 1 and N >= 0");
+  if (opt < kOptAdamax || opt > kOptRprop) return set_error(FEDAGG_EINVAL, std::string(name) + ": unknown optimizer");
+  if (!d_src || !d_w || !d_param || !d_state0 || (opt != kOptASGD && !d_state1) || !scalars9)
+    return set_error(FEDAGG_EINVAL, std::string(name) + ": null pointer");
+  if (N == 0) return FEDAGG_OK;
+  if (blocks_for<OpF32>(N) > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, std::string(name) + ": N too large");
+  const Seg<OpF32> s{d_src, N};
+  auto st = reinterpret_cast<hipStream_t>(stream);
+  const bool aligned = (flags & FEDAGG_ALIGNED16) != 0;
+  InlW<float> iw;
+  const bool host_w = (flags & FEDAGG_HOST_WEIGHTS) != 0;
+  if (host_w && !inline_weights<float>(d_w, K, &iw))
+    return set_error(FEDAGG_EINVAL, std::string(name) + ": FEDAGG_HOST_WEIGHTS needs K <= 256");
+  auto run = [&](auto epi) {
+    for (int i = 0; i < 9; ++i) epi.k[i] = scalars9[i];
+    if (host_w)
+      launch_fused<true>(s, epi, iw, K, aligned, st);
+    else
+      launch_fused<true>(s, epi, PtrW<float>{d_w}, K, aligned, st);
+  };
+  switch (opt) {
+    case kOptAdamax: run(OptRepoEpi<kOptAdamax>{d_param, d_state0, d_state1, {}}); break;
+    case kOptNAdam: run(OptRepoEpi<kOptNAdam>{d_param, d_state0, d_state1, {}}); break;
+    case kOptRAdam: run(OptRepoEpi<kOptRAdam>{d_param, d_state0, d_state1, {}}); break;
+    case kOptAdadelta: run(OptRepoEpi<kOptAdadelta>{d_param, d_state0, d_state1, {}}); break;
+    case kOptASGD: run(OptRepoEpi<kOptASGD>{d_param, d_state0, d_state1, {}}); break;
+    default: run(OptRepoEpi<kOptRprop>{d_param, d_state0, d_state1, {}}); break;
+  }
+  return check_launch(name);
+}
+
 int fedagg_round_f32(int32_t dtype, const float* d_in, int64_t N, void* d_out, fedagg_stream_t stream) {
   if (N < 0 || (N > 0 && (!d_in || !d_out))) return set_error(FEDAGG_EINVAL, "fedagg_round_f32: bad argument");
   if (dtype != FEDAGG_DT_BF16 && dtype != FEDAGG_DT_F16)
@@ -2162,6 +2463,42 @@ int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_of
       n, nbytes, threads, [&](int32_t i) { return static_cast<const char*>(src) + src_offs[i]; },
       [&](int32_t i) { return static_cast<char*>(dsts[i]); });
   return FEDAGG_OK;
+}
+
+int fedagg_device_round_f32(const void* const* d_src, const int32_t* codes, const int64_t* numels, int32_t T,
+                            int32_t K, const float* weights, void* const* d_out, fedagg_stream_t stream) {
+  const char* name = "fedagg_device_round_f32";
+  if (T < 1 || K < 1 || T > kDevRoundMaxKeys || int64_t(T) * K > kDevRoundMaxPtrs || !d_src || !codes || !numels ||
+      !weights || !d_out)
+    return set_error(FEDAGG_EINVAL, std::string(name) + ": bad argument (T <= 16 keys, T*K <= 128 pointers)");
+  DevRoundArgs a;
+  a.T = T;
+  a.K = K;
+  int64_t blocks = 0;
+  for (int t = 0; t < T; ++t) {
+    if (codes[t] != FEDAGG_DT_F32 && codes[t] != FEDAGG_DT_I64)
+      return set_error(FEDAGG_EINVAL, std::string(name) + ": keys must be fp32 or int64");
+    if (numels[t] < 0) return set_error(FEDAGG_EINVAL, std::string(name) + ": negative numel");
+    for (int i = 0; i < K; ++i) {
+      a.src[t * K + i] = d_src[size_t(t) * K + i];
+      if (numels[t] && (!a.src[t * K + i] || (reinterpret_cast<uintptr_t>(a.src[t * K + i]) & 15)))
+        return set_error(FEDAGG_EINVAL, std::string(name) + ": client pointers must be 16-byte aligned");
+    }
+    a.out[t] = static_cast<float*>(d_out[t]);
+    if (numels[t] && (!a.out[t] || (reinterpret_cast<uintptr_t>(a.out[t]) & 15)))
+      return set_error(FEDAGG_EINVAL, std::string(name) + ": outputs must be 16-byte aligned");
+    a.numel[t] = numels[t];
+    a.code[t] = codes[t];
+    a.block0[t] = blocks;
+    blocks += (numels[t] + kDevRoundElems - 1) / kDevRoundElems;
+  }
+  a.block0[T] = blocks;
+  for (int i = 0; i < K; ++i) a.w[i] = weights[i];
+  if (blocks == 0) return FEDAGG_OK;
+  if (blocks > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, std::string(name) + ": round too large");
+  hipLaunchKernelGGL(device_round_kernel, dim3(unsigned(blocks)), dim3(kDevRoundBlock), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return check_launch(name);
 }
 
 int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes, const int64_t* numels, int32_t T,
@@ -2295,6 +2632,7 @@ __attribute__((visibility("hidden"))) int fedagg_set_error_internal(int code, co
 
 int32_t fedagg_version(void) { return 1; }
 
+#ifdef FEDAGG_TUNING  // the tuning entries (tools/tuning_lib.py)
 int fedagg_wsum_f32_variant(const float* const* d_src, const float* d_w, int32_t K, int64_t N, float* d_out,
                             int32_t variant, fedagg_stream_t stream) {
   if (variant < 0 || variant >= kNumVariants) return set_error(FEDAGG_EINVAL, "bad variant");
@@ -2333,5 +2671,6 @@ const char* fedagg_tiny_variant_name(int32_t variant) {
 }
 
 int32_t fedagg_num_tiny_variants(void) { return kNumTinyVariants; }
+#endif  // FEDAGG_TUNING
 
 }  // extern "C"

@@ -13,45 +13,31 @@
 
 #include "../../include/fedagg.h"
 
-// A/B knob for tools/median_ab.py: 1 keeps the mirrored-pair merge (a lane
-// select per cross-lane step) in the packed 4-lane kernels
-#ifndef FEDAGG_PK16_MIRROR
-#define FEDAGG_PK16_MIRROR 0
-#endif
+// 1 would keep the mirrored-pair merge (a lane select per cross-lane step) in
+// the packed 4-lane kernels; 0 since round 4 (NOTES.md §5b)
+constexpr int kPk16Mirror = 0;
 // reversed DPP reads issued per batch in lanes4_merge_median
-#ifndef FEDAGG_PK16_BATCH
-#define FEDAGG_PK16_BATCH 2
-#endif
+constexpr int kPk16Batch = 2;
 // Packed 16-bit lane groups (128 < K <= 1024): 1 selects the median by
 // counting (median_pk16_count: byte-wise bisection with v_sad_u8), 0 by the
-// sorting networks and cross-lane merges (A/B knob for tools/median_ab.py)
-#ifndef FEDAGG_PK16_COUNT
-#define FEDAGG_PK16_COUNT 1
-#endif
+// sorting networks and cross-lane merges (the round-3 form, NOTES.md §5b)
+constexpr int kPk16Count = 1;
 // values per lane of the counting kernels (P = KMAX / R lanes per column pair;
 // 64 and 32, i.e. 8 and 16 rows per wave instruction, ran config 4 in 32 and
 // 66 ms against 21 ms at 128: profiles/r04/c/median_ab_variants.json)
-#ifndef FEDAGG_PK16_COUNT_R
-#define FEDAGG_PK16_COUNT_R 128
-#endif
+constexpr int kPk16CountR = 128;
 // independent v_sad_u8 accumulator chains per sum (4: 21.3 vs 22.5 ms at
 // config 4's 512 clients, profiles/r04/c/)
-#ifndef FEDAGG_SAD_CHAINS
-#define FEDAGG_SAD_CHAINS 4
-#endif
+constexpr int kSadChains = 4;
 // Loads of the lane-group kernels: a wave instruction reads 64 B of each of P
 // rows' 128-B lines and the block's next wave reads the other half, so plain
 // loads (0) keep the line in L2 for it; non-temporal ones (1) fetched 1.04-1.5x
 // the algorithmic bytes vs 1.00-1.03x, at the same time
 // (profiles/r03/lanes_nt/)
-#ifndef FEDAGG_LANES_NT
-#define FEDAGG_LANES_NT 0
-#endif
+constexpr int kLanesNT = 0;
 // Loads of the one-lane-per-column kernels (K <= 128; 256 B per wave
 // instruction): 1 non-temporal, 0 plain
-#ifndef FEDAGG_COLS_NT
-#define FEDAGG_COLS_NT 1
-#endif
+constexpr int kColsNT = 1;
 
 extern "C" int fedagg_set_error_internal(int code, const char* msg);
 
@@ -72,18 +58,18 @@ __device__ __forceinline__ const T __attribute__((address_space(1)))* as_global(
   return (const T __attribute__((address_space(1)))*)(p);
 }
 
-// loads of the lane-group kernels (FEDAGG_LANES_NT)
+// loads of the lane-group kernels (kLanesNT)
 template <class T>
 __device__ __forceinline__ T lanes_load(const T __attribute__((address_space(1)))* p) {
-  if constexpr (FEDAGG_LANES_NT)
+  if constexpr (kLanesNT)
     return __builtin_nontemporal_load(p);
   else
     return *p;
 }
-// loads of the one-lane-per-column kernels (FEDAGG_COLS_NT)
+// loads of the one-lane-per-column kernels (kColsNT)
 template <class T>
 __device__ __forceinline__ T cols_load(const T __attribute__((address_space(1)))* p) {
-  if constexpr (FEDAGG_COLS_NT)
+  if constexpr (kColsNT)
     return __builtin_nontemporal_load(p);
   else
     return *p;
@@ -640,7 +626,7 @@ __device__ __forceinline__ void lanes_merge_levels(float (&v)[R], int sub) {
 
 template <class T, int R>
 __device__ __forceinline__ T lanes4_merge_median(T (&v)[R]) {
-  constexpr int B = FEDAGG_PK16_BATCH;  // reversed reads in batches: none right behind its register's write
+  constexpr int B = kPk16Batch;  // reversed reads in batches: none right behind its register's write
 #pragma unroll
   for (int i0 = 0; i0 < R; i0 += B) {
     T t[B];
@@ -833,7 +819,7 @@ template <class E>
 __device__ uint32_t g_median_pad2[2] = {E::kNegInf * 0x10001u, E::kPosInf * 0x10001u};
 
 // ---------------------------------------------------------------------------
-// Selection by counting (FEDAGG_PK16_COUNT), for the packed lane groups: the
+// Selection by counting (kPk16Count), for the packed lane groups: the
 // sorting networks above spend ~35 half-rate min/max per value at 512
 // clients (VALU-bound at 0.85 of the SIMDs' issue capacity).  Counting needs
 // far fewer operations per value:
@@ -887,7 +873,7 @@ __device__ __forceinline__ void sad_bisect(const uint32_t (&b0)[NB], const uint3
   for (int bit = 7; bit >= 0; --bit) {
     const uint32_t p0 = (v0 + (1u << bit) - 1u) * 0x01010101u, p1 = (v1 + (1u << bit) - 1u) * 0x01010101u;
     const uint32_t q0 = p0 + 0x01010101u, q1 = p1 + 0x01010101u;
-    constexpr int C = FEDAGG_SAD_CHAINS < NB ? FEDAGG_SAD_CHAINS : NB;
+    constexpr int C = kSadChains < NB ? kSadChains : NB;
     uint32_t s0[C], t0[C], s1[C], t1[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) s0[c] = t0[c] = s1[c] = t1[c] = 0;
@@ -1023,7 +1009,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
 #pragma unroll
   for (int j = 0; j < R; ++j) v[j] = pk16_key(raw[j]);
   short2_t m;
-  if constexpr (P == 4 && !FEDAGG_PK16_MIRROR) {
+  if constexpr (P == 4 && !kPk16Mirror) {
     // odd lanes hold complemented keys (~k reverses the int16 order): every
     // cross-lane step is min(own, ~partner) in every lane (lanes4_merge_median)
     const short2_t flip = (sub & 1) ? short2_t(short(-1)) : short2_t(short(0));
@@ -1176,8 +1162,8 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
     if constexpr (sizeof(typename E::S) == 2) {
       if (aligned && K <= 4096) {  // two columns per lane on packed int16 keys
-        if constexpr (FEDAGG_PK16_COUNT) {  // selection by counting: R values per lane, 256 / R .. 1024 / R lanes
-          constexpr int RC = FEDAGG_PK16_COUNT_R;
+        if constexpr (kPk16Count) {  // selection by counting: R values per lane, 256 / R .. 1024 / R lanes
+          constexpr int RC = kPk16CountR;
           if (K <= 256) return launch_median_pk16_lanes<256 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
           if (K <= 512) return launch_median_pk16_lanes<512 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
           if (K <= 1024) return launch_median_pk16_lanes<1024 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);

@@ -35,19 +35,6 @@
 
 #include "../../include/fedagg.h"
 
-#ifndef FEDAGG_CLIP_CLIENTS
-#define FEDAGG_CLIP_CLIENTS 2
-#endif
-#ifndef FEDAGG_DIST2_BATCH
-#define FEDAGG_DIST2_BATCH 16
-#endif
-#ifndef FEDAGG_DIST2_REF_NT
-#define FEDAGG_DIST2_REF_NT false
-#endif
-// client rows of dist2: non-temporal (true) or plain loads
-#ifndef FEDAGG_DIST2_X_NT
-#define FEDAGG_DIST2_X_NT true
-#endif
 
 extern "C" int fedagg_set_error_internal(int code, const char* msg);
 
@@ -75,7 +62,7 @@ constexpr int kLaneCols = FEDAGG_DIST_CHUNK / 64;  // columns per lane per chunk
 // would cover 128 clients in one pass but costs the occupancy: 2.61 vs 1.99 ms
 // at config 3 (tools/robust_variants.py, profiles/r03/dist/); with the
 // reference row cached in L2 (ld4<false>) the second pass's re-read is cheap
-constexpr int kBatch = FEDAGG_DIST2_BATCH;
+constexpr int kBatch = 16;  // dist2: clients per batch (16 vs 32: profiles/r03/dist/)
 
 // A workgroup barrier that waits for this wave's LDS operations only.
 // __syncthreads() carries a release fence that waits for EVERY outstanding
@@ -153,7 +140,7 @@ __global__ __launch_bounds__(kBS) void dist2_kernel(const float* const* __restri
       const int len = int(chunks[2 * c + 1]);
       f32x4 r[kLaneCols / 4];
       if (ref) {
-        load_chunk<FEDAGG_DIST2_REF_NT>(ref + start, len, lane, r);
+        load_chunk<false>(ref + start, len, lane, r);
       } else {
 #pragma unroll
         for (int u = 0; u < kLaneCols / 4; ++u) r[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -163,7 +150,7 @@ __global__ __launch_bounds__(kBS) void dist2_kernel(const float* const* __restri
         const int i = cb + w + kWaves * j;
         if (i < K) {  // wave-uniform
           f32x4 x[kLaneCols / 4];
-          load_chunk<FEDAGG_DIST2_X_NT>(src[i] + start, len, lane, x);
+          load_chunk<true>(src[i] + start, len, lane, x);
 #pragma unroll
           for (int u = 0; u < kLaneCols / 4; ++u) {
             acc[j] = sq_diff(x[u].x, r[u].x, acc[j]);
@@ -637,20 +624,7 @@ __global__ __launch_bounds__(256) void tri_finish_kernel(const double* __restric
 // order as the reference's own fp32 torch.norm when the clients' spread is
 // of the order of their distances (tests/test_gpu_dist_defenses.py checks
 // the Krum selections and D against the exact-difference kernel).
-// stages (64 columns each) summed in fp32 by the MFMAs before one fp64 fold
-// (2 / 4: 5.19 / 5.09 against 5.44 ms at config 3, for a 2x / 4x longer fp32
-// chain per partial; profiles/r04/f/gram_map.json; kept at 1)
-#ifndef FEDAGG_GRAM_FOLD
-#define FEDAGG_GRAM_FOLD 1
-#endif
-// Diagnostics for tools/gram_variants.py (wrong results, timing only):
-// 1 skips the MFMA phase, 2 skips the staging of every stage after the first
-#ifndef FEDAGG_GRAM_DIAG
-#define FEDAGG_GRAM_DIAG 0
-#endif
 constexpr int kGramMax = 128;          // clients the Gram kernel holds (8 groups of 16)
-constexpr int kGramBS = 256;           // 4 waves: one per SIMD
-constexpr int kGramRS = kStage + 4;    // LDS row stride in floats
 constexpr int kGramBlocksPerCU = 2;    // 2 x (2 stage buffers of 128 rows) = 143 KB of LDS per CU
 
 __host__ __device__ inline int gram_groups(int K) { return (K + 15) / 16; }
@@ -671,216 +645,9 @@ __device__ __forceinline__ int2 gram_tile(int t, int nb) {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-template <int NB>
-__global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
-    const float* const* __restrict__ src, int K, const int64_t* __restrict__ chunks, int64_t n_chunks, int G,
-    double* __restrict__ partial) {
-  constexpr int ROWS = NB * 16;
-  constexpr int TPW = (NB * (NB + 1) / 2 + 3) / 4;  // tiles per wave, at most
-  constexpr int LPW = ROWS / 16;                    // 16-byte loads per lane and stage (4 rows per wave-load)
-  // the tiles of THIS K (the finish kernel and the workspace size use the
-  // same count): nb groups of 16 clients, NT tiles, TPWr per wave
-  const int nb = gram_groups(K), NT = nb * (nb + 1) / 2, TPWr = (NT + 3) / 4;
-  __shared__ float sX[2][ROWS * kGramRS];
-  __shared__ float sSum[2][4][kStage];
-  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int i16 = lane & 15, q = lane >> 4;
-  // Staging: wave w owns rows w * ROWS/4 .. + ROWS/4; each wave-load covers 4
-  // rows (lane group q) x 64 columns (lane i16: columns 4 i16 .. 4 i16 + 3)
-  // with 16-byte loads, so every lane addresses its own row (VGPR pointers:
-  // one pointer per row in SGPRs spilled and serialized the loads).
-  const float* rowp[LPW];
-  bool rlive[LPW];
-#pragma unroll
-  for (int u = 0; u < LPW; ++u) {
-    const int cl = wave * (ROWS / 4) + 4 * u + q;
-    rlive[u] = cl < K;
-    rowp[u] = src[cl < K ? cl : 0];
-  }
-  const int t0 = wave * TPWr;
-  const int nmine = NT - t0 < TPWr ? (NT - t0 > 0 ? NT - t0 : 0) : TPWr;
-  double acc64[TPW][4];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc64[j][r] = 0.0;
-  const float invK = 1.0f / float(K);
-  int64_t c = g;
-  int s0 = 0;
-  f32x4 v[LPW];
-  int w_next = 0;
-  auto fetch = [&]() {
-    if (c >= n_chunks) return false;
-    const int len = int(chunks[2 * c + 1]);
-    const int64_t col0 = chunks[2 * c] + s0;
-    w_next = len - s0 < kStage ? len - s0 : kStage;
-    const int c4 = 4 * i16;
-    if (w_next == kStage) {  // wave-uniform: a full stage, one unconditional 16-byte load per row
-      // raw values: the rows past K are zeroed in stage_to, so nothing here
-      // consumes the loads and they stay in flight through the next compute
-#pragma unroll
-      for (int u = 0; u < LPW; ++u) v[u] = ld4<true>(rowp[u] + col0 + c4);
-    } else {  // the ragged end of a chunk: element loads, never past column w
-#pragma unroll
-      for (int u = 0; u < LPW; ++u) {
-        const float* p = rowp[u] + col0;
-        const bool ok = rlive[u];
-        v[u].x = ok && c4 < w_next ? gptr(p)[c4] : 0.f;
-        v[u].y = ok && c4 + 1 < w_next ? gptr(p)[c4 + 1] : 0.f;
-        v[u].z = ok && c4 + 2 < w_next ? gptr(p)[c4 + 2] : 0.f;
-        v[u].w = ok && c4 + 3 < w_next ? gptr(p)[c4 + 3] : 0.f;
-      }
-    }
-    s0 += kStage;
-    if (s0 >= len) {
-      s0 = 0;
-      c += G;
-    }
-    return true;
-  };
-  auto fetch_skip = [&]() {  // FEDAGG_GRAM_DIAG == 2: advance the stage walk only
-    if (c >= n_chunks) return false;
-    const int len = int(chunks[2 * c + 1]);
-    s0 += kStage;
-    if (s0 >= len) {
-      s0 = 0;
-      c += G;
-    }
-    return true;
-  };
-  // Staging, in two halves around a barrier: stage_sums publishes this
-  // wave's column sums of the loaded rows (still in registers), and once
-  // every wave's sums are in, stage_centred writes the rows minus the column
-  // mean (the fragments then need no centring: no means held in registers
-  // and no subtracts in the MFMA loop).
-  auto masked = [&](int u) {
-    const uint32_t m = rlive[u] ? 0xffffffffu : 0u;  // a row past K (it loaded row 0)
-    return f32x4{__uint_as_float(__float_as_uint(v[u].x) & m), __uint_as_float(__float_as_uint(v[u].y) & m),
-                 __uint_as_float(__float_as_uint(v[u].z) & m), __uint_as_float(__float_as_uint(v[u].w) & m)};
-  };
-  auto stage_sums = [&](int buf) {
-    f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < LPW; ++u) cs += masked(u);
-    // the wave's column sums: add the four lane groups (xor 16, xor 32)
-#pragma unroll
-    for (int m = 16; m <= 32; m <<= 1) {
-      cs.x += __shfl_xor(cs.x, m, 64);
-      cs.y += __shfl_xor(cs.y, m, 64);
-      cs.z += __shfl_xor(cs.z, m, 64);
-      cs.w += __shfl_xor(cs.w, m, 64);
-    }
-    if (q == 0) *reinterpret_cast<f32x4*>(&sSum[buf][wave][4 * i16]) = cs;
-  };
-  auto stage_centred = [&](int buf) {
-    // this lane's 4 columns' means, the four waves' sums in a fixed order;
-    // 0 past the stage's width (every row is 0 there)
-    const f32x4 s0v = *reinterpret_cast<const f32x4*>(&sSum[buf][0][4 * i16]);
-    const f32x4 s1v = *reinterpret_cast<const f32x4*>(&sSum[buf][1][4 * i16]);
-    const f32x4 s2v = *reinterpret_cast<const f32x4*>(&sSum[buf][2][4 * i16]);
-    const f32x4 s3v = *reinterpret_cast<const f32x4*>(&sSum[buf][3][4 * i16]);
-    const f32x4 r = ((s0v + s1v) + (s2v + s3v)) * invK;
-#pragma unroll
-    for (int u = 0; u < LPW; ++u)
-      *reinterpret_cast<f32x4*>(&sX[buf][(wave * (ROWS / 4) + 4 * u + q) * kGramRS + 4 * i16]) = masked(u) - r;
-  };
-  auto frag = [&](int buf, int grp, float (&F)[16]) {
-    const float* p = &sX[buf][(16 * grp + i16) * kGramRS + 16 * q];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const f32x4 x = *reinterpret_cast<const f32x4*>(p + 4 * k);
-      F[4 * k] = x.x;
-      F[4 * k + 1] = x.y;
-      F[4 * k + 2] = x.z;
-      F[4 * k + 3] = x.w;
-    }
-  };
-  // fp32 MFMA accumulators, folded into acc64 every FEDAGG_GRAM_FOLD stages
-  f32x4v acc[TPW];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  int unfolded = 0;
-  auto fold = [&]() {
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      asm volatile("s_nop 15" : "+v"(acc[j]));  // MFMA -> VALU wait states (see pairgram_split_kernel)
-      acc64[j][0] += double(acc[j].x);
-      acc64[j][1] += double(acc[j].y);
-      acc64[j][2] += double(acc[j].z);
-      acc64[j][3] += double(acc[j].w);
-      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    }
-    unfolded = 0;
-  };
-  auto compute = [&](int buf) {
-    // tiles two at a time, their MFMAs interleaved: two independent
-    // accumulation chains hide the 16x16x4 MFMA's dependent latency (40
-    // cycles against a 32-cycle issue; one chain at a time left the waves
-    // issue-stalled 42 % of their cycles, SQ_WAIT_INST_ANY)
-    float A0[16], B0[16], A1[16], B1[16];
-#pragma unroll
-    for (int j = 0; j < TPW; j += 2) {
-      if (j < nmine) {
-        const int2 ab0 = gram_tile(t0 + j, nb);
-        const bool two = j + 1 < TPW && j + 1 < nmine;
-        const int2 ab1 = two ? gram_tile(t0 + j + 1, nb) : ab0;
-        frag(buf, ab0.x, A0);
-        frag(buf, ab0.y, B0);
-        frag(buf, ab1.x, A1);
-        frag(buf, ab1.y, B1);
-        if (two) {
-#pragma unroll
-          for (int m = 0; m < 16; ++m) {
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[m], B0[m], acc[j], 0, 0, 0);
-            acc[j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[m], B1[m], acc[j + 1], 0, 0, 0);
-          }
-        } else {
-#pragma unroll
-          for (int m = 0; m < 16; ++m) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[m], B0[m], acc[j], 0, 0, 0);
-        }
-      }
-    }
-    if (++unfolded == FEDAGG_GRAM_FOLD) fold();
-  };
-  // stage s computes from buffer s & 1 while stage s + 1 is staged into the
-  // other (sums, barrier, centred rows) and stage s + 2's loads are in
-  // flight: two barriers per stage
-  bool have = fetch();
-  if (have) {
-    stage_sums(0);
-    lds_barrier();
-    stage_centred(0);
-    have = fetch();
-    lds_barrier();
-    for (int buf = 0;; buf ^= 1) {
-      if constexpr (FEDAGG_GRAM_DIAG != 1) compute(buf);
-      if (!have) break;
-      if constexpr (FEDAGG_GRAM_DIAG == 2) {  // same stage count, no loads, sums or barriers
-        have = fetch_skip();
-        continue;
-      }
-      stage_sums(buf ^ 1);
-      lds_barrier();
-      stage_centred(buf ^ 1);
-      have = fetch();
-      lds_barrier();
-    }
-  }
-  if (unfolded) fold();
-  // C/D layout of the 16x16 MFMA: lane l holds row 4 * (l >> 4) + r, column l & 15
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    if (j < nmine) {
-      double* out = partial + (int64_t(g) * NT + t0 + j) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) out[(4 * q + r) * 16 + i16] = acc64[j][r];
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// The same centred Gram on the bf16 matrix cores (FEDAGG_GRAM_SPLIT, default).
+// The centred Gram on the bf16 matrix cores (the shipped kernel; the fp32-MFMA form
+// it replaced, 5.3 ms at config 3, is recorded in NOTES.md §5c).
 //
 // Every centred value is split EXACTLY into three bf16 parts, c = h + m + l
 // (h = bf16(c) rounded to nearest, m = bf16(c - h), l = c - h - m: each
@@ -898,7 +665,7 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 // 1.64 ms of reading the rows once.
 //
 // LDS: the three planes of one stage, [plane][client][64 columns] bf16, rows
-// of FEDAGG_GRAM_ROW_BYTES (160).  gfx950 serves a ds_read_b128 in the lane
+// of kSplitRB (160) bytes.  gfx950 serves a ds_read_b128 in the lane
 // groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
 // {36-43,48-51,60-63}, i.e. (rows 0-3, 12-15 at k-block q) with (rows 4-11 at
 // q + 1): with 160-byte rows those 16 reads hit 16 distinct 16-byte bank
@@ -910,28 +677,8 @@ __global__ __launch_bounds__(kGramBS, kGramBlocksPerCU) void pairgram_kernel(
 // B[k = 8q + j][col i] are both 16 bytes of row (16 g + i) at columns
 // 32 ks + 8q .. + 7.  A wave's tiles are a contiguous run in row-major order,
 // so consecutive tiles share their A group: its fragments are read once per run.
-#ifndef FEDAGG_GRAM_SPLIT
-#define FEDAGG_GRAM_SPLIT 2
-#endif
-#ifndef FEDAGG_GRAM_SPLIT_FOLD
-#define FEDAGG_GRAM_SPLIT_FOLD 4
-#endif
-// diagnostic: per-phase s_memtime stamps of the 8-wave kernel (wrong results)
-#ifndef FEDAGG_GRAM_STAMPS
-#define FEDAGG_GRAM_STAMPS 0
-#endif
-// 1: the 8-wave kernel's 2 x 2 group-block schedule at 8 groups (K 113..128)
-#ifndef FEDAGG_GRAM_BLK8
-#define FEDAGG_GRAM_BLK8 1
-#endif
-// producer waves' stages of loads in flight (FEDAGG_GRAM_SPLIT == 3): 2, 4 or 6
-#ifndef FEDAGG_GRAM_WS_PD
-#define FEDAGG_GRAM_WS_PD 4
-#endif
-#ifndef FEDAGG_GRAM_ROW_BYTES
-#define FEDAGG_GRAM_ROW_BYTES 160
-#endif
-constexpr int kSplitRB = FEDAGG_GRAM_ROW_BYTES;  // bytes per plane row: 64 bf16 + padding
+constexpr int kSplitFold = 4;  // stages summed in fp32 by the MFMAs before one fp64 fold
+constexpr int kSplitRB = 160;  // bytes per plane row: 64 bf16 + padding
 
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
@@ -942,15 +689,6 @@ typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 // two floats -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32)
 [[maybe_unused]] __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
-}
-// FEDAGG_GRAM_STAMPS (diagnostic builds only, tools/gram_variants.py):
-// s_memtime with its lgkmcnt wait in one statement, fenced for the scheduler
-[[maybe_unused]] __device__ __forceinline__ unsigned long long gram_stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
 }
 [[maybe_unused]] __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 [[maybe_unused]] __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -978,203 +716,7 @@ __device__ __forceinline__ void split_frag(const unsigned char* fp, int grp, int
   return x;
 }
 
-// NB = the groups of 16 clients of THIS K (1..8): every wave's tiles, their
-// rows and columns are compile-time constants, so the fragment ping-pong and
-// the A reloads (only where a wave's run of tiles changes row) are static
-template <int NB>
-__global__ __launch_bounds__(kGramBS, 2) void pairgram_split_kernel(const float* const* __restrict__ src, int K,
-                                                                    const int64_t* __restrict__ chunks,
-                                                                    int64_t n_chunks, int G,
-                                                                    double* __restrict__ partial) {
-  constexpr int ROWS = NB * 16;
-  constexpr int NT = NB * (NB + 1) / 2;
-  constexpr int TPW = NB + 1;  // tiles per wave, at most (two rows)
-  constexpr int LPW = ROWS / 16;
-  constexpr int PLANE = ROWS * kSplitRB;
-  __shared__ __attribute__((aligned(16))) unsigned char sP[3 * PLANE];
-  __shared__ float sSum[2][4][kStage];
-  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int i16 = lane & 15, q = lane >> 4;
-  const float* rowp[LPW];
-  bool rlive[LPW];
-#pragma unroll
-  for (int u = 0; u < LPW; ++u) {
-    const int cl = wave * (ROWS / 4) + 4 * u + q;
-    rlive[u] = cl < K;
-    rowp[u] = src[cl < K ? cl : 0];
-  }
-  double acc64[TPW][4];
-  f32x4v acc[TPW];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc64[j][r] = 0.0;
-  }
-  const float invK = 1.0f / float(K);
-  int64_t c = g;
-  int s0 = 0;
-  f32x4 v[LPW];
-  auto fetch = [&]() {
-    if (c >= n_chunks) return false;
-    const int len = int(chunks[2 * c + 1]);
-    const int64_t col0 = chunks[2 * c] + s0;
-    const int w = len - s0 < kStage ? len - s0 : kStage;
-    const int c4 = 4 * i16;
-    if (w == kStage) {
-#pragma unroll
-      for (int u = 0; u < LPW; ++u) v[u] = ld4<true>(rowp[u] + col0 + c4);
-    } else {
-#pragma unroll
-      for (int u = 0; u < LPW; ++u) {
-        const float* p = rowp[u] + col0;
-        const bool ok = rlive[u];
-        v[u].x = ok && c4 < w ? gptr(p)[c4] : 0.f;
-        v[u].y = ok && c4 + 1 < w ? gptr(p)[c4 + 1] : 0.f;
-        v[u].z = ok && c4 + 2 < w ? gptr(p)[c4 + 2] : 0.f;
-        v[u].w = ok && c4 + 3 < w ? gptr(p)[c4 + 3] : 0.f;
-      }
-    }
-    s0 += kStage;
-    if (s0 >= len) {
-      s0 = 0;
-      c += G;
-    }
-    return true;
-  };
-  auto fetch_skip = [&]() {
-    if (c >= n_chunks) return false;
-    const int len = int(chunks[2 * c + 1]);
-    s0 += kStage;
-    if (s0 >= len) {
-      s0 = 0;
-      c += G;
-    }
-    return true;
-  };
-  auto masked = [&](int u) {
-    const uint32_t m = rlive[u] ? 0xffffffffu : 0u;
-    return f32x4{__uint_as_float(__float_as_uint(v[u].x) & m), __uint_as_float(__float_as_uint(v[u].y) & m),
-                 __uint_as_float(__float_as_uint(v[u].z) & m), __uint_as_float(__float_as_uint(v[u].w) & m)};
-  };
-  auto stage_sums = [&](int sb) {
-    f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < LPW; ++u) cs += masked(u);
-#pragma unroll
-    for (int m = 16; m <= 32; m <<= 1) {
-      cs.x += __shfl_xor(cs.x, m, 64);
-      cs.y += __shfl_xor(cs.y, m, 64);
-      cs.z += __shfl_xor(cs.z, m, 64);
-      cs.w += __shfl_xor(cs.w, m, 64);
-    }
-    if (q == 0) *reinterpret_cast<f32x4*>(&sSum[sb][wave][4 * i16]) = cs;
-  };
-  // the rows minus the column means, split into the three bf16 planes
-  auto stage_split = [&](int sb) {
-    const f32x4 s0v = *reinterpret_cast<const f32x4*>(&sSum[sb][0][4 * i16]);
-    const f32x4 s1v = *reinterpret_cast<const f32x4*>(&sSum[sb][1][4 * i16]);
-    const f32x4 s2v = *reinterpret_cast<const f32x4*>(&sSum[sb][2][4 * i16]);
-    const f32x4 s3v = *reinterpret_cast<const f32x4*>(&sSum[sb][3][4 * i16]);
-    const f32x4 r = ((s0v + s1v) + (s2v + s3v)) * invK;
-#pragma unroll
-    for (int u = 0; u < LPW; ++u) {
-      const f32x4 cc = masked(u) - r;
-      const uint32_t h01 = pk_bf16(cc.x, cc.y), h23 = pk_bf16(cc.z, cc.w);
-      const float r0 = cc.x - bf16_lo(h01), r1 = cc.y - bf16_hi(h01);
-      const float r2 = cc.z - bf16_lo(h23), r3 = cc.w - bf16_hi(h23);
-      const uint32_t m01 = pk_bf16(r0, r1), m23 = pk_bf16(r2, r3);
-      const uint32_t l01 = pk_bf16(r0 - bf16_lo(m01), r1 - bf16_hi(m01));
-      const uint32_t l23 = pk_bf16(r2 - bf16_lo(m23), r3 - bf16_hi(m23));
-      unsigned char* d = sP + (wave * (ROWS / 4) + 4 * u + q) * kSplitRB + 8 * i16;
-      *reinterpret_cast<u32x2v*>(d) = u32x2v{h01, h23};
-      *reinterpret_cast<u32x2v*>(d + PLANE) = u32x2v{m01, m23};
-      *reinterpret_cast<u32x2v*>(d + 2 * PLANE) = u32x2v{l01, l23};
-    }
-  };
-  int unfolded = 0;
-  auto fold = [&]() {
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      // 16 wait states between the last MFMA writing acc[j] and this VALU
-      // read: the compiler left none when the fold follows the MFMA chain
-      // directly (NB = 1: wrong sums on the box)
-      asm volatile("s_nop 15" : "+v"(acc[j]));
-      acc64[j][0] += double(acc[j].x);
-      acc64[j][1] += double(acc[j].y);
-      acc64[j][2] += double(acc[j].z);
-      acc64[j][3] += double(acc[j].w);
-      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    }
-    unfolded = 0;
-  };
-  // this wave's rows of tiles: r1 = wave (n1 tiles), r2 = NB - 1 - wave (n2)
-  const int r1 = wave, r2 = NB - 1 - wave;
-  const int n1 = wave < (NB + 1) / 2 ? NB - wave : 0;
-  const int n2 = r2 > r1 ? wave + 1 : 0;
-  const int nmine = n1 + n2;
-  const unsigned char* fp = sP + i16 * kSplitRB + 16 * q;
-  auto compute = [&]() {
-    if (nmine > 0) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8v A1[3], A2[3], B[2][3];
-        split_frag<PLANE>(fp, r1, ks, A1);
-        split_frag<PLANE>(fp, r1, ks, B[0]);  // tile 0 = (r1, r1)
-        if (n2) split_frag<PLANE>(fp, r2, ks, A2);
-#pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-          if (j < nmine) {
-            if (j + 1 < nmine)  // tile j + 1's column group
-              split_frag<PLANE>(fp, j + 1 < n1 ? r1 + j + 1 : r2 + (j + 1 - n1), ks, B[(j + 1) & 1]);
-            acc[j] = j < n1 ? split_mfma6(A1, B[j & 1], acc[j]) : split_mfma6(A2, B[j & 1], acc[j]);
-          }
-        }
-      }
-    }
-    if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
-  };
-  // one plane buffer: compute(s), then stage s + 1's sums (its loads had the
-  // whole compute to land), barrier (every wave done reading the planes),
-  // split-write stage s + 1, issue stage s + 2's loads, barrier
-  bool have = fetch();
-  if (have) {
-    stage_sums(0);
-    lds_barrier();
-    stage_split(0);
-    have = fetch();
-    lds_barrier();
-    for (int sb = 1;; sb ^= 1) {
-      if constexpr (FEDAGG_GRAM_DIAG != 1) compute();
-      if (!have) break;
-      if constexpr (FEDAGG_GRAM_DIAG == 2) {  // same stage count, no loads, sums or barriers
-        have = fetch_skip();
-        continue;
-      }
-      stage_sums(sb);
-      lds_barrier();
-      stage_split(sb);
-      have = fetch();
-      lds_barrier();
-    }
-  }
-  if (unfolded) fold();
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    if (j < nmine) {
-      // row-major index of tile (a, b) in the triangle: the workspace layout
-      const int a = j < n1 ? r1 : r2, b = j < n1 ? r1 + j : r2 + (j - n1);
-      const int tt = a * NB - a * (a - 1) / 2 + (b - a);
-      double* out = partial + (int64_t(g) * NT + tt) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) out[(4 * q + r) * 16 + i16] = acc64[j][r];
-    }
-  }
-}
-
-#if FEDAGG_GRAM_SPLIT >= 2  // the 8-wave kernel (default) and the experimental producer / consumer one
-// FEDAGG_GRAM_SPLIT == 2: the same split Gram with 8 waves per block and ONE
+// pairgram_split8_kernel: the split Gram with 8 waves per block and ONE
 // block per CU, so the planes can be double-buffered (2 x 55 KB) and a stage
 // needs one barrier, and each lane's raw rows are prefetched two stages
 // ahead (two register sets; 16 rows per wave).  Iteration k: split stage
@@ -1316,16 +858,6 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     }
     return true;
   };
-  auto fetch_skip = [&]() __attribute__((always_inline)) {
-    if (c >= n_chunks) return false;
-    const int len = int(chunks[2 * c + 1]);
-    s0 += kStage;
-    if (s0 >= len) {
-      s0 = 0;
-      c += G;
-    }
-    return true;
-  };
   auto masked = [&](const f32x4& x, int u) __attribute__((always_inline)) {
     const uint32_t m = rlive[u] ? 0xffffffffu : 0u;
     return f32x4{__uint_as_float(__float_as_uint(x.x) & m), __uint_as_float(__float_as_uint(x.y) & m),
@@ -1373,7 +905,11 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
   auto fold = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-      asm volatile("s_nop 15" : "+v"(acc[j]));  // MFMA -> VALU wait states (see pairgram_split_kernel)
+      // 16 wait states between the last MFMA writing acc[j] and this VALU
+      // read: the compiler once left only 3 where the fold follows the MFMA
+      // chain directly (NB = 1: wrong sums on the box); tools/mfma_hazards.py
+      // checks every shipped build
+      asm volatile("s_nop 15" : "+v"(acc[j]));
       acc64[j][0] += double(acc[j].x);
       acc64[j][1] += double(acc[j].y);
       acc64[j][2] += double(acc[j].z);
@@ -1384,11 +920,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
   };
   const int fo = i16 * kSplitRB + 16 * q;
   auto compute = [&](const unsigned char* P) __attribute__((always_inline)) {
-    if constexpr (FEDAGG_GRAM_DIAG == 1) {  // staging only: one LDS read keeps the planes live
-      acc[0].x += *reinterpret_cast<const float*>(P + fo);
-      return;
-    }
-    if constexpr (NB == 8 && FEDAGG_GRAM_BLK8) {
+    if constexpr (NB == 8) {
       const unsigned char* fp = P + fo;
       switch (wave) {
         case 0: gblocks8<PLANE, 0>(fp, acc); break;
@@ -1400,7 +932,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
         case 6: gblocks8<PLANE, 6>(fp, acc); break;
         default: gblocks8<PLANE, 7>(fp, acc); break;
       }
-      if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
+      if (++unfolded == kSplitFold) fold();
       return;
     }
     if (nmine > 0) {
@@ -1421,7 +953,7 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
         }
       }
     }
-    if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
+    if (++unfolded == kSplitFold) fold();
   };
   // prologue: stages 0 and 1 loaded, stage 0 split, stage 1's sums published
   bool h0 = fetch(v[0]);
@@ -1434,34 +966,17 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
     if (h1) stage_sums(v[1], 1);
     lds_barrier();
     // iteration k (two at a time, so the register sets are static)
-    [[maybe_unused]] int it = 0;
-    [[maybe_unused]] double phase_sum[4] = {0.0, 0.0, 0.0, 0.0};
     auto iter = [&](auto cur_tag, bool& hn, bool& hnn) __attribute__((always_inline)) {
       constexpr int C = decltype(cur_tag)::value;  // k % 2
       // hn: stage k + 1 exists (in v[C ^ 1], sums in sSum[C ^ 1]); hnn: stage k + 2 (in v[C])
       bool hnnn = false;
-      unsigned long long ts[5] = {0, 0, 0, 0, 0};
-      if constexpr (FEDAGG_GRAM_STAMPS) ts[0] = gram_stamp();
-      if (hn && FEDAGG_GRAM_DIAG != 2) {
+      if (hn) {
         stage_split(v[C ^ 1], C ^ 1, sP[C ^ 1]);
         hnnn = hnn && fetch(v[C ^ 1]);  // stage k + 3
       }
-      if (FEDAGG_GRAM_DIAG == 2) hnnn = hnn && fetch_skip();  // compute only: same stage count
-      if constexpr (FEDAGG_GRAM_STAMPS) ts[1] = gram_stamp();
       compute(sP[C]);
-      if constexpr (FEDAGG_GRAM_STAMPS) ts[2] = gram_stamp();
-      if (hnn && FEDAGG_GRAM_DIAG != 2) stage_sums(v[C], C);
-      if constexpr (FEDAGG_GRAM_STAMPS) ts[3] = gram_stamp();
+      if (hnn) stage_sums(v[C], C);
       lds_barrier();
-      if constexpr (FEDAGG_GRAM_STAMPS) {
-        ts[4] = gram_stamp();
-        // iterations 64..191: the four phase lengths, summed (written at the end)
-        if (it >= 64 && it < 192) {
-#pragma unroll
-          for (int ph = 0; ph < 4; ++ph) phase_sum[ph] += double(ts[ph + 1] - ts[ph]);
-        }
-        ++it;
-      }
       const bool more = hn;
       hn = hnn;
       hnn = hnnn;
@@ -1472,24 +987,14 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
       if (!iter(std::integral_constant<int, 0>{}, hn, hnn)) break;
       if (!iter(std::integral_constant<int, 1>{}, hn, hnn)) break;
     }
-    if constexpr (FEDAGG_GRAM_STAMPS) {
-      // blocks 0..7, every wave: the four phase lengths summed over
-      // iterations 64..191, into the workspace's unused tail (G1 = 256 of the
-      // G it was sized for)
-      if (g < 8 && lane == 0) {
-        double* st = partial + int64_t(256) * NT * 256 + (g * 8 + wave) * 4;
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph) st[ph] = phase_sum[ph];
-      }
-    }
   }
   if (unfolded) fold();
-  const int nout = NB == 8 && FEDAGG_GRAM_BLK8 ? (wave < 4 ? 4 : 5) : nmine;
+  const int nout = NB == 8 ? (wave < 4 ? 4 : 5) : nmine;
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     if (j < nout) {
       int a = j < n1 ? r1 : r2, b = j < n1 ? b1 + j : b2 + (j - n1);
-      if constexpr (NB == 8 && FEDAGG_GRAM_BLK8) {
+      if constexpr (NB == 8) {
         a = kBlk8Tile[wave][j][0];
         b = kBlk8Tile[wave][j][1];
       }
@@ -1501,282 +1006,6 @@ __global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split8_kernel(const flo
   }
 }
 
-#if FEDAGG_GRAM_SPLIT == 3  // the producer / consumer variant
-// Consumer wave W's tiles, unrolled at compile time (no branches between
-// tiles): tile J of its row pair, B fragments ping-ponged by J, tile J + 1's
-// read issued before tile J's six MFMAs.  Rows W (n1 tiles) and NB - 1 - W
-// (n2 tiles), as pairgram_split_kernel's run-time schedule.
-template <int NB, int W>
-struct WsRows {
-  static constexpr int n1 = W < (NB + 1) / 2 ? NB - W : 0;
-  static constexpr int n2 = (NB - 1 - W > W) && n1 ? W + 1 : 0;
-  static constexpr int nm = n1 + n2;
-  static constexpr int bgrp(int j) { return j < n1 ? W + j : (NB - 1 - W) + (j - n1); }
-};
-
-template <int NB, int PLANE, int W, int KS, int BG, int TPW>
-__device__ __forceinline__ void ws_tiles(const unsigned char* fp, f32x4v (&acc)[TPW], const bf16x8v (&A1)[3],
-                                         const bf16x8v (&A2)[3], bf16x8v (&B)[2][3]) {
-  // column group BG: tile (W, BG), and (NB - 1 - W, BG) when BG is in that
-  // row too -- both from ONE read of BG's fragments
-  using R = WsRows<NB, W>;
-  constexpr int r2 = NB - 1 - W;
-  if constexpr (BG < NB && R::n1 > 0) {
-    if constexpr (BG + 1 < NB) split_frag<PLANE>(fp, BG + 1, KS, B[(BG + 1) & 1]);
-    acc[BG - W] = split_mfma6(A1, B[BG & 1], acc[BG - W]);
-    if constexpr (R::n2 > 0 && BG >= r2) acc[R::n1 + (BG - r2)] = split_mfma6(A2, B[BG & 1], acc[R::n1 + (BG - r2)]);
-    ws_tiles<NB, PLANE, W, KS, BG + 1, TPW>(fp, acc, A1, A2, B);
-  }
-}
-
-template <int NB, int PLANE, int W, int TPW>
-__device__ __forceinline__ void ws_compute(const unsigned char* fp, f32x4v (&acc)[TPW]) {
-  using R = WsRows<NB, W>;
-  if constexpr (R::nm > 0) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8v A1[3], A2[3], B[2][3];
-      split_frag<PLANE>(fp, W, ks, A1);
-      split_frag<PLANE>(fp, W, ks, B[W & 1]);  // the first column group is the row's own
-      if constexpr (R::n2 > 0) split_frag<PLANE>(fp, NB - 1 - W, ks, A2);
-      if (ks == 0)
-        ws_tiles<NB, PLANE, W, 0, W, TPW>(fp, acc, A1, A2, B);
-      else
-        ws_tiles<NB, PLANE, W, 1, W, TPW>(fp, acc, A1, A2, B);
-    }
-  }
-}
-
-// FEDAGG_GRAM_SPLIT == 3: producer / consumer waves.  One block of 8 waves
-// per CU; waves 0-3 (one per SIMD) only run MFMAs, waves 4-7 (one per SIMD)
-// only load, centre and split, so every SIMD has its matrix work and its
-// VALU work in two different waves that the scheduler interleaves (in the
-// other variants both phases sit in the same waves between barriers and do
-// not overlap).  A producer owns 16 of a stage's 64 columns for ALL rows, so
-// its column sums stay inside the wave (no exchange, no extra barrier), and
-// keeps two stages of loads in flight in registers.  The planes are double-
-// buffered: at barrier k the producers have written stage k + 1 and the
-// consumers have finished stage k, so one barrier per stage.  Consumers use
-// the row-pair tile schedule of pairgram_split_kernel.
-template <int NB>
-__global__ __launch_bounds__(kSplit8BS, 1) void pairgram_split_ws_kernel(const float* const* __restrict__ src, int K,
-                                                                       const int64_t* __restrict__ chunks,
-                                                                       int64_t n_chunks, int G,
-                                                                       double* __restrict__ partial) {
-  constexpr int ROWS = NB * 16;
-  constexpr int NT = NB * (NB + 1) / 2;
-  constexpr int TPW = NB + 1;
-  constexpr int PLANE = ROWS * kSplitRB;
-  __shared__ __attribute__((aligned(16))) unsigned char sP[2][3 * PLANE];
-  const int g = blockIdx.x, t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  // this block's stage count (every wave walks the chunk table: wave-uniform)
-  int S = 0;
-  for (int64_t cc = g; cc < n_chunks; cc += G) S += int((chunks[2 * cc + 1] + kStage - 1) / kStage);
-  constexpr int PD = FEDAGG_GRAM_WS_PD;  // stages of loads in flight per producer
-  const int Spad = (S + PD - 1) / PD * PD;  // barriers: one per (padded) stage
-  if (wave >= 4) {
-    // ---- producer: columns 16 pw .. 16 pw + 15 of every stage, all rows ----
-    // lane = (rsub = l & 15, cq = l >> 4): a column quad's 16 row groups sit
-    // in one 16-lane DPP row, so the column sums need no cross-row shuffles
-    const int pw = wave - 4, cq = lane >> 4, rsub = lane & 15;
-    const int cofs = 16 * pw + 4 * cq;  // this lane's 4 columns in the stage
-    const float* rowp[NB];
-    bool rlive[NB];
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int cl = rsub + 16 * u;
-      rlive[u] = cl < K;
-      rowp[u] = src[cl < K ? cl : 0];
-    }
-    const float invK = 1.0f / float(K);
-    int64_t c = g;
-    int s0 = 0;
-    f32x4 v[PD][NB];
-    // One code path for full and ragged stages, so every stage issues the
-    // same NB loads and the compiler's load counting stays exact across the
-    // register sets (a ragged branch made it wait for every load in flight,
-    // s_waitcnt vmcnt(0), at each stage).  Lanes past the stage's width w
-    // load the stage's first quad (valid memory) and are zeroed when used;
-    // a quad that starts inside the stage stays inside the 16-byte aligned,
-    // 256-byte padded row.
-    auto fetch = [&](f32x4 (&vv)[NB], int& wout) __attribute__((always_inline)) {
-      // past this block's last stage: the same loads from column 0 (valid
-      // memory), width 0 -- the load count must not depend on the data
-      const bool live = c < n_chunks;
-      const int64_t cc = live ? c : 0;
-      const int len = live ? int(chunks[2 * cc + 1]) : 0;
-      const int64_t col0 = live ? chunks[2 * cc] + s0 : 0;
-      const int w = live ? (len - s0 < kStage ? len - s0 : kStage) : 0;
-      const int off = cofs < w ? cofs : 0;
-#pragma unroll
-      for (int u = 0; u < NB; ++u) vv[u] = ld4<true>(rowp[u] + col0 + off);
-      wout = w;
-      if (live) {
-        s0 += kStage;
-        if (s0 >= len) {
-          s0 = 0;
-          c += G;
-        }
-      }
-    };
-    // rows past K and columns past the stage's width read as 0
-    auto masked = [&](const f32x4& x, int u, int w) __attribute__((always_inline)) {
-      const uint32_t m = rlive[u] ? 0xffffffffu : 0u;
-      return f32x4{__uint_as_float(__float_as_uint(x.x) & (cofs < w ? m : 0u)),
-                   __uint_as_float(__float_as_uint(x.y) & (cofs + 1 < w ? m : 0u)),
-                   __uint_as_float(__float_as_uint(x.z) & (cofs + 2 < w ? m : 0u)),
-                   __uint_as_float(__float_as_uint(x.w) & (cofs + 3 < w ? m : 0u))};
-    };
-    // column means of this lane's 4 columns (sum over the wave's 16 row
-    // groups: lanes with the same cq, lane bits 2..5), centre, split, write
-    // sum over the 16 lanes of a DPP row: xor 1, xor 2 (quad_perm), then the
-    // half-row and row mirrors
-    auto row_sum = [](float x) __attribute__((always_inline)) {
-      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xf, 0xf, false));
-      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xf, 0xf, false));
-      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
-      x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false));
-      return x;
-    };
-    const bool all_rows = K >= ROWS;
-    auto split_stage = [&](const f32x4 (&vv)[NB], int w, unsigned char* P) __attribute__((always_inline)) {
-      // a full stage of live rows (the common case) needs no masking
-      const bool plain = all_rows && w == kStage;
-      f32x4 x[NB];
-#pragma unroll
-      for (int u = 0; u < NB; ++u) x[u] = plain ? vv[u] : masked(vv[u], u, w);
-      f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < NB; ++u) cs += x[u];
-      cs = f32x4{row_sum(cs.x), row_sum(cs.y), row_sum(cs.z), row_sum(cs.w)};
-      const f32x4 r = cs * invK;
-#pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        const f32x4 cc = x[u] - r;
-        const uint32_t h01 = pk_bf16(cc.x, cc.y), h23 = pk_bf16(cc.z, cc.w);
-        const float e0 = cc.x - bf16_lo(h01), e1 = cc.y - bf16_hi(h01);
-        const float e2 = cc.z - bf16_lo(h23), e3 = cc.w - bf16_hi(h23);
-        const uint32_t m01 = pk_bf16(e0, e1), m23 = pk_bf16(e2, e3);
-        const uint32_t l01 = pk_bf16(e0 - bf16_lo(m01), e1 - bf16_hi(m01));
-        const uint32_t l23 = pk_bf16(e2 - bf16_lo(m23), e3 - bf16_hi(m23));
-        unsigned char* d = P + (rsub + 16 * u) * kSplitRB + 2 * cofs;
-        *reinterpret_cast<u32x2v*>(d) = u32x2v{h01, h23};
-        *reinterpret_cast<u32x2v*>(d + PLANE) = u32x2v{m01, m23};
-        *reinterpret_cast<u32x2v*>(d + 2 * PLANE) = u32x2v{l01, l23};
-      }
-    };
-    // prologue: stages 0 .. PD - 1 in flight (stage s in register set s % PD),
-    // stage 0 split into P[0], stage PD issued into the freed set
-    int wset[PD];  // each register set's stage width
-    // (no loop here: a loop over the sets, even unrolled, left v[][] in
-    // scratch memory)
-    fetch(v[0], wset[0]);
-    fetch(v[1], wset[1]);
-    if constexpr (PD > 2) {
-      fetch(v[2], wset[2]);
-      fetch(v[3], wset[3]);
-    }
-    if constexpr (PD > 4) {
-      fetch(v[4], wset[4]);
-      fetch(v[5], wset[5]);
-    }
-    if (S > 0) split_stage(v[0], wset[0], sP[0]);
-    fetch(v[0], wset[0]);
-    lds_barrier();
-    // iteration k: split stage k + 1 (set (k + 1) % PD) into P[(k + 1) & 1],
-    // issue stage k + 1 + PD into that set, barrier.  Every iteration issues
-    // its loads (past the end: dummies), and the trip count is a multiple of
-    // PD, so the compiler's count of loads in flight is exact.
-    f32x4 diag_acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto iter = [&](auto set_tag, int k) __attribute__((always_inline)) {
-      constexpr int SL = decltype(set_tag)::value;
-      if constexpr (FEDAGG_GRAM_DIAG == 3) {  // loads only: the data feeds one sum
-#pragma unroll
-        for (int u = 0; u < NB; ++u) diag_acc += v[SL][u];
-      } else if (k + 1 < S && FEDAGG_GRAM_DIAG != 2) split_stage(v[SL], wset[SL], sP[(k + 1) & 1]);
-      fetch(v[SL], wset[SL]);
-      lds_barrier();
-    };
-    for (int k = 0; k < Spad; k += PD) {
-      iter(std::integral_constant<int, 1 % PD>{}, k);
-      if constexpr (PD > 1) iter(std::integral_constant<int, 2 % PD>{}, k + 1);
-      if constexpr (PD > 2) iter(std::integral_constant<int, 3 % PD>{}, k + 2);
-      if constexpr (PD > 3) iter(std::integral_constant<int, 4 % PD>{}, k + 3);
-      if constexpr (PD > 4) iter(std::integral_constant<int, 5 % PD>{}, k + 4);
-      if constexpr (PD > 5) iter(std::integral_constant<int, 6 % PD>{}, k + 5);
-    }
-    if constexpr (FEDAGG_GRAM_DIAG == 3)
-      if (diag_acc.x == 1.2345f && n_chunks < 0) partial[0] = diag_acc.y;  // never: keeps the loads
-    return;
-  }
-  // ---- consumer: the MFMAs of its row pair of tiles, one static code path
-  // per wave (the producers' registers are not live here, so the four paths
-  // do not crowd each other) ----
-  const int i16 = lane & 15, q = lane >> 4;
-  const unsigned char* fp0 = sP[0] + i16 * kSplitRB + 16 * q;
-  const unsigned char* fp1 = sP[1] + i16 * kSplitRB + 16 * q;
-  auto consume = [&](auto wtag) __attribute__((always_inline)) {
-    constexpr int W = decltype(wtag)::value;
-    using R = WsRows<NB, W>;
-    double acc64[TPW][4];
-    f32x4v acc[TPW];
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc64[j][r] = 0.0;
-    }
-    int unfolded = 0;
-    auto fold = [&]() __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < R::nm; ++j) {
-        asm volatile("s_nop 15" : "+v"(acc[j]));  // MFMA -> VALU wait states (see pairgram_split_kernel)
-        acc64[j][0] += double(acc[j].x);
-        acc64[j][1] += double(acc[j].y);
-        acc64[j][2] += double(acc[j].z);
-        acc64[j][3] += double(acc[j].w);
-        acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      }
-      unfolded = 0;
-    };
-    auto step = [&](const unsigned char* fp, bool live) __attribute__((always_inline)) {
-      if (live) {
-        if constexpr (FEDAGG_GRAM_DIAG == 1)  // staging only: one LDS read keeps the planes live
-          acc[0].x += *reinterpret_cast<const float*>(fp);
-        else
-          ws_compute<NB, PLANE, W, TPW>(fp, acc);
-        if (++unfolded == FEDAGG_GRAM_SPLIT_FOLD) fold();
-      }
-      lds_barrier();
-    };
-    lds_barrier();  // the prologue's barrier: stage 0 in P[0]
-    for (int k = 0; k < Spad; k += 2) {  // Spad is even when PD is
-      step(fp0, k < S);
-      step(fp1, k + 1 < S);
-    }
-    if (unfolded) fold();
-#pragma unroll
-    for (int j = 0; j < R::nm; ++j) {
-      const int a = j < R::n1 ? W : NB - 1 - W, b = R::bgrp(j);
-      const int tt = a * NB - a * (a - 1) / 2 + (b - a);
-      double* out = partial + (int64_t(g) * NT + tt) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) out[(4 * q + r) * 16 + i16] = acc64[j][r];
-    }
-  };
-  if (wave == 0)
-    consume(std::integral_constant<int, 0>{});
-  else if (wave == 1)
-    consume(std::integral_constant<int, 1>{});
-  else if (wave == 2)
-    consume(std::integral_constant<int, 2>{});
-  else
-    consume(std::integral_constant<int, 3>{});
-}
-
-#endif  // FEDAGG_GRAM_SPLIT == 3
-#endif  // FEDAGG_GRAM_SPLIT >= 2
 
 // M (K x K, fp64, both triangles) = the tiles' partials summed over the chunk
 // groups in four fixed-order quarters (as tri_finish_kernel)
@@ -1892,7 +1121,7 @@ __global__ __launch_bounds__(kBS) void clip_diff_kernel(const float* const* __re
   }
 }
 
-constexpr int kClipClients = FEDAGG_CLIP_CLIENTS;  // clients in flight per wave in clip_diff_kernel
+constexpr int kClipClients = 2;  // clients in flight per wave in clip_diff_kernel
 
 int grid_groups(int per_group_blocks, int64_t n_chunks, int64_t work_len, int64_t per_group_work) {
   int64_t G = (4096 + per_group_blocks - 1) / per_group_blocks;
@@ -2009,25 +1238,6 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     return rset(FEDAGG_EINVAL, "fedagg_pairgram2_f32: workspace too small (fedagg_robust_work_len)");
   int G = grid_groups(4096 / (256 * kGramBlocksPerCU), n_chunks, work_len - mat, per);
   double* M = d_work + int64_t(G) * per;
-  // one kernel per build (FEDAGG_GRAM_SPLIT): only the selected one is instantiated
-#if FEDAGG_GRAM_SPLIT == 3
-  {
-    auto kern = pairgram_split_ws_kernel<8>;
-    switch (gram_groups(K)) {
-      case 1: kern = pairgram_split_ws_kernel<1>; break;
-      case 2: kern = pairgram_split_ws_kernel<2>; break;
-      case 3: kern = pairgram_split_ws_kernel<3>; break;
-      case 4: kern = pairgram_split_ws_kernel<4>; break;
-      case 5: kern = pairgram_split_ws_kernel<5>; break;
-      case 6: kern = pairgram_split_ws_kernel<6>; break;
-      case 7: kern = pairgram_split_ws_kernel<7>; break;
-      default: break;
-    }
-    const int G1 = G < 256 ? G : 256;  // one block per CU
-    hipLaunchKernelGGL(kern, dim3(unsigned(G1)), dim3(kSplit8BS), 0, st, d_src, K, d_chunks, n_chunks, G1, d_work);
-    G = G1;
-  }
-#elif FEDAGG_GRAM_SPLIT == 2
   {
     auto kern = pairgram_split8_kernel<8>;
     switch (gram_groups(K)) {
@@ -2044,29 +1254,6 @@ int fedagg_pairgram2_f32(const float* const* d_src, int32_t K, const int64_t* d_
     hipLaunchKernelGGL(kern, dim3(unsigned(G1)), dim3(kSplit8BS), 0, st, d_src, K, d_chunks, n_chunks, G1, d_work);
     G = G1;
   }
-#elif FEDAGG_GRAM_SPLIT == 1
-  {
-    auto kern = pairgram_split_kernel<8>;
-    switch (gram_groups(K)) {
-      case 1: kern = pairgram_split_kernel<1>; break;
-      case 2: kern = pairgram_split_kernel<2>; break;
-      case 3: kern = pairgram_split_kernel<3>; break;
-      case 4: kern = pairgram_split_kernel<4>; break;
-      case 5: kern = pairgram_split_kernel<5>; break;
-      case 6: kern = pairgram_split_kernel<6>; break;
-      case 7: kern = pairgram_split_kernel<7>; break;
-      default: break;
-    }
-    hipLaunchKernelGGL(kern, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G, d_work);
-  }
-#else
-  if (K <= 64)
-    hipLaunchKernelGGL(pairgram_kernel<4>, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G,
-                       d_work);
-  else
-    hipLaunchKernelGGL(pairgram_kernel<8>, dim3(unsigned(G)), dim3(kGramBS), 0, st, d_src, K, d_chunks, n_chunks, G,
-                       d_work);
-#endif
   hipLaunchKernelGGL(gram_sum_kernel, dim3(unsigned((per + 63) / 64)), dim3(256), 0, st, d_work, G, K, M);
   hipLaunchKernelGGL(gram_dist_kernel, dim3(unsigned((mat + 255) / 256)), dim3(256), 0, st, M, K, d_out);
   return rcheck("fedagg_pairgram2_f32");

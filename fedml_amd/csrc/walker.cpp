@@ -451,6 +451,112 @@ PyObject* host_round(PyObject*, PyObject* args) {
   }
 }
 
+// device_round(dicts: list, keys: list, weights: list of float, fn: int,
+//              stream_of: callable) -> None | (rc, outs)
+//   One small round of device tensors through libfedagg's
+//   fedagg_device_round_f32 (fn is its address): every key of every client a
+//   contiguous, 16-byte aligned tensor of fp32 or int64 on ONE CUDA device,
+//   same shapes across clients, at most 16 keys and 128 client tensors.
+//   outs[t] is a new fp32 tensor on that device shaped like client 0's key t
+//   (the caching allocator, on the device's current stream), written by the
+//   launch on stream_of(device_index) (torch's current raw stream there).
+//   None for anything else (the caller's general path then runs and raises
+//   the reference's errors).  Asynchronous, like every device path.
+using DeviceRoundFn = HostRoundFn;
+constexpr Py_ssize_t kDevRoundMaxKeys = 16, kDevRoundMaxPtrs = 128;
+
+PyObject* device_round(PyObject*, PyObject* args) {
+  PyObject* dicts;
+  PyObject* keys;
+  PyObject* weights;
+  PyObject* stream_of;
+  unsigned long long fn_addr = 0;
+  if (!PyArg_ParseTuple(args, "O!O!O!KO", &PyList_Type, &dicts, &PyList_Type, &keys, &PyList_Type, &weights,
+                        &fn_addr, &stream_of))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(dicts), T = PyList_GET_SIZE(keys);
+  if (K < 1 || T < 1 || T > kDevRoundMaxKeys || T * K > kDevRoundMaxPtrs || PyList_GET_SIZE(weights) != K ||
+      !fn_addr)
+    Py_RETURN_NONE;
+  try {
+    for (Py_ssize_t i = 0; i < K; ++i)
+      if (!plain_lookup(PyList_GET_ITEM(dicts, i))) Py_RETURN_NONE;
+    float w[kDevRoundMaxPtrs];
+    for (Py_ssize_t i = 0; i < K; ++i) {
+      const double v = PyFloat_AsDouble(PyList_GET_ITEM(weights, i));  // a Python float: n_i / sum n
+      if (v == -1.0 && PyErr_Occurred()) {
+        PyErr_Clear();
+        Py_RETURN_NONE;
+      }
+      w[i] = static_cast<float>(v);  // RNE, as torch rounds the scalar of p * w
+    }
+    const void* src[kDevRoundMaxPtrs];
+    int32_t codes[kDevRoundMaxKeys];
+    int64_t numels[kDevRoundMaxKeys];
+    const at::Tensor* first[kDevRoundMaxKeys];
+    int dev = -1;
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      const at::Tensor* x0 = nullptr;
+      for (Py_ssize_t i = 0; i < K; ++i) {
+        PyObject* v = PyDict_GetItemWithError(PyList_GET_ITEM(dicts, i), PyList_GET_ITEM(keys, t));
+        if (!v) {
+          if (PyErr_Occurred()) return nullptr;
+          Py_RETURN_NONE;
+        }
+        if (Py_TYPE(v) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) Py_RETURN_NONE;
+        const at::Tensor& x = THPVariable_Unpack(v);
+        if (!x.defined() || x.layout() != c10::kStrided || x.device().type() != c10::DeviceType::CUDA ||
+            !x.is_contiguous())
+          Py_RETURN_NONE;
+        if (i == 0) {
+          x0 = &x;
+          const auto st = x.scalar_type();
+          if (st != c10::ScalarType::Float && st != c10::ScalarType::Long) Py_RETURN_NONE;
+          if (t == 0) dev = x.get_device();
+          if (x.get_device() != dev) Py_RETURN_NONE;
+          codes[t] = st == c10::ScalarType::Float ? 0 : 4;
+          numels[t] = x.numel();
+          first[t] = x0;
+        } else if (x.scalar_type() != x0->scalar_type() || x.sizes() != x0->sizes() || x.get_device() != dev) {
+          Py_RETURN_NONE;
+        }
+        const void* p = x.data_ptr();
+        if (numels[t] && (reinterpret_cast<uintptr_t>(p) & 15)) Py_RETURN_NONE;
+        src[t * K + i] = p;
+      }
+    }
+    PyObject* sobj = PyObject_CallFunction(stream_of, "i", dev);
+    if (!sobj) return nullptr;
+    const unsigned long long stream = PyLong_AsUnsignedLongLong(sobj);
+    Py_DECREF(sobj);
+    if (stream == static_cast<unsigned long long>(-1) && PyErr_Occurred()) return nullptr;
+    std::vector<at::Tensor> outs;  // only once every key has passed
+    outs.reserve(size_t(T));
+    void* optr[kDevRoundMaxKeys];
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      outs.push_back(at::empty(first[t]->sizes(), first[t]->options().dtype(at::kFloat)));
+      optr[t] = outs.back().data_ptr();
+      if (reinterpret_cast<uintptr_t>(optr[t]) & 15) Py_RETURN_NONE;  // the caching allocator never does this
+    }
+    const int rc = reinterpret_cast<DeviceRoundFn>(fn_addr)(src, codes, numels, int32_t(T), int32_t(K), w, optr,
+                                                            reinterpret_cast<void*>(stream));
+    PyObject* py_outs = PyList_New(T);
+    if (!py_outs) return nullptr;
+    for (Py_ssize_t t = 0; t < T; ++t) {
+      PyObject* o = THPVariable_Wrap(std::move(outs[t]));
+      if (!o) {
+        Py_DECREF(py_outs);
+        return nullptr;
+      }
+      PyList_SET_ITEM(py_outs, t, o);
+    }
+    return Py_BuildValue("(iN)", rc, py_outs);
+  } catch (const std::exception&) {
+    PyErr_Clear();
+    Py_RETURN_NONE;
+  }
+}
+
 // group_by_device(d: dict, keys: list) -> None | [(device, [key indices])]
 //   The keys of one state dict grouped by the CUDA device their tensor lives
 //   on (devices in order of first appearance), each group largest tensor
@@ -559,6 +665,7 @@ PyMethodDef kMethods[] = {
     {"group_by_device", group_by_device, METH_VARARGS,
      "Key indices of a state dict grouped by CUDA device, largest first, or None."},
     {"host_round", host_round, METH_VARARGS, "One small host round through fedagg_host_round_f32, or None."},
+    {"device_round", device_round, METH_VARARGS, "One small device round through fedagg_device_round_f32, or None."},
     {"walk", walk, METH_VARARGS, "Pointer tables of K device state dicts for fedagg_wsum_multi, or None."},
     {"order_by_size", order_by_size, METH_VARARGS, "Key indices of a state dict, largest tensor first, or None."},
     {"walk_host", walk_host, METH_VARARGS, "Host pointer tables of K CPU state dicts for one batched pack, or None."},

@@ -37,8 +37,25 @@ Supported server optimizers (OptRepo names, optrepo.py:10); parameters are fp32:
           momentum 0, not centered, weight_decay 0)
           (fedagg_wsum_fedopt_rmsprop_f32); square_avg bit-identical to
           torch, parameters with the sqrt caveat.
-Any other OptRepo name, and weight decay / momentum / centered variants of
-these, raise NotImplementedError.
+  "adamax" / "nadam" / "radam" / "adadelta" / "asgd" / "rprop"
+          the other elementwise optimizers OptRepo names, with torch's
+          defaults and lr=server_lr as FedOptAPI builds them
+          (fedagg_wsum_fedopt_optrepo_f32, the per-element rules beside
+          OptRepoEpi in csrc/fedagg.hip).  Adamax, ASGD and Rprop take no
+          sqrt and are bit-exact with torch, state included; NAdam, RAdam and
+          Adadelta carry Adam's sqrt caveat (Adadelta's acc_delta too, since
+          it is built from a square root).  server_momentum is ignored for
+          them, as for Adam.
+Any other OptRepo name (LBFGS needs a closure, SparseAdam sparse gradients,
+Adafactor and Muon are not elementwise), and weight decay / momentum /
+centered variants of these, raise NotImplementedError.
+
+A client dict added at two indices (add_local_trained_result) behaves as in
+FedOptAggregator.aggregate (:93-101): the averaged dict IS index 0's, so an
+index holding that same dict object reads the running average at its turn
+in the loop.  Such a round is reduced by the aliasing program of
+fedml_amd.agg_operator (_run_cells) and then stepped with the average as one
+source at weight 1.0, bit-identical to the reference's chain.
 
 Device layout: the round's updates sit in a ClientBucket; the global model
 and the momentum buffers are flat fp32 vectors with the bucket's fp32 layout.
@@ -57,7 +74,47 @@ import torch
 from . import kernels as kn
 from .bucket import ClientBucket
 
-FUSED_OPTIMIZERS = ("sgd", "adam", "adamw", "adagrad", "rmsprop")
+# the OptRepo optimizers of fedagg_wsum_fedopt_optrepo_f32 and their
+# per-element state buffers (torch's state names, in the kernel's order)
+OPTREPO_STATE = {"adamax": ("exp_avg", "exp_inf"), "nadam": ("exp_avg", "exp_avg_sq"),
+                 "radam": ("exp_avg", "exp_avg_sq"), "adadelta": ("square_avg", "acc_delta"),
+                 "asgd": ("ax",), "rprop": ("prev", "step_size")}
+FUSED_OPTIMIZERS = ("sgd", "adam", "adamw", "adagrad", "rmsprop") + tuple(OPTREPO_STATE)
+# OptRepo names that cannot be a fused elementwise server step
+_NOT_ELEMENTWISE = {"lbfgs": "torch.optim.LBFGS.step() needs a closure",
+                    "sparseadam": "torch.optim.SparseAdam takes sparse gradients only",
+                    "adafactor": "torch.optim.Adafactor's second moment is factored over rows and columns",
+                    "muon": "torch.optim.Muon orthogonalises 2-D updates (Newton-Schulz matrix products)"}
+
+
+def _unsupported(name: str) -> NotImplementedError:
+    why = _NOT_ELEMENTWISE.get(name.lower())
+    return NotImplementedError(f"server_optimizer {name!r}: " + (f"{why}; " if why else "") +
+                               f"{FUSED_OPTIMIZERS} are fused")
+
+
+def optrepo_carry(optimizer: str, lr: float) -> "ctypes.Array":
+    """The fp32 scalar state of an OptRepo optimizer before its first step:
+    NAdam's mu_product 1.0; ASGD's eta fl32(lr) and mu 1.0."""
+    import ctypes
+
+    c = (ctypes.c_float * 2)()
+    if optimizer == "nadam":
+        c[0] = 1.0
+    elif optimizer == "asgd":
+        c[0], c[1] = lr, 1.0
+    return c
+
+
+def _ref(obj):
+    """A reference that does not keep a client's dict alive where Python
+    allows it (OrderedDict, every state_dict), a strong one otherwise."""
+    import weakref
+
+    try:
+        return weakref.ref(obj)
+    except TypeError:
+        return lambda: obj
 
 
 def _weight_decay(optimizer: str, weight_decay: Optional[float]) -> float:
@@ -89,7 +146,7 @@ class FedOptServer:
                  server_momentum: float = 0.0, device=None, server_weight_decay: Optional[float] = None):
         self.optimizer = server_optimizer.lower()
         if self.optimizer not in FUSED_OPTIMIZERS:
-            raise NotImplementedError(f"server_optimizer {server_optimizer!r}: {FUSED_OPTIMIZERS} are fused")
+            raise _unsupported(server_optimizer)
         self.lr = float(server_lr)
         _check_momentum(self.optimizer, server_momentum)
         self.momentum = float(server_momentum) if self.optimizer == "sgd" else 0.0
@@ -124,6 +181,14 @@ class FedOptServer:
             # Adagrad's state_sum, RMSprop's square_avg: both start at zero
             acc = f32 and self.optimizer in ("adagrad", "rmsprop")
             self.state_sum = torch.zeros_like(self.global_flat[torch.float32]) if acc else None
+            # the OptRepo optimizers' per-element state, as torch creates it
+            self.opt_state: Dict[str, torch.Tensor] = {}
+            if f32 and self.optimizer in OPTREPO_STATE:
+                for name in OPTREPO_STATE[self.optimizer]:
+                    self.opt_state[name] = torch.zeros_like(self.global_flat[torch.float32])
+                if self.optimizer == "rprop":  # step_size = full_like(grad, lr)
+                    self.opt_state["step_size"].fill_(self.lr)
+        self._carry = optrepo_carry(self.optimizer, self.lr)
         self.first_step = True
         self._views: Optional["OrderedDict[str, torch.Tensor]"] = None
         self.runs: List[Tuple[bool, int, int]] = self._runs(f32) if f32 else []
@@ -132,6 +197,8 @@ class FedOptServer:
         self.model_dict: Dict[int, "OrderedDict"] = {}
         self.sample_num_dict: Dict[int, float] = {}
         self.flag_client_model_uploaded_dict = {i: False for i in range(worker_num)}
+        self._refs: Dict[int, object] = {}  # index -> reference to the dict added there this round
+        self._same: set = set()  # {i, j} index pairs that were handed the same dict object
 
     def _runs(self, g) -> List[Tuple[bool, int, int]]:
         """Maximal runs of consecutive keys of one kind: (is_param, lo, hi)."""
@@ -152,8 +219,24 @@ class FedOptServer:
     def add_local_trained_result(self, index: int, model_params, sample_num) -> None:
         """:68-72; the update goes straight into its HBM row."""
         self.bucket.put(index, model_params, sample_num)
+        self.note_dict(index, model_params)
         self.sample_num_dict[index] = sample_num
         self.flag_client_model_uploaded_dict[index] = True
+
+    def note_dict(self, index: int, model_params) -> None:
+        """Remember which dict object index holds this round, and which other
+        indices hold the same object (compared while both are alive, so a
+        reused id() of a freed dict cannot match)."""
+        self._same = {p for p in self._same if index not in p}
+        for i, r in self._refs.items():
+            if i != index and r() is model_params:
+                self._same.add(frozenset((i, index)))
+        self._refs[index] = _ref(model_params)
+
+    def _aliases_of_client0(self) -> List[int]:
+        """Indices j > 0 holding index 0's dict object: FedOptAggregator.py:
+        93-101 reads the running average there."""
+        return sorted(j for p in self._same if 0 in p for j in p if j != 0 and j < self.worker_num)
 
     def check_whether_all_receive(self) -> bool:
         for idx in range(self.worker_num):
@@ -169,51 +252,103 @@ class FedOptServer:
         ns = [self.sample_num_dict[i] for i in range(self.worker_num)]
         weights = self.bucket.weights(ns)
         K = self.worker_num
+        alias = self._aliases_of_client0()
+        self._refs, self._same = {}, set()  # the round's dicts are consumed
         with torch.cuda.device(self.device):
             self.bucket.sync_ingest()
+            if alias:
+                return self._aggregate_aliased(ns, weights, alias, events)
             w32 = kn.weights_for(weights, torch.float32, self.device)  # by value for K <= 256
-            f32 = self.global_flat.get(torch.float32)
-            step = self.step_count + 1
-            sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step) \
-                if self.optimizer in ("adam", "adamw") else None
-            if events is not None:
-                events[0].record()
-            # torch's Adagrad: clr = lr / (1 + (step - 1) * lr_decay), in double
-            clr = self.lr / (1 + (step - 1) * self.lr_decay)
-            for (is_param, lo, hi), d_ptrs in zip(self.runs, self.run_ptrs):
-                if is_param and self.optimizer == "adagrad":
-                    kn.wsum_fedopt_adagrad(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], clr, self.eps,
-                                           True)
-                elif is_param and self.optimizer == "rmsprop":
-                    kn.wsum_fedopt_rmsprop(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], self.lr,
-                                           self.alpha, self.eps, True)
-                elif is_param and self.optimizer == "adamw":
-                    kn.wsum_fedopt_adamw(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
-                                         self.exp_avg_sq[lo:hi], sc, 1 - self.lr * self.weight_decay,
-                                         self.first_step, True)
-                elif is_param and sc is not None:
-                    kn.wsum_fedopt_adam(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
-                                        self.exp_avg_sq[lo:hi], sc, self.first_step, True)
-                elif is_param:
-                    kn.wsum_fedopt_sgd(d_ptrs, w32, K, hi - lo, f32[lo:hi],
-                                       self.mom[lo:hi] if self.mom is not None else None,
-                                       self.lr, self.momentum, self.first_step, True)
-                else:
-                    kn.wsum_ptrs(torch.float32, d_ptrs, w32, K, hi - lo, f32[lo:hi], True)
-            if events is not None:
-                events[1].record()
-            for dt, g in self.bucket.groups.items():
-                if dt == torch.float32 or g.length == 0:
-                    continue
-                w = kn.weights_for(weights, dt, self.device)
-                kn.wsum_ptrs(dt, g.d_ptrs, w, K, g.length, self.global_flat[dt], True)
-            for k, t in self._int_state.items():
-                # load_state_dict's copy_: the float32 average truncates toward zero
-                g, j = self.bucket.where[k]
-                t.reshape(-1).copy_(self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]])
+            return self._step(self.run_ptrs, w32, K, weights, events)
+
+    def _step(self, run_ptrs, w32, K: int, weights, events, averaged=None) -> "OrderedDict[str, torch.Tensor]":
+        """The fused launches of one round over `run_ptrs` (K sources per run
+        at weights w32); `averaged`, when given, holds the round's average per
+        dtype group for the groups the fused runs do not cover."""
+        f32 = self.global_flat.get(torch.float32)
+        step = self.step_count + 1
+        sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step) \
+            if self.optimizer in ("adam", "adamw") else None
+        osc = kn.optrepo_scalars(self.optimizer, self.lr, step, self._carry) \
+            if self.optimizer in OPTREPO_STATE else None
+        st0 = self.opt_state.get(OPTREPO_STATE[self.optimizer][0]) if osc is not None else None
+        st1 = self.opt_state.get(OPTREPO_STATE[self.optimizer][-1]) if osc is not None and \
+            len(OPTREPO_STATE[self.optimizer]) > 1 else None
+        if events is not None:
+            events[0].record()
+        # torch's Adagrad: clr = lr / (1 + (step - 1) * lr_decay), in double
+        clr = self.lr / (1 + (step - 1) * self.lr_decay)
+        for (is_param, lo, hi), d_ptrs in zip(self.runs, run_ptrs):
+            if is_param and osc is not None:
+                kn.wsum_fedopt_optrepo(self.optimizer, d_ptrs, w32, K, hi - lo, f32[lo:hi], st0[lo:hi],
+                                       st1[lo:hi] if st1 is not None else None, osc, True)
+            elif is_param and self.optimizer == "adagrad":
+                kn.wsum_fedopt_adagrad(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], clr, self.eps,
+                                       True)
+            elif is_param and self.optimizer == "rmsprop":
+                kn.wsum_fedopt_rmsprop(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], self.lr,
+                                       self.alpha, self.eps, True)
+            elif is_param and self.optimizer == "adamw":
+                kn.wsum_fedopt_adamw(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
+                                     self.exp_avg_sq[lo:hi], sc, 1 - self.lr * self.weight_decay,
+                                     self.first_step, True)
+            elif is_param and sc is not None:
+                kn.wsum_fedopt_adam(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
+                                    self.exp_avg_sq[lo:hi], sc, self.first_step, True)
+            elif is_param:
+                kn.wsum_fedopt_sgd(d_ptrs, w32, K, hi - lo, f32[lo:hi],
+                                   self.mom[lo:hi] if self.mom is not None else None,
+                                   self.lr, self.momentum, self.first_step, True)
+            else:
+                kn.wsum_ptrs(torch.float32, d_ptrs, w32, K, hi - lo, f32[lo:hi], True)
+        if events is not None:
+            events[1].record()
+        for dt, g in self.bucket.groups.items():
+            if dt == torch.float32 or g.length == 0:
+                continue
+            if averaged is not None:
+                self.global_flat[dt][:g.length].copy_(averaged[dt][:g.length])
+                continue
+            w = kn.weights_for(weights, dt, self.device)
+            kn.wsum_ptrs(dt, g.d_ptrs, w, K, g.length, self.global_flat[dt], True)
+        for k, t in self._int_state.items():
+            # load_state_dict's copy_: the float32 average truncates toward zero
+            g, j = self.bucket.where[k]
+            t.reshape(-1).copy_(self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]])
         self.first_step = False
         self.step_count += 1
         return self.get_global_model_params()
+
+    def _aggregate_aliased(self, ns, weights, alias: List[int], events) -> "OrderedDict[str, torch.Tensor]":
+        """A round whose index-0 dict was added again at `alias`: the
+        reference's loop (FedOptAggregator.py:93-101) replayed over the
+        bucket's rows by agg_operator._run_cells, which reads the running
+        average wherever the loop reads index 0's dict again; then the
+        optimizer steps from that average as ONE source at weight 1.0
+        (fl(x * 1.0) = x: the same step bit for bit)."""
+        from .agg_operator import _run_cells
+
+        class _A:
+            fedagg_low_precision_acc = "reference"
+            fedagg_device = None
+
+        views = [self.bucket.view(i) for i in range(self.worker_num)]
+        raw = [(ns[i], views[i]) for i in range(self.worker_num)]
+        for j in alias:
+            raw[j] = (ns[j], views[0])
+        keys = [k for k, _, _ in self.bucket.entries]
+        _run_cells(raw, (1,), keys, weights, _A())
+        avg = views[0]  # rebound to the round's average, key by key
+        flat = self.bucket.new_outputs()
+        for k in keys:
+            g, j = self.bucket.where[k]
+            flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]].copy_(avg[k].reshape(-1))
+        f32 = flat.get(torch.float32)
+        run_ptrs = [kn.upload_i64([f32.data_ptr() + lo * 4], self.device) for _, lo, _ in self.runs] if f32 is not None \
+            else []
+        out = self._step(run_ptrs, kn.HostWeights([1.0]), 1, [1.0], events, averaged=flat)
+        torch.cuda.current_stream(self.device).synchronize()  # the one-off tables and the flat average
+        return out
 
     # ---- optimizer state (the reference's opt.state_dict() round trip) ------
 
@@ -226,13 +361,21 @@ class FedOptServer:
         """Per named parameter, the state torch's optimizer would hold after the
         same rounds: {"step": n, <buffer>: {name: tensor}} with buffer
         "momentum_buffer" (sgd with momentum), "exp_avg" / "exp_avg_sq"
-        (adam) or "sum" (adagrad).  Copies; for checkpointing and parity checks."""
+        (adam), "sum" (adagrad), "square_avg" (rmsprop) or OPTREPO_STATE's
+        names, plus the fp32 scalar state as floats ("mu_product" for nadam,
+        "eta" / "mu" for asgd; torch keeps one equal tensor per parameter).
+        Copies; for checkpointing and parity checks."""
         out: Dict[str, object] = {"step": self.step_count}
         bufs = self._state_buffers()
         for name, flat in bufs.items():
             if flat is None or (self.step_count == 0 and self.optimizer != "adagrad"):
                 continue
             out[name] = OrderedDict((k, flat[o:o + n].view(shape).clone()) for k, o, n, shape in self._param_slices())
+        if self.step_count:  # the fp32 scalar state, the same for every parameter
+            if self.optimizer == "nadam":
+                out["mu_product"] = float(self._carry[0])
+            elif self.optimizer == "asgd":
+                out["eta"], out["mu"] = float(self._carry[0]), float(self._carry[1])
         return out
 
     def _state_buffers(self) -> Dict[str, Optional[torch.Tensor]]:
@@ -243,6 +386,8 @@ class FedOptServer:
             return {"sum": self.state_sum}  # exists from construction in torch (initial_accumulator_value)
         if self.optimizer == "rmsprop":
             return {"square_avg": self.state_sum}  # created at the first step in torch
+        if self.optimizer in OPTREPO_STATE:
+            return {name: self.opt_state.get(name) for name in OPTREPO_STATE[self.optimizer]}
         return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
 
     def load_optimizer_state(self, state: Dict[str, object]) -> None:
@@ -259,9 +404,21 @@ class FedOptServer:
                     if step:
                         raise KeyError(f"optimizer state at step {step} lacks {name!r}")
                     flat.zero_()  # a fresh optimizer's state
+                    if name == "step_size":  # Rprop's starts at lr
+                        flat.fill_(self.lr)
                     continue
                 for k, o, n, _ in self._param_slices():
                     flat[o:o + n].copy_(src[k].detach().reshape(-1))
+        self._carry = optrepo_carry(self.optimizer, self.lr)
+        for i, name in enumerate({"nadam": ("mu_product",), "asgd": ("eta", "mu")}.get(self.optimizer, ())):
+            v = state.get(name)
+            if v is None:
+                if step:
+                    raise KeyError(f"optimizer state at step {step} lacks {name!r}")
+                continue
+            if isinstance(v, dict):  # torch's per-parameter scalar tensors (all equal)
+                v = next(iter(v.values()))
+            self._carry[i] = float(v)
         self.step_count = step
         self.first_step = step == 0
 
@@ -294,6 +451,9 @@ class FedOptServer:
                 tot += 2 * n * 4 + (4 if not self.first_step else 2) * n * 4
             elif self.optimizer in ("adagrad", "rmsprop"):  # p and state_sum / square_avg read and written
                 tot += 4 * n * 4
+            elif self.optimizer in OPTREPO_STATE:  # p and each state buffer read and written (ASGD: ax written)
+                tot += 2 * n * 4 + (2 * len(OPTREPO_STATE[self.optimizer]) * n * 4 if self.optimizer != "asgd"
+                                    else n * 4)
             else:
                 tot += 2 * n * 4 + (2 * n * 4 if self.mom is not None and not self.first_step else
                                     (n * 4 if self.mom is not None else 0))
@@ -361,6 +521,7 @@ class MultiDeviceFedOptServer:
         gather_jobs([j for _, js in jobs for j in js])
         for s, js in jobs:
             s.bucket.put_issue(js)
+            s.note_dict(index, model_params)
             s.sample_num_dict[index] = sample_num
             s.flag_client_model_uploaded_dict[index] = True
         dict.__setitem__(self.sample_num_dict, index, sample_num)
@@ -400,18 +561,20 @@ class MultiDeviceFedOptServer:
         out: Dict[str, object] = {"step": self.step_count}
         for s in self.servers:
             for name, v in s.optimizer_state().items():
-                if name != "step":
+                if isinstance(v, dict):
                     out.setdefault(name, OrderedDict()).update(v)
+                elif name != "step":  # a scalar state, the same on every device
+                    out[name] = v
         for name, v in list(out.items()):  # the model's parameter order
-            if name != "step":
+            if isinstance(v, dict):
                 out[name] = OrderedDict((k, v[k]) for k in self.param_names if k in v)
         return out
 
     def load_optimizer_state(self, state: Dict[str, object]) -> None:
         for s in self.servers:
             mine = {k for k, _, _ in s.bucket.entries}
-            s.load_optimizer_state({name: (v if name == "step" else
-                                           OrderedDict((k, t) for k, t in v.items() if k in mine))
+            s.load_optimizer_state({name: (OrderedDict((k, t) for k, t in v.items() if k in mine)
+                                           if isinstance(v, dict) else v)
                                     for name, v in state.items()})
 
     def algorithmic_bytes(self) -> int:

@@ -199,7 +199,7 @@ def muldiv_weights(dtype: torch.dtype, pairs: Sequence, device: torch.device) ->
         rec["d"] = [scalar_f32(d) for _, d in pairs]
     raw = np.frombuffer(rec.tobytes(), dtype=np.uint8)
     host = torch.from_numpy(raw.copy())
-    if torch.cuda.is_available():
+    if _cuda_ok():
         host = host.pin_memory()
     return host.to(device, non_blocking=True)
 
@@ -428,6 +428,32 @@ def wsum_fedopt_rmsprop(d_ptrs: torch.Tensor, d_w, K: int, N: int, param: torch.
     nat.check(nat.lib().fedagg_wsum_fedopt_rmsprop_f32(
         d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), square_avg.data_ptr(), float(lr), float(alpha),
         float(eps), flags, nat.stream_handle()), "wsum_fedopt_rmsprop_f32")
+
+
+def optrepo_scalars(opt: str, lr: float, step: int, carry: "ctypes.Array") -> "ctypes.Array":
+    """The nine fp32 scalars of one step of an OptRepo optimizer
+    (fedagg_optrepo_scalars; `carry` is its fp32 scalar state, two floats,
+    updated in place: NAdam's mu_product, ASGD's eta and mu)."""
+    out = (ctypes.c_float * 9)()
+    nat.check(nat.lib().fedagg_optrepo_scalars(nat.OPT_CODES[opt], float(lr), int(step), ctypes.addressof(carry),
+                                               ctypes.addressof(out)), "optrepo_scalars")
+    return out
+
+
+def wsum_fedopt_optrepo(opt: str, d_ptrs: torch.Tensor, d_w, K: int, N: int, param: torch.Tensor,
+                        state0: torch.Tensor, state1: Optional[torch.Tensor], scalars: "ctypes.Array",
+                        aligned: bool) -> None:
+    """FedAvg of K fp32 sources fused with the server step of an OptRepo
+    optimizer (adamax / nadam / radam / adadelta / asgd / rprop): param and
+    the state buffers (flat, N elements each) are updated in place."""
+    _require_cuda(param, "wsum_fedopt_optrepo")
+    ts = [t for t in (param, state0, state1) if t is not None]
+    ok = aligned and all((t.data_ptr() & 15) == 0 for t in ts)
+    flags = (nat.FEDAGG_ALIGNED16 if ok else 0) | (nat.FEDAGG_HOST_WEIGHTS if isinstance(d_w, HostWeights) else 0)
+    nat.check(nat.lib().fedagg_wsum_fedopt_optrepo_f32(
+        nat.OPT_CODES[opt], d_ptrs.data_ptr(), d_w.data_ptr(), K, N, param.data_ptr(), state0.data_ptr(),
+        state1.data_ptr() if state1 is not None else None, ctypes.addressof(scalars), flags, nat.stream_handle()),
+        f"wsum_fedopt_optrepo_f32 ({opt})")
 
 
 def round_f32(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

@@ -237,6 +237,23 @@ def _report(args, round_args, metrics) -> tuple:
     return (test_acc, test_loss, None, None)
 
 
+def _plain_load(model) -> bool:
+    """load_state_dict would do nothing to this model's values but copy_ them:
+    no load-state-dict pre / post hooks on any submodule (nor the model-level
+    ones), and no _load_from_state_dict override besides torch's BatchNorm one
+    (_NormBase's only fills in a missing num_batches_tracked of an old
+    checkpoint; the fast path passes every key)."""
+    from torch.nn.modules.batchnorm import _NormBase
+
+    for m in model.modules():
+        if getattr(m, "_load_state_dict_pre_hooks", None) or getattr(m, "_load_state_dict_post_hooks", None):
+            return False
+        f = type(m)._load_from_state_dict
+        if f is not torch.nn.Module._load_from_state_dict and f is not _NormBase._load_from_state_dict:
+            return False
+    return True
+
+
 class MI355XServerAggregator(ServerAggregator):
     """DefaultServerAggregator (default_aggregator.py:12-106) on MI355X:
     state_dict in, load_state_dict out, FedAvg on the GPU, and the
@@ -266,10 +283,20 @@ class MI355XServerAggregator(ServerAggregator):
                 and any(isinstance(t, torch.Tensor) and t.is_cuda for t in model_parameters.values())):
             from .host_copy import to_host
 
+            if not _plain_load(self.model):
+                # a module transforms values on load (its own _load_from_state_dict
+                # or load hooks): load_state_dict runs them, on host tensors
+                # copied one DMA per result buffer instead of one D2H per key
+                self.model.load_state_dict(to_host(model_parameters))
+                return
             host = to_host(model_parameters, into=sd)
-            # keys written in place are the model's own tensors; the rest
+            # keys written in place are the model's own tensors, so bump their
+            # version counters as load_state_dict's copy_ does; the rest
             # (another dtype, e.g. int64 counters from float32 averages) take
             # load_state_dict's conversion
+            for k, v in host.items():
+                if v is sd[k]:
+                    torch.autograd.graph.increment_version(v)
             rest = OrderedDict((k, v) for k, v in host.items() if v is not sd[k])
             if rest:
                 self.model.load_state_dict(rest, strict=False)

@@ -295,11 +295,12 @@ class ShardedFedOpt:
     def __init__(self, rows: torch.Tensor, length: int, global_flat: torch.Tensor, optimizer: str = "sgd",
                  lr: float = 1.0, momentum: float = 0.0, group=None, chunks: int = 8, reducer=None, stepper=None,
                  buffers: Sequence[Tuple[int, int]] = (), weight_decay: Optional[float] = None):
-        from .fedopt import FUSED_OPTIMIZERS, _check_momentum, _weight_decay
+        from .fedopt import (FUSED_OPTIMIZERS, OPTREPO_STATE, _check_momentum, _unsupported, _weight_decay,
+                             optrepo_carry)
 
         self.optimizer = optimizer.lower()
         if self.optimizer not in FUSED_OPTIMIZERS:
-            raise NotImplementedError(f"server_optimizer {optimizer!r}: {FUSED_OPTIMIZERS} are fused")
+            raise _unsupported(optimizer)
         _check_momentum(self.optimizer, momentum)
         self.lr, self.momentum = float(lr), float(momentum) if self.optimizer == "sgd" else 0.0
         self.betas, self.eps = (0.9, 0.999), (1e-10 if self.optimizer == "adagrad" else 1e-8)
@@ -333,8 +334,14 @@ class ShardedFedOpt:
             self.state = {"exp_avg": z(), "exp_avg_sq": z()}
         elif self.optimizer == "adagrad":
             self.state = {"sum": z()}
+        elif self.optimizer in OPTREPO_STATE:
+            self.state = {name: z() for name in OPTREPO_STATE[self.optimizer]}
+            if self.optimizer == "rprop":
+                self.state["step_size"].fill_(self.lr)
         else:
             self.state = {"square_avg": z()}
+        self._carry = optrepo_carry(self.optimizer, self.lr)
+        self._names = OPTREPO_STATE.get(self.optimizer, ())
         self.step_count = 0
         if self.agg.on_gpu and stepper is None:
             self._src = kn.upload_i64([self.agg.shard.data_ptr()], dev)  # one source: the reduced shard
@@ -362,6 +369,10 @@ class ShardedFedOpt:
                 sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step)
                 kn.wsum_fedopt_adamw(self._src, one, 1, n, self.param, self.state["exp_avg"],
                                      self.state["exp_avg_sq"], sc, 1 - self.lr * self.weight_decay, first, True)
+            elif self._names:
+                osc = kn.optrepo_scalars(self.optimizer, self.lr, step, self._carry)
+                kn.wsum_fedopt_optrepo(self.optimizer, self._src, one, 1, n, self.param, self.state[self._names[0]],
+                                       self.state[self._names[-1]] if len(self._names) > 1 else None, osc, True)
             elif self.optimizer == "rmsprop":
                 kn.wsum_fedopt_rmsprop(self._src, one, 1, n, self.param, self.state["square_avg"], self.lr,
                                        self.alpha, self.eps, True)

@@ -37,7 +37,10 @@ class _Defaults:
 
 def fedavg_aggregate(w_locals: List[Tuple[float, "OrderedDict"]], args=None) -> "OrderedDict":
     """fedavg_api.py:144-159.  ``args`` (optional) may carry the fedml_amd
-    options ``fedagg_device`` / ``fedagg_low_precision_acc``."""
+    options ``fedagg_device`` / ``fedagg_low_precision_acc``.  Client 0's
+    dict listed again reads the running average, as the reference's
+    rebind-then-``+=`` loop makes it (fedml_amd.agg_operator._run_cells, the
+    rule torch_aggregator follows)."""
     training_num = 0
     for idx in range(len(w_locals)):
         (sample_num, averaged_params) = w_locals[idx]
@@ -47,8 +50,11 @@ def fedavg_aggregate(w_locals: List[Tuple[float, "OrderedDict"]], args=None) -> 
     if not keys:
         return averaged_params
     weights = [w_locals[i][0] / training_num for i in range(len(w_locals))]
-    res = weighted_reduce([w_locals[i][1] for i in range(len(w_locals))], keys, weights,
-                          args if args is not None else _Defaults())
+    a = args if args is not None else _Defaults()
+    if _reads_running_cell(w_locals, (1,)):  # client 0's dict listed again reads the running sum (:150-158)
+        _run_cells(w_locals, (1,), keys, weights, a)
+        return averaged_params
+    res = weighted_reduce([w_locals[i][1] for i in range(len(w_locals))], keys, weights, a)
     for k in keys:
         averaged_params[k] = res[k]
     return averaged_params

@@ -245,6 +245,40 @@ int fedagg_wsum_fedopt_rmsprop_f32(const float* const* d_src, const float* d_w,
                                    float eps, uint32_t flags,
                                    fedagg_stream_t stream);
 
+/* The other elementwise optimizers OptRepo names (sp/fedopt/optrepo.py:10,
+ * torch.optim's direct Optimizer subclasses), each as FedOptAPI builds it
+ * with lr only (fedopt_api.py:78-85) and steps it (:121-130), fused with the
+ * FedAvg of K fp32 clients in one pass.  opt selects the optimizer; state0 /
+ * state1 are its per-element buffers in the state torch creates before its
+ * first step:
+ *   FEDAGG_OPT_ADAMAX    exp_avg / exp_inf       (zeros)
+ *   FEDAGG_OPT_NADAM     exp_avg / exp_avg_sq    (zeros)
+ *   FEDAGG_OPT_RADAM     exp_avg / exp_avg_sq    (zeros)
+ *   FEDAGG_OPT_ADADELTA  square_avg / acc_delta  (zeros)
+ *   FEDAGG_OPT_ASGD      ax / unused (may be NULL)  (zeros)
+ *   FEDAGG_OPT_RPROP     prev / step_size        (zeros / fl32(lr))
+ * scalars9 (host memory) comes from fedagg_optrepo_scalars() for the 1-based
+ * step about to be taken; carry2 is the optimizer's fp32 scalar state, updated
+ * by that call: NAdam's mu_product (1.0 before the first step), ASGD's eta and
+ * mu (fl32(lr), 1.0), ignored otherwise.  Per element each step rounds as
+ * torch 2.10's single-tensor CPU path (lerp_ / addcmul_ / add_(alpha) fused,
+ * addcdiv_ not; the formulas beside OptRepoEpi in csrc/fedagg.hip); sqrt is
+ * correctly rounded, so NAdam / RAdam / Adadelta differ from torch's MKL sqrt
+ * by its rounding only (Adamax, ASGD and Rprop take no sqrt: bit-exact). */
+#define FEDAGG_OPT_ADAMAX 1
+#define FEDAGG_OPT_NADAM 2
+#define FEDAGG_OPT_RADAM 3
+#define FEDAGG_OPT_ADADELTA 4
+#define FEDAGG_OPT_ASGD 5
+#define FEDAGG_OPT_RPROP 6
+int fedagg_optrepo_scalars(int32_t opt, double lr, int64_t step, float* carry2,
+                           float* out9);
+int fedagg_wsum_fedopt_optrepo_f32(int32_t opt, const float* const* d_src,
+                                   const float* d_w, int32_t K, int64_t N,
+                                   float* d_param, float* d_state0,
+                                   float* d_state1, const float* scalars9,
+                                   uint32_t flags, fedagg_stream_t stream);
+
 /* ---- Robust aggregation --------------------------------------------------- */
 
 /* Coordinate-wise median over K fp32 clients (the "wise_median" defense,
@@ -399,6 +433,27 @@ int fedagg_host_unpack(const void* src, void* const* dsts, const int64_t* src_of
 int fedagg_host_gather(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int32_t n,
                        int32_t threads);
 
+/* ---- Small device-resident rounds --------------------------------------- */
+
+/* One whole FedAvg round of DEVICE tensors in one launch: the reference call
+ * shape FedMLAggOperator.agg(args, [(n_i, gpu_state_dict)]) (agg_operator.py:
+ * 35-44, the server's `using_gpu` mode, ml_engine_adapter.py:234-254) for
+ * rounds of at most 16 keys and 128 client tensors (config 1: 4 clients x 2
+ * keys), where uploads and launches, not bytes, are the cost.
+ *   d_src   : host array of device pointers [T][K], key-major (key t of
+ *             client i at t*K + i), 16-byte aligned
+ *   codes   : FEDAGG_DT_F32 or FEDAGG_DT_I64 per key (int64 values enter as
+ *             fl32(v) and give fp32 results, the reference's promotion)
+ *   weights : K fp32 weights fl32(n_i / sum n), host memory
+ *   d_out   : host array of T device fp32 buffers (16-byte aligned)
+ * Every pointer, length and weight travels in the kernel arguments (no
+ * upload, no allocation); asynchronous and ordered on `stream`.
+ * Bit-identical to the reference chain. */
+int fedagg_device_round_f32(const void* const* d_src, const int32_t* codes,
+                            const int64_t* numels, int32_t T, int32_t K,
+                            const float* weights, void* const* d_out,
+                            fedagg_stream_t stream);
+
 /* ---- Small host-resident rounds ----------------------------------------- */
 
 /* One whole FedAvg round of HOST tensors, host to host, in one call: the
@@ -428,31 +483,6 @@ int fedagg_host_round_f32(const void* const* h_src, const int32_t* codes,
 const char* fedagg_last_error(void);
 int32_t fedagg_version(void);
 
-/* Tuning entry (not part of the product path): fp32 weighted sum with an
- * explicit kernel variant; used by tools/tune_wsum.py to pick the shipped
- * variant.  variant indexes the table printed by fedagg_variant_name(). */
-int fedagg_wsum_f32_variant(const float* const* d_src, const float* d_w,
-                            int32_t K, int64_t N, float* d_out,
-                            int32_t variant, fedagg_stream_t stream);
-const char* fedagg_variant_name(int32_t variant);
-int32_t fedagg_num_variants(void);
-
-/* Tuning entry for many clients over small tensors (tools/tune_tiny.py) and
- * for the tile shapes of large rows (tools/ab_backtoback.py): dtype
- * FEDAGG_DT_F32, FEDAGG_DT_BF16 (reference chain), FEDAGG_TUNE_BF16_F32OUT
- * (bf16 rows, fp32 partial out, as fedagg_wsum_bf16_f32out) or
- * FEDAGG_TUNE_BF16_ACC32 (bf16 rows, fp32 accumulation, FEDAGG_ACC_FP32);
- * the last two for wide tiles only, FEDAGG_EINVAL for the others; pointers
- * 16-byte aligned, d_w a device array; variant indexes
- * fedagg_tiny_variant_name(). */
-#define FEDAGG_TUNE_BF16_F32OUT 0x101
-#define FEDAGG_TUNE_BF16_ACC32 0x102
-int fedagg_wsum_tiny_variant(int32_t dtype, const void* const* d_src,
-                             const float* d_w, int32_t K, int64_t N,
-                             void* d_out, int32_t variant,
-                             fedagg_stream_t stream);
-const char* fedagg_tiny_variant_name(int32_t variant);
-int32_t fedagg_num_tiny_variants(void);
 
 #ifdef __cplusplus
 }

@@ -173,3 +173,10 @@ void oracle_adagrad_sum_f32(const float* p, const float* avg, float* sum, int64_
     sum[e] = fmaf(g, g, sum[e]);
   }
 }
+
+/* out = fmaf(a, b, c) elementwise: the fused multiply-adds of torch's CPU
+ * lerp_ / addcmul_ / add_(alpha) kernels, for the numpy restatements of the
+ * server optimizers (fedavg_oracle.py fedopt_step). */
+void oracle_fma_f32(const float* a, const float* b, const float* c, float* out, int64_t N) {
+  for (int64_t e = 0; e < N; ++e) out[e] = fmaf(a[e], b[e], c[e]);
+}

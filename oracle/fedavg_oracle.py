@@ -380,6 +380,7 @@ def clib() -> ctypes.CDLL:
             "oracle_fedopt_sgd_f32": [P, P, P, L, F, F, I],
             "oracle_adam_moments_f32": [P, P, P, P, L, F, F, F],
             "oracle_adagrad_sum_f32": [P, P, P, L],
+            "oracle_fma_f32": [P, P, P, P, L],
         }.items():
             fn = getattr(lib, name)
             fn.restype = None
@@ -577,6 +578,166 @@ def fedopt_rmsprop_round(global_sd: "OrderedDict[str, torch.Tensor]", param_name
     for k, t_old in global_sd.items():
         if k in param_names:
             p, state[k] = fedopt_rmsprop(to_np(t_old).ravel(), to_np(avg[k]).ravel(), state.get(k), lr, sqrt=sqrt)
+            out[k] = torch.from_numpy(p).reshape(t_old.shape)
+        else:
+            out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)
+    return out
+
+
+# The other elementwise optimizers OptRepo can name (sp/fedopt/optrepo.py:10,
+# the direct subclasses of torch.optim.Optimizer), each as FedOptAPI builds it
+# (lr only, torch defaults; fedopt_api.py:78-85) and steps it on grad =
+# p_old - avg (_set_model_global_grads :155-160), following torch 2.10's
+# single-tensor CPU paths op by op (torch/optim/{adamax,nadam,radam,adadelta,
+# asgd,rprop}.py, _single_tensor_*).  Every torch op is one IEEE rounding; the
+# fused ones are fmaf through the C oracle:
+#   lerp_(g, w)             fma(w, g - m, m) for w < 0.5, else fma(w - 1, g - m, g)
+#   mul_(b).addcmul_(x, x, value=c)   fma(fl(c * x), x, fl(s * b))
+#   add_(x, alpha=a)        fma(x, a, s)
+#   addcdiv_(x, d, value=c) s + fl(fl(c * x) / d)   (not fused)
+#   tensor / python float   divides by the float rounded to fp32
+#   python float / tensor   Tensor.__rtruediv__: fl(fl(1 / t) * fl32(float))
+# Scalars (bias corrections, NAdam's mu products, ASGD's eta) are computed in
+# double as torch computes them, and rounded to fp32 where a kernel takes them;
+# NAdam's mu_product and ASGD's eta / mu are fp32 state tensors.
+# sqrt: "torch" (torch's CPU sqrt, an MKL routine on this image, not
+# correctly rounded) or "ieee" (what the GPU computes), as for Adam.
+
+OPTREPO_STATE = {"adamax": ("exp_avg", "exp_inf"), "nadam": ("exp_avg", "exp_avg_sq"),
+                 "radam": ("exp_avg", "exp_avg_sq"), "adadelta": ("square_avg", "acc_delta"),
+                 "asgd": ("ax",), "rprop": ("prev", "step_size")}
+
+
+def _fma(a, b, c) -> np.ndarray:
+    n = max(np.size(a), np.size(b), np.size(c))
+    a, b, c = (np.ascontiguousarray(np.broadcast_to(np.float32(x) if np.ndim(x) == 0 else x, (n,)),
+                                    dtype=np.float32) for x in (a, b, c))
+    out = np.empty(n, np.float32)
+    clib().oracle_fma_f32(a.ctypes.data, b.ctypes.data, c.ctypes.data, out.ctypes.data, n)
+    return out
+
+
+def _sqrt(x: np.ndarray, sqrt: str) -> np.ndarray:
+    if sqrt == "torch":
+        return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).sqrt().numpy()
+    if sqrt == "ieee":
+        return np.sqrt(x).astype(np.float32)
+    raise ValueError(sqrt)
+
+
+def _lerp(m: np.ndarray, g: np.ndarray, w: float) -> np.ndarray:
+    wf = np.float32(w)
+    d = (g - m).astype(np.float32)
+    return _fma(wf, d, m) if abs(wf) < 0.5 else _fma(np.float32(wf - np.float32(1.0)), d, g)
+
+
+def _sign(x: np.ndarray) -> np.ndarray:
+    """torch.sign: (0 < x) - (x < 0), so 0 for NaN."""
+    return ((x > 0).astype(np.float32) - (x < 0).astype(np.float32)).astype(np.float32)
+
+
+def optrepo_init(opt: str, n: int, lr: float) -> Dict[str, object]:
+    """The state torch creates at a parameter's first step (buffers and the
+    per-parameter fp32 scalar tensors), before that step runs."""
+    z = lambda: np.zeros(n, np.float32)  # noqa: E731
+    st: Dict[str, object] = {name: z() for name in OPTREPO_STATE[opt]}
+    if opt == "rprop":
+        st["step_size"] = np.full(n, np.float32(lr), np.float32)
+    if opt == "nadam":
+        st["mu_product"] = np.float32(1.0)
+    if opt == "asgd":
+        st["eta"], st["mu"] = np.float32(lr), np.float32(1.0)
+    return st
+
+
+def fedopt_step(opt: str, p_old: np.ndarray, avg: np.ndarray, st: Dict[str, object], lr: float, step: int,
+                sqrt: str = "torch") -> np.ndarray:
+    """One server step of `opt` on one named parameter (1-based `step`); the
+    state dict is updated in place, the new parameter returned."""
+    p = np.ascontiguousarray(p_old, dtype=np.float32).reshape(-1).copy()
+    a = np.ascontiguousarray(avg, dtype=np.float32).reshape(-1)
+    g = (p - a).astype(np.float32)
+    f = np.float32
+    if opt in ("adamax", "nadam", "radam"):
+        b1, b2, eps = 0.9, 0.999, 1e-8
+        m = _lerp(st["exp_avg"], g, 1 - b1)
+        st["exp_avg"] = m
+        if opt == "adamax":  # adamax.py:277-303
+            ei = np.maximum((st["exp_inf"] * f(b2)).astype(np.float32), (np.abs(g) + f(eps)).astype(np.float32))
+            st["exp_inf"] = ei
+            clr = lr / (1 - b1 ** step)
+            return (p + (f(-clr) * m) / ei).astype(np.float32)
+        v = _fma((f(1 - b2) * g).astype(np.float32), g, (st["exp_avg_sq"] * f(b2)).astype(np.float32))
+        st["exp_avg_sq"] = v
+        bc2 = 1 - b2 ** step
+        if opt == "nadam":  # nadam.py:330-379, momentum_decay 4e-3
+            mu = b1 * (1.0 - 0.5 * (0.96 ** (step * 4e-3)))
+            mu_next = b1 * (1.0 - 0.5 * (0.96 ** ((step + 1) * 4e-3)))
+            mp = f(st["mu_product"] * f(mu))
+            st["mu_product"] = mp
+            denom = (_sqrt((v / f(bc2)).astype(np.float32), sqrt) + f(eps)).astype(np.float32)
+            p = (p + (f(-lr * (1.0 - mu) / (1.0 - float(mp))) * g) / denom).astype(np.float32)
+            mpn = float(mp) * mu_next
+            return (p + (f(-lr * mu_next / (1.0 - mpn)) * m) / denom).astype(np.float32)
+        # radam.py:301-360
+        bc1 = 1 - b1 ** step
+        bcm = (m / f(bc1)).astype(np.float32)
+        rho_inf = 2 / (1 - b2) - 1
+        rho_t = rho_inf - 2 * step * (b2 ** step) / bc2
+        x = (bcm * f(lr)).astype(np.float32)
+        if rho_t > 5.0:
+            rect = ((rho_t - 4) * (rho_t - 2) * rho_inf / ((rho_inf - 4) * (rho_inf - 2) * rho_t)) ** 0.5
+            s = (_sqrt(v, sqrt) + f(eps)).astype(np.float32)
+            adaptive = ((f(1.0) / s).astype(np.float32) * f(bc2 ** 0.5)).astype(np.float32)
+            x = ((x * adaptive).astype(np.float32) * f(rect)).astype(np.float32)
+        return (p - x).astype(np.float32)
+    if opt == "adadelta":  # adadelta.py:281-302, rho 0.9, eps 1e-6
+        rho, eps = 0.9, 1e-6
+        sq = _fma((f(1 - rho) * g).astype(np.float32), g, (st["square_avg"] * f(rho)).astype(np.float32))
+        std = _sqrt((sq + f(eps)).astype(np.float32), sqrt)
+        delta = _sqrt((st["acc_delta"] + f(eps)).astype(np.float32), sqrt)
+        delta = ((delta / std).astype(np.float32) * g).astype(np.float32)
+        acc = _fma((f(1 - rho) * delta).astype(np.float32), delta, (st["acc_delta"] * f(rho)).astype(np.float32))
+        st["square_avg"], st["acc_delta"] = sq, acc
+        return _fma(delta, f(-lr), p)
+    if opt == "asgd":  # asgd.py:247-275, lambd 1e-4, alpha 0.75, t0 1e6
+        lambd, alpha, t0 = 1e-4, 0.75, 1e6
+        eta = float(st["eta"])
+        p = (p * f(1 - lambd * eta)).astype(np.float32)
+        p = _fma(g, f(-eta), p)
+        if float(st["mu"]) != 1:
+            st["ax"] = (st["ax"] + ((p - st["ax"]).astype(np.float32) * st["mu"]).astype(np.float32)).astype(np.float32)
+        else:
+            st["ax"] = p.copy()
+        st["eta"] = f(lr / ((1 + lambd * lr * step) ** alpha))
+        st["mu"] = f(1 / max(1, step - t0))
+        return p
+    if opt == "rprop":  # rprop.py:257-291, etas (0.5, 1.2), step sizes (1e-6, 50)
+        sgn = _sign((g * st["prev"]).astype(np.float32))
+        sgn = np.where(sgn > 0, f(1.2), np.where(sgn < 0, f(0.5), f(1.0))).astype(np.float32)
+        ss = np.clip((st["step_size"] * sgn).astype(np.float32), f(1e-6), f(50.0)).astype(np.float32)
+        g2 = np.where(sgn == f(0.5), f(0.0), g).astype(np.float32)
+        st["step_size"], st["prev"] = ss, g2
+        return _fma((f(-1.0) * _sign(g2)).astype(np.float32), ss, p)
+    raise ValueError(opt)
+
+
+def fedopt_optrepo_round(opt: str, global_sd: "OrderedDict[str, torch.Tensor]", param_names: Sequence[str],
+                         raw_grad_list, lr: float, state: Dict[str, Dict[str, object]], step: int,
+                         sqrt: str = "torch") -> "OrderedDict[str, torch.Tensor]":
+    """One FedOptAPI round (fedopt_api.py:121-130) with server_optimizer =
+    opt (adamax / nadam / radam / adadelta / asgd / rprop): FedAvg, the
+    optimizer on named parameters (state[k] carries torch's per-parameter
+    state across rounds, step is 1-based), averaged values for buffers."""
+    class _A:
+        federated_optimizer = "FedAvg"
+    avg = agg(_A(), raw_grad_list)
+    out = OrderedDict()
+    for k, t_old in global_sd.items():
+        if k in param_names:
+            if k not in state:
+                state[k] = optrepo_init(opt, t_old.numel(), lr)
+            p = fedopt_step(opt, to_np(t_old).ravel(), to_np(avg[k]).ravel(), state[k], lr, step, sqrt=sqrt)
             out[k] = torch.from_numpy(p).reshape(t_old.shape)
         else:
             out[k] = avg[k].to(t_old.dtype).reshape(t_old.shape)

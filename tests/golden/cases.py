@@ -155,6 +155,29 @@ FEDOPT_RMSPROP_CASES = [
     dict(name="fedopt_rmsprop_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=100, optimizer="rmsprop"),
     dict(name="fedopt_rmsprop_lr1e-3_small", K=5, rounds=3, lr=0.001, model="small", seed=101, optimizer="rmsprop"),
 ]
+# The other elementwise optimizers OptRepo names (optrepo.py:10), through the
+# same FedOptAPI flow (lr only, torch defaults).  RAdam runs 8 rounds so its
+# rectified branch (rho_t > 5, from step 6 with beta2 = 0.999) is covered.
+FEDOPT_OPTREPO_CASES = [
+    dict(name="fedopt_adamax_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=102, optimizer="adamax"),
+    dict(name="fedopt_adamax_lr1_small", K=3, rounds=3, lr=1.0, model="small", seed=103, optimizer="adamax"),
+    dict(name="fedopt_nadam_lr1e-2", K=4, rounds=4, lr=0.01, model="adam", seed=104, optimizer="nadam"),
+    dict(name="fedopt_nadam_lr1_small", K=3, rounds=3, lr=1.0, model="small", seed=105, optimizer="nadam"),
+    dict(name="fedopt_radam_lr1e-2", K=4, rounds=8, lr=0.01, model="adam", seed=106, optimizer="radam"),
+    dict(name="fedopt_radam_lr1_small", K=3, rounds=8, lr=1.0, model="small", seed=107, optimizer="radam"),
+    dict(name="fedopt_adadelta_lr1", K=4, rounds=4, lr=1.0, model="adam", seed=108, optimizer="adadelta"),
+    dict(name="fedopt_adadelta_lr1e-1_small", K=5, rounds=3, lr=0.1, model="small", seed=109, optimizer="adadelta"),
+    dict(name="fedopt_asgd_lr1e-2", K=4, rounds=3, lr=0.01, model="adam", seed=110, optimizer="asgd"),
+    dict(name="fedopt_asgd_lr1_small", K=3, rounds=3, lr=1.0, model="small", seed=111, optimizer="asgd"),
+    dict(name="fedopt_rprop_lr1e-2", K=4, rounds=5, lr=0.01, model="adam", seed=112, optimizer="rprop"),
+    dict(name="fedopt_rprop_lr1e-1_small", K=3, rounds=5, lr=0.1, model="small", seed=113, optimizer="rprop"),
+]
+# MPI FedOptAggregator with index 0's dict object added again at the listed
+# indices (aggregate() reads the running average there, FedOptAggregator.py:93-101)
+FEDOPT_ALIAS_CASES = [
+    dict(name="fedopt_alias_sgd_m09_k4_x2", K=4, rounds=2, lr=1.0, momentum=0.9, seed=114, alias_of_0=[2]),
+    dict(name="fedopt_alias_sgd_m0_k5_x13", K=5, rounds=2, lr=0.5, momentum=0.0, seed=115, alias_of_0=[1, 3]),
+]
 FEDOPT_CASES = [
     dict(name="fedopt_sgd_m09_lr1", K=4, rounds=3, lr=1.0, momentum=0.9, seed=90),
     dict(name="fedopt_sgd_m09_lr1e-3", K=4, rounds=3, lr=0.001, momentum=0.9, seed=91),
@@ -173,6 +196,30 @@ def fake_model_list(k: int):
         d["linear.bias"] = (i + 1) * b
         out.append((i + 10, d))
     return out
+
+
+def _signed_zero_ties(raw):
+    """Columns whose lower median is a zero while the column holds both -0.0
+    and +0.0, in varying input orders: the corner where torch.median's
+    nth_element (comparing with <) returns whichever zero the order puts at
+    the rank.  Column c: a negatives, z zeros of alternating
+    signs (the first one's sign set by c), the rest positives, permuted by a
+    column-seeded shuffle."""
+    K = len(raw)
+    r = (K - 1) // 2
+    for key in raw[0][1]:
+        cols = raw[0][1][key].numel()
+        for c in range(cols):
+            z = 2 + c % 3
+            a = max(0, r - (c // 3) % z)  # the median rank falls on one of the zeros
+            z = min(z, K - a)
+            vals = [-(1.0 + j) for j in range(a)]
+            vals += [(-0.0 if (j + c) % 2 else 0.0) for j in range(z)]
+            vals += [1.0 + j for j in range(K - a - z)]
+            order = torch.randperm(K, generator=torch.Generator().manual_seed(1000 + c)).tolist()
+            for i in range(K):
+                raw[i][1][key].view(-1)[c] = vals[order[i]]
+    return raw
 
 
 def _specials(raw):
@@ -200,6 +247,8 @@ def build_inputs(spec: Dict[str, Any]):
                        sample_nums=spec.get("sample_nums"), int_range=spec.get("int_range"))
     if spec.get("specials"):
         raw = _specials(raw)
+    if spec.get("signed_zero_ties"):
+        raw = _signed_zero_ties(raw)
     if spec.get("triple"):
         second = host_clients(entries, spec["K"], spec["seed"] + 1000)
         raw = [(n, d, second[i][1]) for i, (n, d) in enumerate(raw)]
@@ -331,6 +380,12 @@ for _k in (3, 17, 128, 200):
 for _k in (5, 130):
     _def(f"median_f16_ragged_k{_k}", "wise_median", _k, [[n, s, F16] for n, s, _ in RAGGED_BF16], seed=160 + _k)
 _def("median_bf16_specials_k9", "wise_median", 9, [["x", [64], BF16]], seed=170, specials=True)
+# zero medians with both zero signs in the column: torch's choice of sign is
+# input-order dependent; recorded as the reference's, compared with the zero
+# sign marked as the known divergence (tests/test_oracle_golden.py)
+for _k, _dt in ((3, F32), (4, F32), (5, F32), (8, F32), (9, BF16), (200, BF16)):
+    _def(f"median_signed_zero_k{_k}_{'bf16' if _dt == BF16 else 'f32'}", "wise_median", _k, [["x", [96], _dt]],
+         seed=180 + _k, signed_zero_ties=True)
 _def("trimmed_k10_b01", "trimmed_mean", 10, RESNET_MINI, seed=140, beta=0.1,
      sample_nums=[50, 10, 10, 70, 30, 90, 20, 60, 40, 80])
 _def("trimmed_k10_b02_ties", "trimmed_mean", 10, RAGGED_F32[:4], seed=141, beta=0.2,

@@ -244,6 +244,8 @@ def run_fedopt_case(FedOptAggregator, spec):
     for r in range(spec["rounds"]):
         raw = cases.fedopt_round_inputs(spec, gsd, r)
         meta["rounds"].append({"in_sha256": fingerprint(raw)})
+        for j in spec.get("alias_of_0", ()):  # the same dict object at index j as at index 0
+            raw[j] = (raw[j][0], raw[0][1])
         for i, (n, d) in enumerate(raw):
             agg.add_local_trained_result(i, d, n)
         out = agg.aggregate()
@@ -251,6 +253,13 @@ def run_fedopt_case(FedOptAggregator, spec):
         for k, t in gsd.items():
             arrays[f"r{r}:{k}"] = tensor_bytes(t)
     save(spec["name"], meta, arrays)
+
+
+# torch's per-parameter state recorded per round (scalar tensors included)
+STATE_BUFFERS = {"adagrad": ("sum",), "rmsprop": ("square_avg",), "adamax": ("exp_avg", "exp_inf"),
+                 "nadam": ("exp_avg", "exp_avg_sq", "mu_product"), "radam": ("exp_avg", "exp_avg_sq"),
+                 "adadelta": ("square_avg", "acc_delta"), "asgd": ("ax", "eta", "mu"),
+                 "rprop": ("prev", "step_size")}
 
 
 def import_sp_fedopt():
@@ -330,8 +339,7 @@ def run_fedopt_adam_case(FedOptAPI, spec):
             arrays[f"r{r}:{k}"] = tensor_bytes(t)
         st = api.opt.state_dict()["state"]
         for j, name in enumerate(cases.FEDOPT_PARAMS):
-            for buf in {"adagrad": ("sum",), "rmsprop": ("square_avg",)}.get(A.server_optimizer,
-                                                                              ("exp_avg", "exp_avg_sq")):
+            for buf in STATE_BUFFERS.get(A.server_optimizer, ("exp_avg", "exp_avg_sq")):
                 arrays[f"r{r}:{buf}:{name}"] = tensor_bytes(st[j][buf])
     save(spec["name"], meta, arrays)
 
@@ -401,12 +409,12 @@ def main(only=()):
     for spec in filter(want, cases.CASES + cases.ALIAS_CASES):
         run_agg_case(FedMLAggOperator, spec)
         print("wrote", spec["name"])
-    for spec in filter(want, cases.FEDOPT_CASES):
+    for spec in filter(want, cases.FEDOPT_CASES + cases.FEDOPT_ALIAS_CASES):
         run_fedopt_case(FedOptAggregator, spec)
         print("wrote", spec["name"])
     FedOptAPI = import_sp_fedopt()
     for spec in filter(want, cases.FEDOPT_ADAM_CASES + cases.FEDOPT_ADAGRAD_CASES + cases.FEDOPT_ADAMW_CASES
-                       + cases.FEDOPT_RMSPROP_CASES):
+                       + cases.FEDOPT_RMSPROP_CASES + cases.FEDOPT_OPTREPO_CASES):
         run_fedopt_adam_case(FedOptAPI, spec)
         print("wrote", spec["name"])
     Median, Trimmed = import_defenses()

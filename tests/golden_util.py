@@ -57,11 +57,22 @@ def bits(t: torch.Tensor) -> np.ndarray:
     return t.numpy()
 
 
-def assert_same(actual: torch.Tensor, expected: torch.Tensor, what: str = "") -> None:
+def assert_same(actual: torch.Tensor, expected: torch.Tensor, what: str = "", zero_sign: bool = True) -> int:
     """Bit-identical, except that any NaN matches any NaN (payloads are not part
-    of torch's contract either)."""
+    of torch's contract either).  zero_sign=False also lets -0.0 match +0.0:
+    the known divergence of a zero median whose column holds both zero signs
+    (torch's nth_element returns whichever its input order puts at the rank;
+    DESIGN.md §5b).  Returns the number of elements that differed only in the
+    sign of a zero."""
     assert actual.dtype == expected.dtype, f"{what}: dtype {actual.dtype} != {expected.dtype}"
     assert tuple(actual.shape) == tuple(expected.shape), f"{what}: shape {actual.shape} != {expected.shape}"
+    signs = 0
+    if not zero_sign and actual.is_floating_point():
+        av, ev = actual.detach().cpu().float(), expected.float()
+        both_zero = (av == 0) & (ev == 0)
+        signs = int((both_zero & (torch.signbit(av) != torch.signbit(ev))).sum())
+        actual = torch.where(both_zero.to(actual.device), torch.zeros_like(actual), actual)
+        expected = torch.where(both_zero, torch.zeros_like(expected), expected)
     a, e = bits(actual).ravel(), bits(expected).ravel()
     pos = np.arange(a.size)
     if actual.is_floating_point():
@@ -75,17 +86,22 @@ def assert_same(actual: torch.Tensor, expected: torch.Tensor, what: str = "") ->
         raise AssertionError(f"{what}: {bad.size} of {a.size} elements differ; first at {j}: "
                              f"got {actual.detach().cpu().reshape(-1)[j].item()!r} "
                              f"want {expected.reshape(-1)[j].item()!r}")
+    return signs
 
 
-def assert_groups(actual, meta, arrays, what="") -> None:
+def assert_groups(actual, meta, arrays, what="", zero_sign: bool = True) -> int:
+    """Every output group against the fixture (assert_same); returns the
+    count of zero-sign-only differences (zero_sign=False)."""
     exp = expected_groups(meta, arrays)
     got = list(actual) if isinstance(actual, tuple) else [actual]
     assert bool(meta.get("tuple")) == isinstance(actual, tuple), f"{what}: tuple-ness differs"
     assert len(got) == len(exp)
+    signs = 0
     for g, (gd, ed) in enumerate(zip(got, exp)):
         assert list(gd.keys()) == list(ed.keys()), f"{what}: key order differs"
         for k in ed:
-            assert_same(gd[k], ed[k], f"{what}[{g}][{k}]")
+            signs += assert_same(gd[k], ed[k], f"{what}[{g}][{k}]", zero_sign)
+    return signs
 
 
 def snapshot_third(raw):

@@ -106,3 +106,40 @@ def test_running_sum_detection():
     assert ao._reads_running_sum([buf[0:8], buf[8:16]]) == []  # neighbouring rows of one storage
     with pytest.raises(NotImplementedError):
         ao._reads_running_sum([buf[0:8], buf[4:12]])
+
+
+def test_interleaved_views_that_share_no_element_are_independent():
+    """clients holding different columns of one matrix span
+    overlapping byte extents but share no element; the reference's in-place
+    FedAvg_seq sum into client 0's column handles them, so they are not
+    refused.  A view that does share an element still is."""
+    m = torch.arange(24.0).reshape(4, 6)
+    cols = [m[:, j] for j in range(6)]
+    assert ao._reads_running_sum(cols) == []
+    assert not ao._shares_elements(m[:, 0], m[:, 1])
+    assert ao._shares_elements(m[:, 0], m[0:2, 0])
+    with pytest.raises(NotImplementedError):  # rows 1..3 of column 0: three shared elements
+        ao._reads_running_sum([m[:, 0], m.view(-1)[6:24:6]])
+    every_other = torch.arange(16.0)
+    assert ao._reads_running_sum([every_other[0::2], every_other[1::2]]) == []
+
+
+def test_fedavg_seq_over_column_views_matches_the_reference_loop():
+    """The in-place sum of agg_operator.py:58-63 over column views of one
+    matrix (restated with torch ops): client 0's column receives the sum, the
+    other columns keep their values.  Host dicts go to the GPU, so this runs
+    where a GPU is present."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    m = torch.randn(5, 4)
+    ref = m.clone()
+    acc = ref[:, 0]
+    for j in range(1, 4):
+        acc += ref[:, j]
+    raw = [(1.0, OrderedDict(w=m[:, j])) for j in range(4)]
+
+    class A:
+        federated_optimizer = "FedAvg_seq"
+
+    ao.FedMLAggOperator.agg(A(), raw)
+    assert torch.equal(m, ref)

@@ -115,3 +115,48 @@ def test_set_model_params_into_a_host_model_is_load_state_dict(cuda_device):
         got = net.state_dict()[k]
         assert _bits_equal(got, v), k
         assert got.data_ptr() == before[k], k  # written in place, as load_state_dict does
+
+
+class _Scaled(torch.nn.Linear):
+    """A module that transforms values on load (its own _load_from_state_dict)."""
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        state_dict = {k: (v * 2 if k.startswith(prefix) else v) for k, v in state_dict.items()}
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+
+def test_plain_load_detects_load_overrides_and_hooks():
+    """CPU: the in-place fast path is taken only when load_state_dict would
+    only copy: torch's BatchNorm override is benign, a custom
+    override or a load hook is not."""
+    from fedml_amd.server_aggregator import _plain_load
+
+    assert _plain_load(_Net())
+    assert not _plain_load(torch.nn.Sequential(torch.nn.Linear(2, 2), _Scaled(2, 2)))
+    m = torch.nn.Sequential(torch.nn.Linear(2, 2))
+    m[0].register_load_state_dict_post_hook(lambda module, keys: None)
+    assert not _plain_load(m)
+
+
+@pytest.mark.gpu
+def test_set_model_params_runs_load_overrides_and_bumps_versions(cuda_device):
+    """A model whose module transforms values on load gets what
+    load_state_dict gives it; the in-place fast path bumps the parameters'
+    version counters as load_state_dict's copy_ does."""
+    net = torch.nn.Sequential(torch.nn.Linear(8, 4), _Scaled(4, 2))
+    raw = [(1 + i, OrderedDict((k, torch.randn(v.shape, device=cuda_device)) for k, v in net.state_dict().items()))
+           for i in range(3)]
+    avg = FedMLAggOperator.agg(_A(), raw)
+    ref = torch.nn.Sequential(torch.nn.Linear(8, 4), _Scaled(4, 2))
+    ref.load_state_dict(OrderedDict((k, v.cpu()) for k, v in avg.items()))
+    MI355XServerAggregator(net, _A()).set_model_params(avg)
+    for k, v in ref.state_dict().items():
+        assert _bits_equal(net.state_dict()[k], v), k
+    plain = _Net()
+    raw = [(1 + i, OrderedDict((k, (torch.randn(v.shape) if v.is_floating_point() else v.clone()).to(cuda_device))
+                               for k, v in plain.state_dict().items())) for i in range(2)]
+    avg = FedMLAggOperator.agg(_A(), raw)
+    versions = {k: v._version for k, v in plain.state_dict().items()}
+    MI355XServerAggregator(plain, _A()).set_model_params(avg)
+    for k, v in plain.state_dict().items():
+        assert v._version > versions[k], k

@@ -130,3 +130,38 @@ def test_muldiv_kernel_every_tile_vs_oracle(K, N, dtype, cuda_device):
         exp = orc.mpi_fedavg(host)["x"]
         got = fedavg_mpi_aggregate(raw)["x"]
         gu.assert_same(got.cpu(), exp, f"K={K} N={N} {dtype} offset={offset}")
+
+
+SP_ALIAS = [c["name"] for c in __import__("cases").ALIAS_CASES if c["optimizer"] in ("FedAvg", "FedProx")
+            and not c.get("tensor_alias")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SP_ALIAS)
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_sp_aggregate_alias_matches_reference(name, where, cuda_device):
+    """FedAvgAPI._aggregate (fedavg_api.py:144-159) is the same rebind-then-+=
+    loop as the plugin's FedAvg / FedProx branch, so client 0's dict listed
+    again reads the running sum there too: the FedAvg / FedProx alias
+    fixtures, produced by the reference's own loop, bit for bit through
+    fedavg_aggregate on host and device dicts."""
+    import cases
+
+    meta, arrays = gu.load(name)
+    raw = cases.build_inputs(meta["spec"])
+    if where == "device":
+        raw = _to_device_aliased(raw, cuda_device)
+    first = raw[0][1]
+    res = fedavg_aggregate(raw)
+    assert res is first
+    gu.assert_groups(OrderedDict((k, t.cpu()) for k, t in res.items()), meta, arrays, name)
+
+
+def test_sp_aggregate_alias_known_answer_contract():
+    """Host-side: the alias program is taken (no GPU needed to decide it) --
+    [(1, d), (1, d), (2, e)] reads the running sum at index 1."""
+    from fedml_amd.agg_operator import _reads_running_cell
+
+    d, e = OrderedDict(w=torch.tensor([1.0, 2.0])), OrderedDict(w=torch.tensor([3.0, 4.0]))
+    assert _reads_running_cell([(1, d), (1, d), (2, e)], (1,))
+    assert not _reads_running_cell([(1, d), (1, OrderedDict(d)), (2, e)], (1,))

@@ -39,7 +39,9 @@ def main() -> None:
                          "large-tile table: persistent, streaming, XCD forms)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    lib = nat.lib()
+    from tools import tuning_lib
+
+    lib = tuning_lib.lib()  # the tuning build: the product library has no variant entries
     if a.table == "f32":
         if a.dtype != "f32":
             raise SystemExit("--table f32 takes --dtype f32")
@@ -62,7 +64,7 @@ def main() -> None:
             rc = lib.fedagg_wsum_f32_variant(ptrs.data_ptr(), w.data_ptr(), K, N, outs[v].data_ptr(), v, st)
         else:
             rc = lib.fedagg_wsum_tiny_variant(code, ptrs.data_ptr(), w.data_ptr(), K, N, outs[v].data_ptr(), v, st)
-        nat.check(rc, names[v])
+        tuning_lib.check(rc, names[v])
 
     for v in idx:
         run(v)

@@ -94,13 +94,19 @@ def main():
         wk = ao._walker()
         keys = list(raw[0][1].keys())
         ws = [n / sum(n for n, _ in raw) for n, _ in raw]
-        ao._reduce_host_round(wk, [d for _, d in raw], keys, ws)  # resolve the function pointer once
+        ao._reduce_host_round(wk, [d for _, d in raw], keys, ws)  # resolve the function pointers once
+        ao._reduce_device_round(wk, [d for _, d in draw], keys, ws)
         r = {
             "native_host_round_us": _time(lambda l: wk.host_round([d for _, d in l], keys, ws, ao._HOST_ROUND_FN, 0,
                                                                   ao._HOST_ROUND_MAX_BYTES), host_list, 500, True,
                                           False),
             "agg_host_dicts_us": _time(lambda l: FedMLAggOperator.agg(args, l), host_list, 500, True, False),
-            "agg_device_dicts_us": _time(lambda l: FedMLAggOperator.agg(args, l), dev_list, 200, True),
+            "agg_device_dicts_us": _time(lambda l: FedMLAggOperator.agg(args, l), dev_list, 500, True),
+            # host time of the call alone (the result is stream-ordered, as every device path's)
+            "agg_device_dicts_issue_us": _time(lambda l: FedMLAggOperator.agg(args, l), dev_list, 500, True, False),
+            "native_device_round_us": _time(
+                lambda l: wk.device_round([d for _, d in l], keys, ws, ao._DEVICE_ROUND_FN,
+                                          torch._C._cuda_getCurrentRawStream), dev_list, 500, True),
             "reference_loop_cpu_us": _time(_eager, host_list, 500, False),
             "reference_loop_cpu_1thread_us": _one_thread(lambda: _time(_eager, host_list, 500, False)),
             "reference_loop_gpu_eager_us": _time(_eager, dev_list, 200, True),

@@ -34,7 +34,9 @@ def main() -> None:
     ap.add_argument("--blocks", type=int, nargs="*", default=[32, 64, 128, 256, 512, 768, 1023, 1536])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    lib = nat.lib()
+    from tools import tuning_lib
+
+    lib = tuning_lib.lib()  # the tuning build: the product library has no variant entries
     names = [lib.fedagg_variant_name(v).decode() for v in range(lib.fedagg_num_variants())]
     idx = {n: i for i, n in enumerate(names)}
     st = nat.stream_handle()
@@ -51,7 +53,7 @@ def main() -> None:
             times = {v: [] for v in VARIANTS}
 
             def run(v):
-                nat.check(lib.fedagg_wsum_f32_variant(ptrs.data_ptr(), w.data_ptr(), K, N, outs[v].data_ptr(),
+                tuning_lib.check(lib.fedagg_wsum_f32_variant(ptrs.data_ptr(), w.data_ptr(), K, N, outs[v].data_ptr(),
                                                       idx[v], st), v)
 
             for v in VARIANTS:

@@ -31,7 +31,9 @@ def main() -> None:
     ap.add_argument("--out", default="gpurun_out/tune_tiny.json")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    lib = nat.lib()
+    from tools import tuning_lib
+
+    lib = tuning_lib.lib()  # the tuning build: the product library has no variant entries
     names = [lib.fedagg_tiny_variant_name(v).decode() for v in range(lib.fedagg_num_tiny_variants())]
     st = nat.stream_handle()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,7 +52,7 @@ def main() -> None:
                 times = [[] for _ in names]
 
                 def run(v):
-                    nat.check(lib.fedagg_wsum_tiny_variant(code, ptrs.data_ptr(), w.data_ptr(), K, N,
+                    tuning_lib.check(lib.fedagg_wsum_tiny_variant(code, ptrs.data_ptr(), w.data_ptr(), K, N,
                                                            outs[v].data_ptr(), v, st), names[v])
 
                 for v in range(len(names)):

@@ -33,7 +33,9 @@ def main() -> None:
     a = ap.parse_args()
     K, N = a.K, a.N
     dev = torch.device("cuda:0")
-    lib = nat.lib()
+    from tools import tuning_lib
+
+    lib = tuning_lib.lib()  # the tuning build: the product library has no variant entries
     g = torch.Generator(device=dev).manual_seed(0)
     row = (N + 63) // 64 * 64
     bucket = torch.empty((K, row), dtype=torch.float32, device=dev)
@@ -74,7 +76,7 @@ def main() -> None:
     bytes_alg = (K + 1) * N * 4
 
     def run(v: int) -> None:
-        nat.check(lib.fedagg_wsum_f32_variant(ptrs.data_ptr(), w.data_ptr(), K, N, out.data_ptr(), v, st),
+        tuning_lib.check(lib.fedagg_wsum_f32_variant(ptrs.data_ptr(), w.data_ptr(), K, N, out.data_ptr(), v, st),
                   names[v])
 
     for v in range(nv):  # warm-up + correctness
