@@ -883,8 +883,10 @@ def measure_inprocess(a, config: str, world: int) -> dict:
     doms = [b.dominant_dtype() for b in mb.shards]
 
     def step(evs=None):
-        for s, b in enumerate(mb.shards):  # every device's launches queued before any is waited for
-            b.reduce_into(outs[s], w, events={doms[s]: evs[s]} if evs is not None else None)
+        # every device's launch in one native call (MultiDeviceBucket.reduce_into_all), or shard by shard
+        if not mb.reduce_into_all(outs, w, events=evs):
+            for s, b in enumerate(mb.shards):
+                b.reduce_into(outs[s], w, events={doms[s]: evs[s]} if evs is not None else None)
 
     for _ in range(a.warmup):
         step()

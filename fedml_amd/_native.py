@@ -26,6 +26,21 @@ FEDAGG_ACC_FP32 = 1
 DT_F32, DT_BF16, DT_F16, DT_F64, DT_I64, DT_I32 = 0, 1, 2, 3, 4, 5
 DIST_CHUNK, PAIR_CHUNK = 1024, 256  # FEDAGG_DIST_CHUNK / FEDAGG_PAIR_CHUNK
 WORK_DIST2, WORK_PAIRDIST2, WORK_PAIRGRAM = 0, 1, 2
+# FEDAGG_FEDOPT_*: the launch kinds of fedagg_wsum_fedopt_batch (besides the FEDAGG_OPT_* codes)
+FEDOPT_AVG, FEDOPT_SGD, FEDOPT_ADAM, FEDOPT_ADAMW, FEDOPT_ADAGRAD, FEDOPT_RMSPROP = 0, 16, 17, 18, 19, 20
+
+
+class FedOptLaunch(ctypes.Structure):
+    """fedagg_fedopt_launch (include/fedagg.h), field for field."""
+    _fields_ = [("d_src", ctypes.c_void_p), ("weights", ctypes.c_void_p), ("d_param", ctypes.c_void_p),
+                ("d_state0", ctypes.c_void_p), ("d_state1", ctypes.c_void_p), ("scalars", ctypes.c_void_p),
+                ("stream", ctypes.c_void_p), ("N", ctypes.c_int64), ("alpha", ctypes.c_double),
+                ("lr", ctypes.c_float), ("momentum", ctypes.c_float), ("eps", ctypes.c_float),
+                ("decay", ctypes.c_float), ("K", ctypes.c_int32), ("opt", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("first_step", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("dtype", ctypes.c_int32), ("acc_mode", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 # FEDAGG_OPT_*: the OptRepo optimizers of fedagg_wsum_fedopt_optrepo_f32
 OPT_CODES = {"adamax": 1, "nadam": 2, "radam": 3, "adadelta": 4, "asgd": 5, "rprop": 6}
 
@@ -59,6 +74,7 @@ SIGNATURES = {
                                                       _P]),
     "fedagg_optrepo_scalars": (ctypes.c_int, [_I32, ctypes.c_double, _I64, _P, _P]),
     "fedagg_wsum_fedopt_optrepo_f32": (ctypes.c_int, [_I32, _P, _P, _I32, _I64, _P, _P, _P, _P, _U32, _P]),
+    "fedagg_wsum_fedopt_batch": (ctypes.c_int, [_P, _I32]),
     "fedagg_wsum_rlr_f32": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _P, _U32, _P]),
     "fedagg_median_f32": (ctypes.c_int, [_P, _I32, _I64, _P, _U32, _P]),
     "fedagg_median": (ctypes.c_int, [_I32, _P, _I32, _I64, _P, _U32, _P]),

@@ -2394,6 +2394,80 @@ int fedagg_wsum_fedopt_optrepo_f32(int32_t opt, const float* const* d_src, const
   return check_launch(name);
 }
 
+int fedagg_wsum_fedopt_batch(const fedagg_fedopt_launch* launches, int32_t n) {
+  const char* name = "fedagg_wsum_fedopt_batch";
+  if (n < 0 || (n > 0 && !launches)) return set_error(FEDAGG_EINVAL, std::string(name) + ": bad argument");
+  int cur = -1;
+  if (n && hipGetDevice(&cur) != hipSuccess) return set_error(FEDAGG_EINVAL, std::string(name) + ": no device");
+  int dev = cur, rc = FEDAGG_OK;
+  for (int32_t i = 0; i < n && rc == FEDAGG_OK; ++i) {
+    const fedagg_fedopt_launch& l = launches[i];
+    if (l.device != dev) {
+      if (hipSetDevice(l.device) != hipSuccess) {
+        rc = set_error(FEDAGG_EINVAL, std::string(name) + ": bad device ordinal");
+        break;
+      }
+      dev = l.device;
+    }
+    switch (l.opt) {
+      case FEDAGG_FEDOPT_AVG:
+        switch (l.dtype) {
+          case FEDAGG_DT_F32:
+            rc = fedagg_wsum_f32(l.d_src, l.weights, l.K, l.N, l.d_param, l.flags, l.stream);
+            break;
+          case FEDAGG_DT_BF16:
+            rc = fedagg_wsum_bf16(reinterpret_cast<const uint16_t* const*>(l.d_src), l.weights, l.K, l.N,
+                                  reinterpret_cast<uint16_t*>(l.d_param), l.acc_mode, l.flags, l.stream);
+            break;
+          case FEDAGG_DT_F16:
+            rc = fedagg_wsum_f16(reinterpret_cast<const uint16_t* const*>(l.d_src), l.weights, l.K, l.N,
+                                 reinterpret_cast<uint16_t*>(l.d_param), l.acc_mode, l.flags, l.stream);
+            break;
+          case FEDAGG_DT_F64:
+            rc = fedagg_wsum_f64(reinterpret_cast<const double* const*>(l.d_src),
+                                 reinterpret_cast<const double*>(l.weights), l.K, l.N,
+                                 reinterpret_cast<double*>(l.d_param), l.flags, l.stream);
+            break;
+          case FEDAGG_DT_I64:
+            rc = fedagg_wsum_i64_f32(reinterpret_cast<const int64_t* const*>(l.d_src), l.weights, l.K, l.N,
+                                     l.d_param, l.flags, l.stream);
+            break;
+          default:
+            rc = set_error(FEDAGG_EINVAL, std::string(name) + ": FEDAGG_FEDOPT_AVG dtype");
+        }
+        break;
+      case FEDAGG_FEDOPT_SGD:
+        rc = fedagg_wsum_fedopt_sgd_f32(l.d_src, l.weights, l.K, l.N, l.d_param, l.d_state0, l.lr, l.momentum,
+                                        l.first_step, l.flags, l.stream);
+        break;
+      case FEDAGG_FEDOPT_ADAM:
+        rc = fedagg_wsum_fedopt_adam_f32(l.d_src, l.weights, l.K, l.N, l.d_param, l.d_state0, l.d_state1, l.scalars,
+                                         l.first_step, l.flags, l.stream);
+        break;
+      case FEDAGG_FEDOPT_ADAMW:
+        rc = fedagg_wsum_fedopt_adamw_f32(l.d_src, l.weights, l.K, l.N, l.d_param, l.d_state0, l.d_state1, l.scalars,
+                                          l.decay, l.first_step, l.flags, l.stream);
+        break;
+      case FEDAGG_FEDOPT_ADAGRAD:
+        rc = fedagg_wsum_fedopt_adagrad_f32(l.d_src, l.weights, l.K, l.N, l.d_param, l.d_state0, l.lr, l.eps, l.flags,
+                                            l.stream);
+        break;
+      case FEDAGG_FEDOPT_RMSPROP:
+        rc = fedagg_wsum_fedopt_rmsprop_f32(l.d_src, l.weights, l.K, l.N, l.d_param, l.d_state0, l.lr, l.alpha, l.eps,
+                                            l.flags, l.stream);
+        break;
+      default:
+        if (l.opt >= kOptAdamax && l.opt <= kOptRprop)
+          rc = fedagg_wsum_fedopt_optrepo_f32(l.opt, l.d_src, l.weights, l.K, l.N, l.d_param, l.d_state0, l.d_state1,
+                                              l.scalars, l.flags, l.stream);
+        else
+          rc = set_error(FEDAGG_EINVAL, std::string(name) + ": unknown opt code");
+    }
+  }
+  if (dev != cur) (void)hipSetDevice(cur);
+  return rc;
+}
+
 int fedagg_round_f32(int32_t dtype, const float* d_in, int64_t N, void* d_out, fedagg_stream_t stream) {
   if (N < 0 || (N > 0 && (!d_in || !d_out))) return set_error(FEDAGG_EINVAL, "fedagg_round_f32: bad argument");
   if (dtype != FEDAGG_DT_BF16 && dtype != FEDAGG_DT_F16)

@@ -67,12 +67,23 @@ For a LoRA adapter set (config 5) all keys are parameters: one launch.
 from __future__ import annotations
 
 from collections import OrderedDict
+import ctypes
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
+from . import _native as nat
 from . import kernels as kn
 from .bucket import ClientBucket
+
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream(device: torch.device) -> int:
+    """torch's current stream on `device` as a raw hipStream_t."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(device.index)
+    return torch.cuda.current_stream(device).cuda_stream
 
 # the OptRepo optimizers of fedagg_wsum_fedopt_optrepo_f32 and their
 # per-element state buffers (torch's state names, in the kernel's order)
@@ -251,58 +262,93 @@ class FedOptServer:
         fp32 launches (the benchmark's kernel timing)."""
         ns = [self.sample_num_dict[i] for i in range(self.worker_num)]
         weights = self.bucket.weights(ns)
-        K = self.worker_num
         alias = self._aliases_of_client0()
         self._refs, self._same = {}, set()  # the round's dicts are consumed
         with torch.cuda.device(self.device):
             self.bucket.sync_ingest()
             if alias:
                 return self._aggregate_aliased(ns, weights, alias, events)
-            w32 = kn.weights_for(weights, torch.float32, self.device)  # by value for K <= 256
-            return self._step(self.run_ptrs, w32, K, weights, events)
+            return self._step(self._table(), weights, events)
 
-    def _step(self, run_ptrs, w32, K: int, weights, events, averaged=None) -> "OrderedDict[str, torch.Tensor]":
-        """The fused launches of one round over `run_ptrs` (K sources per run
-        at weights w32); `averaged`, when given, holds the round's average per
-        dtype group for the groups the fused runs do not cover."""
+    # ---- the round's fused launches (fedagg_wsum_fedopt_batch) ---------------
+
+    _OPT_CODE = {"sgd": nat.FEDOPT_SGD, "adam": nat.FEDOPT_ADAM, "adamw": nat.FEDOPT_ADAMW,
+                 "adagrad": nat.FEDOPT_ADAGRAD, "rmsprop": nat.FEDOPT_RMSPROP, **nat.OPT_CODES}
+
+    def _table(self, run_ptrs=None, K: Optional[int] = None):
+        """The round's launch descriptors, one per run of parameter keys (the
+        fused server step) or buffer keys (the plain FedAvg into the global
+        vector), with every field that does not change between rounds filled
+        in.  Cached for the bucket's own rows; `run_ptrs` / `K` build a
+        one-off table over other sources (the aliased round's average)."""
+        cached = run_ptrs is None
+        if cached and getattr(self, "_launches", None) is not None:
+            return self._launches
+        run_ptrs = self.run_ptrs if run_ptrs is None else run_ptrs
+        K = self.worker_num if K is None else K
         f32 = self.global_flat.get(torch.float32)
+        if f32 is None or not self.runs:  # no fp32 keys: nothing fused (the other groups average in _after)
+            tab = (nat.FedOptLaunch * 0)()
+            if cached:
+                self._launches, self._launches_keep = tab, (tab, [])
+            return tab
+        st = [None, None]
+        if self.optimizer == "sgd":
+            st = [self.mom, None]
+        elif self.optimizer in ("adam", "adamw"):
+            st = [self.exp_avg, self.exp_avg_sq]
+        elif self.optimizer in ("adagrad", "rmsprop"):
+            st = [self.state_sum, None]
+        elif self.optimizer in OPTREPO_STATE:
+            names = OPTREPO_STATE[self.optimizer]
+            st = [self.opt_state[names[0]], self.opt_state[names[-1]] if len(names) > 1 else None]
+        tab = (nat.FedOptLaunch * len(self.runs))()
+        for d, (is_param, lo, hi), ptrs in zip(tab, self.runs, run_ptrs):
+            d.d_src = ptrs.data_ptr()
+            d.K, d.N = K, hi - lo
+            d.d_param = f32.data_ptr() + 4 * lo
+            d.opt = self._OPT_CODE[self.optimizer] if is_param else nat.FEDOPT_AVG
+            if is_param:
+                d.d_state0 = st[0].data_ptr() + 4 * lo if st[0] is not None else 0
+                d.d_state1 = st[1].data_ptr() + 4 * lo if st[1] is not None else 0
+            d.device = self.device.index
+            d.lr, d.momentum, d.eps, d.alpha = self.lr, self.momentum, self.eps, self.alpha
+            d.decay = 1 - self.lr * self.weight_decay  # ctypes rounds it to fp32, as torch does
+            ptrs_all = [d.d_param] + ([d.d_state0, d.d_state1] if is_param else [])
+            d.flags = nat.FEDAGG_ALIGNED16 if all((p & 15) == 0 for p in ptrs_all if p) else 0
+        keep = (tab, list(run_ptrs))  # the tables stay alive as long as the descriptors point at them
+        if cached:
+            self._launches = tab
+            self._launches_keep = keep
+        return tab
+
+    def _fill(self, tab, off: int, w32) -> None:
+        """This round's fields of the descriptors tab[off : off + runs]: the
+        weights, the step's scalars, the first-step flag, the stream."""
         step = self.step_count + 1
-        sc = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step) \
-            if self.optimizer in ("adam", "adamw") else None
-        osc = kn.optrepo_scalars(self.optimizer, self.lr, step, self._carry) \
-            if self.optimizer in OPTREPO_STATE else None
-        st0 = self.opt_state.get(OPTREPO_STATE[self.optimizer][0]) if osc is not None else None
-        st1 = self.opt_state.get(OPTREPO_STATE[self.optimizer][-1]) if osc is not None and \
-            len(OPTREPO_STATE[self.optimizer]) > 1 else None
-        if events is not None:
-            events[0].record()
+        scal = None
+        if self.optimizer in ("adam", "adamw"):
+            scal = kn.adam_scalars(self.lr, self.betas[0], self.betas[1], self.eps, step)
+        elif self.optimizer in OPTREPO_STATE:
+            scal = kn.optrepo_scalars(self.optimizer, self.lr, step, self._carry)
+        self._scal = scal  # alive until the launch (host memory the launch reads)
+        host_w = nat.FEDAGG_HOST_WEIGHTS if isinstance(w32, kn.HostWeights) else 0
+        wptr = w32.data_ptr()
+        sptr = ctypes.addressof(scal) if scal is not None else 0
+        stream = _raw_stream(self.device)
         # torch's Adagrad: clr = lr / (1 + (step - 1) * lr_decay), in double
-        clr = self.lr / (1 + (step - 1) * self.lr_decay)
-        for (is_param, lo, hi), d_ptrs in zip(self.runs, run_ptrs):
-            if is_param and osc is not None:
-                kn.wsum_fedopt_optrepo(self.optimizer, d_ptrs, w32, K, hi - lo, f32[lo:hi], st0[lo:hi],
-                                       st1[lo:hi] if st1 is not None else None, osc, True)
-            elif is_param and self.optimizer == "adagrad":
-                kn.wsum_fedopt_adagrad(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], clr, self.eps,
-                                       True)
-            elif is_param and self.optimizer == "rmsprop":
-                kn.wsum_fedopt_rmsprop(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.state_sum[lo:hi], self.lr,
-                                       self.alpha, self.eps, True)
-            elif is_param and self.optimizer == "adamw":
-                kn.wsum_fedopt_adamw(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
-                                     self.exp_avg_sq[lo:hi], sc, 1 - self.lr * self.weight_decay,
-                                     self.first_step, True)
-            elif is_param and sc is not None:
-                kn.wsum_fedopt_adam(d_ptrs, w32, K, hi - lo, f32[lo:hi], self.exp_avg[lo:hi],
-                                    self.exp_avg_sq[lo:hi], sc, self.first_step, True)
-            elif is_param:
-                kn.wsum_fedopt_sgd(d_ptrs, w32, K, hi - lo, f32[lo:hi],
-                                   self.mom[lo:hi] if self.mom is not None else None,
-                                   self.lr, self.momentum, self.first_step, True)
-            else:
-                kn.wsum_ptrs(torch.float32, d_ptrs, w32, K, hi - lo, f32[lo:hi], True)
-        if events is not None:
-            events[1].record()
+        clr = self.lr / (1 + (step - 1) * self.lr_decay) if self.optimizer == "adagrad" else None
+        first = int(self.first_step)
+        for i in range(off, off + len(self.runs)):
+            d = tab[i]
+            d.weights, d.scalars, d.stream, d.first_step = wptr, sptr, stream, first
+            d.flags = (d.flags & nat.FEDAGG_ALIGNED16) | host_w
+            if clr is not None:
+                d.lr = clr
+
+    def _after(self, weights, K: int, averaged=None) -> None:
+        """The rest of a round after the fused launches: the other dtype
+        groups' averages, the integer buffers' truncation, the step count."""
         for dt, g in self.bucket.groups.items():
             if dt == torch.float32 or g.length == 0:
                 continue
@@ -317,6 +363,21 @@ class FedOptServer:
             t.reshape(-1).copy_(self.global_flat[g.dtype][g.offsets[j]:g.offsets[j] + g.numels[j]])
         self.first_step = False
         self.step_count += 1
+
+    def _step(self, tab, weights, events, K: Optional[int] = None, averaged=None
+              ) -> "OrderedDict[str, torch.Tensor]":
+        """One round's fused launches from a descriptor table (one native
+        call, fedagg_wsum_fedopt_batch), then the rest of the round."""
+        K = self.worker_num if K is None else K
+        w32 = kn.weights_for(weights, torch.float32, self.device)  # by value for K <= 256
+        if len(tab):
+            self._fill(tab, 0, w32)
+            if events is not None:
+                events[0].record()
+            nat.check(nat.lib().fedagg_wsum_fedopt_batch(tab, len(tab)), f"fedopt {self.optimizer} launches")
+            if events is not None:
+                events[1].record()
+        self._after(weights, K, averaged)
         return self.get_global_model_params()
 
     def _aggregate_aliased(self, ns, weights, alias: List[int], events) -> "OrderedDict[str, torch.Tensor]":
@@ -346,7 +407,7 @@ class FedOptServer:
         f32 = flat.get(torch.float32)
         run_ptrs = [kn.upload_i64([f32.data_ptr() + lo * 4], self.device) for _, lo, _ in self.runs] if f32 is not None \
             else []
-        out = self._step(run_ptrs, kn.HostWeights([1.0]), 1, [1.0], events, averaged=flat)
+        out = self._step(self._table(run_ptrs, 1), [1.0], events, K=1, averaged=flat)
         torch.cuda.current_stream(self.device).synchronize()  # the one-off tables and the flat average
         return out
 
@@ -541,11 +602,59 @@ class MultiDeviceFedOptServer:
     def aggregate(self, events=None, device_events=None) -> "OrderedDict[str, torch.Tensor]":
         """Every device's launches are enqueued on its own current stream
         (events, if given, around the first device's fp32 launches;
-        device_events[i] around device i's)."""
-        for i, s in enumerate(self.servers):
-            ev = device_events[i] if device_events is not None else (events if i == 0 else None)
-            s.aggregate(events=ev)
+        device_events[i] around device i's).  The fused launches of ALL
+        devices go out in ONE native call (fedagg_wsum_fedopt_batch), so the
+        last device starts one launch after the one before it, not one
+        Python round of FedOptServer.aggregate later."""
+        first = self.servers[0]
+        if any(s._aliases_of_client0() for s in self.servers):  # the aliased round: shard by shard
+            for i, s in enumerate(self.servers):
+                ev = device_events[i] if device_events is not None else (events if i == 0 else None)
+                s.aggregate(events=ev)
+            return self.get_global_model_params()
+        ns = [first.sample_num_dict[i] for i in range(self.worker_num)]
+        weights = first.bucket.weights(ns)
+        tab, offs = self._combined_table()
+        for s, off in zip(self.servers, offs):
+            s._refs, s._same = {}, set()
+            s.bucket.sync_ingest()
+            s._fill(tab, off, kn.weights_for(weights, torch.float32, s.device))
+        evs = device_events if device_events is not None else ([events] + [None] * (len(self.servers) - 1)
+                                                                if events is not None else None)
+        if evs is not None:
+            for s, ev in zip(self.servers, evs):
+                if ev is not None:
+                    ev[0].record(torch.cuda.current_stream(s.device))
+        if len(tab):
+            nat.check(nat.lib().fedagg_wsum_fedopt_batch(tab, len(tab)), f"fedopt {self.optimizer} launches")
+        if evs is not None:
+            for s, ev in zip(self.servers, evs):
+                if ev is not None:
+                    ev[1].record(torch.cuda.current_stream(s.device))
+        for s in self.servers:
+            if s._int_state or any(dt != torch.float32 and g.length for dt, g in s.bucket.groups.items()):
+                with torch.cuda.device(s.device):
+                    s._after(weights, self.worker_num)
+            else:
+                s._after(weights, self.worker_num)
         return self.get_global_model_params()
+
+    def _combined_table(self):
+        """Every device's launch descriptors in one array (built once), and
+        each device's first index in it."""
+        if getattr(self, "_comb", None) is None:
+            tabs = [s._table() for s in self.servers]
+            offs, n = [], 0
+            for t in tabs:
+                offs.append(n)
+                n += len(t)
+            comb = (nat.FedOptLaunch * n)()
+            for t, off in zip(tabs, offs):
+                if len(t):
+                    ctypes.memmove(ctypes.addressof(comb) + off * ctypes.sizeof(nat.FedOptLaunch),
+                                   ctypes.addressof(t), ctypes.sizeof(t))
+            self._comb = (comb, offs)
+        return self._comb
 
     def get_global_model_params(self) -> "OrderedDict[str, torch.Tensor]":
         if self._views is None:

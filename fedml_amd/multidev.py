@@ -43,8 +43,19 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from . import kernels as kn
 from .bucket import ClientBucket, _pad, gather_jobs
 from .layout import INT_DTYPES, numel
+
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream(device: torch.device) -> int:
+    """torch's current stream on `device` as a raw hipStream_t."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(device.index)
+    return torch.cuda.current_stream(device).cuda_stream
+
 
 Entry = Tuple[str, Tuple[int, ...], torch.dtype]
 
@@ -332,13 +343,92 @@ class MultiDeviceBucket:
         if any(n is None for n in ns):
             raise ValueError("sample count missing for some slot")
         w = self.weights(ns)
-        parts = []
+        outs_list = [b.new_outputs() for b in self.shards]
+        if not self.reduce_into_all(outs_list, w, K):
+            for b, outs in zip(self.shards, outs_list):
+                with torch.cuda.device(b.device):
+                    b.reduce_into(outs, w, K)
+        return merge_in_order(self.entries, [b.unflatten(o) for b, o in zip(self.shards, outs_list)])
+
+    def reduce_into_all(self, outs_list: Sequence[Dict[torch.dtype, torch.Tensor]], weights: Sequence[float],
+                        num_clients: Optional[int] = None, events: Optional[Sequence] = None,
+                        slots: Optional[Sequence[int]] = None) -> bool:
+        """Every device's reduction in ONE native call (fedagg_wsum_fedopt_batch
+        with FEDAGG_FEDOPT_AVG launches, each on its device's current stream),
+        so the last device starts one launch after the one before it instead
+        of one Python reduce_into later.  The arithmetic is each shard's
+        reduce_into's (the same kernels, the same bits).  events[s]: optional
+        (start, end) torch.cuda.Events around shard s's launch.  Returns False
+        and launches nothing when a shard needs more than one launch (several
+        dtype groups) or K > 256 (weights not by value); the caller then uses
+        the shards' reduce_into."""
+        K = num_clients if num_clients is not None else (len(slots) if slots is not None else self.capacity)
+        if slots is not None and (len(slots) != K or any(not 0 <= s < self.capacity for s in slots)):
+            raise ValueError("slots: one valid slot per client")
+        if not 1 <= K <= self.capacity and slots is None:
+            raise ValueError(f"num_clients {K} outside [1, {self.capacity}]")
+        if len(weights) != K:
+            raise ValueError("one weight per client")
+        if K > kn.INLINE_MAX_K:
+            return False
+        groups = []
         for b in self.shards:
-            with torch.cuda.device(b.device):
-                outs = b.new_outputs()
-                b.reduce_into(outs, w, K)
-                parts.append(b.unflatten(outs))
-        return merge_in_order(self.entries, parts)
+            live = [(dt, g) for dt, g in b.groups.items() if g.length]
+            if len(live) > 1:
+                return False
+            groups.append(live[0] if live else None)
+        if slots is not None and list(slots) == list(range(K)):
+            slots = None
+        tabs = [b.slot_ptrs(slots) if slots is not None else None for b in self.shards]
+        key = tuple((o[dg[0]].data_ptr() if dg else 0, t[dg[0]].data_ptr() if (dg and t is not None) else 0)
+                    for o, dg, t in zip(outs_list, groups, tabs))
+        cache = getattr(self, "_avg_table", None)
+        if cache is None or cache[0] != key or cache[2] != K:
+            n = sum(1 for dg in groups if dg is not None)
+            tab = (nat.FedOptLaunch * n)()
+            i = 0
+            for b, o, dg, t in zip(self.shards, outs_list, groups, tabs):
+                if dg is None:
+                    continue
+                dt, g = dg
+                d = tab[i]
+                d.d_src = (g.d_ptrs if t is None else t[dt]).data_ptr()
+                d.d_param = o[dt].data_ptr()
+                d.N, d.K, d.opt, d.device = g.length, K, nat.FEDOPT_AVG, b.device.index
+                d.dtype, d.acc_mode = _CODE[dt], b.acc_mode
+                d.flags = nat.FEDAGG_HOST_WEIGHTS | (nat.FEDAGG_ALIGNED16 if (o[dt].data_ptr() & 15) == 0 else 0)
+                i += 1
+            cache = self._avg_table = (key, tab, K)
+        tab = cache[1]
+        w32 = kn.weights_for(weights, torch.float32, self.devices[0])
+        w64 = kn.weights_for(weights, torch.float64, self.devices[0]) if any(
+            dg is not None and dg[0] == torch.float64 for dg in groups) else None
+        i = 0
+        live = []
+        for s, (b, dg) in enumerate(zip(self.shards, groups)):
+            if dg is None:
+                continue
+            b.sync_ingest()
+            stream = _raw_stream(b.device)
+            d = tab[i]
+            d.weights = (w64 if dg[0] == torch.float64 else w32).data_ptr()
+            d.stream = stream
+            live.append((s, b))
+            i += 1
+        if events is not None:
+            for s, b in live:
+                if events[s] is not None:
+                    events[s][0].record(torch.cuda.current_stream(b.device))
+        if len(tab):
+            nat.check(nat.lib().fedagg_wsum_fedopt_batch(tab, len(tab)), "multi-device reduction")
+        if events is not None:
+            for s, b in live:
+                if events[s] is not None:
+                    events[s][1].record(torch.cuda.current_stream(b.device))
+        if slots is not None:  # the slot tables were read on these streams
+            for (s, b), t in zip(live, [tabs[s] for s, _ in live]):
+                t[groups[s][0]].record_stream(torch.cuda.current_stream(b.device))
+        return True
 
     def bind_slot(self, slot: int, state_dict, view) -> None:
         """As ClientBucket.bind_slot: state_dict's values are now ``view``'s
@@ -353,7 +443,10 @@ class MultiDeviceBucket:
         """FedAvg of the given slots on every device (each device's launches
         enqueued before the next device's), results on their keys' devices
         in the model's key order."""
-        return merge_in_order(self.entries, [b.reduce_slots(slots, weights) for b in self.shards])
+        outs_list = [b.new_outputs() for b in self.shards]
+        if not self.reduce_into_all(outs_list, weights, len(slots), slots=slots):
+            return merge_in_order(self.entries, [b.reduce_slots(slots, weights) for b in self.shards])
+        return merge_in_order(self.entries, [b.unflatten(o) for b, o in zip(self.shards, outs_list)])
 
     def reduce_to_host(self, weights: Sequence[float], num_clients: Optional[int] = None,
                        into: Optional[Dict[str, torch.Tensor]] = None, chunks: int = 8

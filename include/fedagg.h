@@ -279,6 +279,48 @@ int fedagg_wsum_fedopt_optrepo_f32(int32_t opt, const float* const* d_src,
                                    float* d_state1, const float* scalars9,
                                    uint32_t flags, fedagg_stream_t stream);
 
+/* Every fused server launch of one FedOpt round in ONE call: the launches of
+ * a server process that drives several GPUs (MultiDeviceFedOptServer: each
+ * GPU its keys, FedOptAggregator.py:81-130 over the whole model), issued in
+ * order, each on its own device and stream (the calling thread's current
+ * device is restored).  A launch is the entry point its `opt` names, with the
+ * descriptor's fields as that entry's arguments:
+ *   FEDAGG_FEDOPT_AVG      the plain FedAvg of `dtype` rows into d_param:
+ *                          fedagg_wsum_f32 / _bf16 / _f16 (acc_mode) / _f64 (double
+ *                          weights) / _i64_f32 (buffer keys of a FedOpt round, and
+ *                          every device's reduction of a one-process multi-GPU round)
+ *   FEDAGG_FEDOPT_SGD      fedagg_wsum_fedopt_sgd_f32 (d_state0 = momentum)
+ *   FEDAGG_FEDOPT_ADAM     fedagg_wsum_fedopt_adam_f32 (scalars = adam scalars6)
+ *   FEDAGG_FEDOPT_ADAMW    fedagg_wsum_fedopt_adamw_f32 (+ decay)
+ *   FEDAGG_FEDOPT_ADAGRAD  fedagg_wsum_fedopt_adagrad_f32 (lr = clr)
+ *   FEDAGG_FEDOPT_RMSPROP  fedagg_wsum_fedopt_rmsprop_f32 (+ alpha)
+ *   FEDAGG_OPT_*           fedagg_wsum_fedopt_optrepo_f32 (scalars = scalars9)
+ * Stops at the first failing launch and returns its code. */
+#define FEDAGG_FEDOPT_AVG 0
+#define FEDAGG_FEDOPT_SGD 16
+#define FEDAGG_FEDOPT_ADAM 17
+#define FEDAGG_FEDOPT_ADAMW 18
+#define FEDAGG_FEDOPT_ADAGRAD 19
+#define FEDAGG_FEDOPT_RMSPROP 20
+typedef struct fedagg_fedopt_launch {
+  const float* const* d_src;  /* device table of K client pointers */
+  const float* weights;       /* device array, or host with FEDAGG_HOST_WEIGHTS */
+  float* d_param;
+  float* d_state0;
+  float* d_state1;
+  const float* scalars;       /* host */
+  fedagg_stream_t stream;
+  int64_t N;
+  double alpha;
+  float lr, momentum, eps, decay;
+  int32_t K, opt, device, first_step;
+  uint32_t flags;
+  int32_t dtype;              /* FEDAGG_FEDOPT_AVG: FEDAGG_DT_* of the rows (0 = fp32) */
+  int32_t acc_mode;           /* FEDAGG_FEDOPT_AVG of bf16 / f16 rows */
+  int32_t reserved;
+} fedagg_fedopt_launch;
+int fedagg_wsum_fedopt_batch(const fedagg_fedopt_launch* launches, int32_t n);
+
 /* ---- Robust aggregation --------------------------------------------------- */
 
 /* Coordinate-wise median over K fp32 clients (the "wise_median" defense,

@@ -154,6 +154,77 @@ int main() {
       ++failures;
     }
   }
+  // ---- a small device round in one launch (fedagg_device_round_f32) ---------
+  {
+    // config 1's shape: 4 clients x {7840 weights, 10 biases} fp32, host
+    // weights, every pointer in the kernel arguments
+    const int KS = 4, T = 2;
+    const int64_t numels[T] = {7840, 10};
+    const int32_t codes[T] = {FEDAGG_DT_F32, FEDAGG_DT_F32};
+    const float ws[KS] = {0.1f, 0.2f, 0.3f, 0.4f};
+    std::vector<std::vector<float>> host(T * KS);
+    std::vector<float*> dsrc(T * KS);
+    for (int t = 0; t < T; ++t)
+      for (int i = 0; i < KS; ++i) {
+        auto& h = host[t * KS + i];
+        h.resize(numels[t]);
+        for (auto& x : h) x = next_f32();
+        HIP_OK(hipMalloc(&dsrc[t * KS + i], numels[t] * 4));
+        HIP_OK(hipMemcpy(dsrc[t * KS + i], h.data(), numels[t] * 4, hipMemcpyHostToDevice));
+      }
+    std::vector<float*> dout(T);
+    for (int t = 0; t < T; ++t) HIP_OK(hipMalloc(&dout[t], numels[t] * 4));
+    int rc = fedagg_device_round_f32(reinterpret_cast<const void* const*>(dsrc.data()), codes, numels, T, KS, ws,
+                                     reinterpret_cast<void* const*>(dout.data()), nullptr);
+    if (rc) {
+      std::printf("fedagg_device_round_f32 rc=%d: %s\n", rc, fedagg_last_error());
+      return 1;
+    }
+    HIP_OK(hipDeviceSynchronize());
+    for (int t = 0; t < T; ++t) {
+      std::vector<float> got(numels[t]), ref(numels[t]);
+      HIP_OK(hipMemcpy(got.data(), dout[t], numels[t] * 4, hipMemcpyDeviceToHost));
+      std::vector<const float*> hp(KS);
+      for (int i = 0; i < KS; ++i) hp[i] = host[t * KS + i].data();
+      oracle_wsum_f32(hp.data(), ws, KS, numels[t], ref.data());
+      if (std::memcmp(got.data(), ref.data(), numels[t] * 4)) {
+        std::printf("device round key %d differs from the oracle\n", t);
+        ++failures;
+      }
+    }
+    // ---- the same clients through a batched launch (fedagg_wsum_fedopt_batch):
+    // FEDAGG_FEDOPT_AVG of key 0 into a parameter buffer equals the plain average
+    float** d_tab;
+    HIP_OK(hipMalloc(&d_tab, KS * sizeof(float*)));
+    HIP_OK(hipMemcpy(d_tab, dsrc.data(), KS * sizeof(float*), hipMemcpyHostToDevice));
+    float* d_param;
+    HIP_OK(hipMalloc(&d_param, numels[0] * 4));
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    fedagg_fedopt_launch l;
+    std::memset(&l, 0, sizeof(l));
+    l.d_src = d_tab;
+    l.weights = ws;
+    l.d_param = d_param;
+    l.N = numels[0];
+    l.K = KS;
+    l.opt = FEDAGG_FEDOPT_AVG;
+    l.device = dev;
+    l.flags = FEDAGG_ALIGNED16 | FEDAGG_HOST_WEIGHTS;
+    rc = fedagg_wsum_fedopt_batch(&l, 1);
+    if (rc) {
+      std::printf("fedagg_wsum_fedopt_batch rc=%d: %s\n", rc, fedagg_last_error());
+      return 1;
+    }
+    HIP_OK(hipDeviceSynchronize());
+    std::vector<float> a(numels[0]), b(numels[0]);
+    HIP_OK(hipMemcpy(a.data(), d_param, numels[0] * 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(b.data(), dout[0], numels[0] * 4, hipMemcpyDeviceToHost));
+    if (std::memcmp(a.data(), b.data(), numels[0] * 4)) {
+      std::printf("batched FedAvg launch differs from the device round\n");
+      ++failures;
+    }
+  }
   // ---- errors are reported, not crashed on ----------------------------------
   if (fedagg_wsum_f32(nullptr, d_w, 0, 10, nullptr, 0, nullptr) != FEDAGG_EINVAL ||
       std::strstr(fedagg_last_error(), "K must be") == nullptr) {

@@ -194,7 +194,8 @@ def test_random_scaffold_mime_round_matches_the_oracle(seed, cuda_device):
         gu.assert_same(a.cpu(), e, f"{what} client-0 tensor {j}")
 
 
-_FEDOPT = [("sgd", 0.0), ("sgd", 0.9), ("adam", 0.0), ("adamw", 0.0), ("adagrad", 0.0), ("rmsprop", 0.0)]
+_FEDOPT = [("sgd", 0.0), ("sgd", 0.9), ("adam", 0.0), ("adamw", 0.0), ("adagrad", 0.0), ("rmsprop", 0.0),
+           ("adamax", 0.0), ("nadam", 0.0), ("radam", 0.0), ("adadelta", 0.0), ("asgd", 0.0), ("rprop", 0.0)]
 
 
 @pytest.mark.parametrize("seed", list(range(_SEED0, _SEED0 + 60 * _SCALE)))
@@ -240,8 +241,10 @@ def test_random_fedopt_rounds_match_the_oracle(seed, cuda_device):
                                         weight_decay=0.01 if opt == "adamw" else 0.0)
         elif opt == "adagrad":
             exp = orc.fedopt_adagrad_round(prev, names, host, lr, state, sqrt="ieee")
-        else:
+        elif opt == "rmsprop":
             exp = orc.fedopt_rmsprop_round(prev, names, host, lr, state, sqrt="ieee")
+        else:
+            exp = orc.fedopt_optrepo_round(opt, prev, names, host, lr, state, r + 1, sqrt="ieee")
         assert list(out) == list(exp), what
         for k in exp:
             gu.assert_same(out[k], exp[k], f"{what} round {r} key {k}")
@@ -256,6 +259,10 @@ def test_random_fedopt_rounds_match_the_oracle(seed, cuda_device):
             elif opt in ("adagrad", "rmsprop"):
                 name = "sum" if opt == "adagrad" else "square_avg"
                 gu.assert_same(st[name][k].cpu().reshape(-1), torch.from_numpy(state[k]), f"{what} {name} {k}")
+            elif opt in orc.OPTREPO_STATE:
+                for name in orc.OPTREPO_STATE[opt]:
+                    gu.assert_same(st[name][k].cpu().reshape(-1), torch.from_numpy(state[k][name]),
+                                   f"{what} {name} {k}")
         prev = out
 
 

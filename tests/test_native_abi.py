@@ -317,3 +317,31 @@ def test_weights_ride_in_pointer_table(K):
     back = packed.view(np.float32)
     assert torch.equal(torch.from_numpy(back[:K].copy()), torch.tensor(ws, dtype=torch.float32))
     assert back.size == K or back[K] == 0.0
+
+
+def test_fedopt_launch_struct_matches_the_header(tmp_path):
+    """fedagg_fedopt_launch: the ctypes mirror (_native.FedOptLaunch) has the
+    C struct's size and field offsets (compiled against include/fedagg.h)."""
+    import ctypes
+    import shutil
+    import subprocess
+
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    fields = [f for f, _ in nat.FedOptLaunch._fields_]
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "fedagg.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(fedagg_fedopt_launch));\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(fedagg_fedopt_launch, {f}));\n' for f in fields) +
+                   "  return 0;\n}\n")
+    exe = tmp_path / "sz"
+    subprocess.run([cc, "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got[0] == ctypes.sizeof(nat.FedOptLaunch)
+    assert got[1:] == [getattr(nat.FedOptLaunch, f).offset for f in fields]
+
+
+def test_fedopt_batch_validation_without_gpu(lib):
+    assert lib.fedagg_wsum_fedopt_batch(None, 0) == 0  # nothing to launch
+    assert lib.fedagg_wsum_fedopt_batch(None, 2) == -1

@@ -21,14 +21,19 @@ def main():
     entries = resnet50()
     K = 128
     out = {}
-    for G in (1, 2, 4, 8):
+    for G, batched in [(g, b) for g in (1, 2, 4, 8) for b in (False, True)]:
         mb = multidev.MultiDeviceBucket(entries, K, [dev] * G)
         outs = [b.new_outputs() for b in mb.shards]
         w = mb.weights([100 + i for i in range(K)])
 
-        def step():
+        def step_each():
             for s, b in enumerate(mb.shards):
                 b.reduce_into(outs[s], w)
+
+        def step_batch():
+            assert mb.reduce_into_all(outs, w)
+
+        step = step_batch if batched else step_each
 
         for _ in range(3):
             step()
@@ -40,10 +45,10 @@ def main():
             issue.append(time.perf_counter() - t0)
             torch.cuda.synchronize()
         issue.sort()
-        out[G] = {"issue_us_median": round(issue[len(issue) // 2] * 1e6, 1),
+        out[f"{G}{' batched' if batched else ''}"] = {"issue_us_median": round(issue[len(issue) // 2] * 1e6, 1),
                   "per_shard_us": round(issue[len(issue) // 2] * 1e6 / G, 1),
                   "launches_per_shard": [sum(1 for g in b.groups.values() if g.length) for b in mb.shards]}
-        print(G, out[G], flush=True)
+        print(G, "batched" if batched else "each", out[f"{G}{' batched' if batched else ''}"], flush=True)
         del mb, outs
         torch.cuda.empty_cache()
     print(json.dumps(out))
