@@ -1976,7 +1976,15 @@ void launch_fused_cfg(const Seg<OpF32>& s, const EPI& epi, const WS& w, int32_t 
 
 template <bool FUSED_CAP, class EPI, class WS>
 void launch_fused(const Seg<OpF32>& s, const EPI& epi, const WS& w, int32_t K, bool aligned, hipStream_t st) {
-  if (blocks_for<OpF32>(s.numel) <= kMidUpToBlocks)
+  const int64_t blocks = blocks_for<OpF32>(s.numel);
+  // A device's shard of a one-process multi-GPU FedOpt round (config 5 over 8
+  // GPUs: 16 keys, 524,288 elements) is 128 mid tiles: half the CUs.  The
+  // plain FedAvg tiers apply (§6a).
+  if (blocks < kSmallBelowBlocks)
+    launch_fused_cfg<FUSED_CAP, SmallCfg>(s, epi, w, K, aligned, st);
+  else if (blocks < kMid2BelowBlocks)
+    launch_fused_cfg<FUSED_CAP, Mid2Cfg>(s, epi, w, K, aligned, st);
+  else if (blocks <= kMidUpToBlocks)
     launch_fused_cfg<FUSED_CAP, MidCfg>(s, epi, w, K, aligned, st);
   else
     launch_fused_cfg<FUSED_CAP, Cfg<OpF32>>(s, epi, w, K, aligned, st);
