@@ -937,9 +937,113 @@ __device__ __forceinline__ uint32_t pk16_count_median(uint32_t (&k)[R]) {
   return lo | l0 | (l1 << 16);
 }
 
-template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256, bool COUNT = false>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
-    const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out) {
+// ---------------------------------------------------------------------------
+// Selection on bit planes (SEL == 2).  Counting with v_sad_u8 costs two
+// instructions per 4 keys per bit; on bit planes a 32-bit register holds one
+// bit of 32 keys, so a most-significant-first radix select costs 4
+// instructions per 32 keys per bit (and, popcount, xor, select):
+//   - the lane's R packed words (client j's key pair: column 0 low, column 1
+//     high) are transposed IN PLACE into planes: word j = 32 g + i holds bit
+//     16 c + b of client 32 g + i's pair; five swap stages exchange register
+//     index bit k with position bit k (i4 <-> c at 16, i3 <-> b3 at 8, whole
+//     bytes: one v_perm_b32 per word; i2, i1, i0 <-> b2, b1, b0 at 4, 2, 1:
+//     a shift and a v_bfi_b32 per word), after which word 32 g + 16 c + b is
+//     plane b of column c for clients 32 g .. 32 g + 31;
+//   - the float -> unsigned order key map (~x for a negative x, x | 0x8000
+//     otherwise) is an xor of every plane with the sign plane, folded into
+//     storing the COMPLEMENTED key planes Z_b (a 1 where the key's bit b is 0);
+//   - per bit, most significant first, per column: c0 = #(active keys whose
+//     bit is 0) summed over the column's P lanes (DPP); the median (rank
+//     KMAX/2 - 1, the padding's fixed slot) has bit 0 if rank < c0 (active &=
+//     Z_b), else bit 1 (rank -= c0, active &= ~Z_b).
+// Per lane at K = 512: 512 transpose + 128 key-map + ~700 select instructions
+// for the two columns' 256 keys, against ~3,600 (2,048 v_sad_u8) above.
+template <int S, int D, int R>
+__device__ __forceinline__ void slice_swap_stage(uint32_t (&w)[R]) {
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (j & D) continue;
+    const uint32_t a = w[j], b = w[j + D];
+    if constexpr (S == 16) {
+      w[j] = __builtin_amdgcn_perm(b, a, 0x05040100u);      // {a.lo, b.lo}
+      w[j + D] = __builtin_amdgcn_perm(b, a, 0x07060302u);  // {a.hi, b.hi}
+    } else if constexpr (S == 8) {
+      w[j] = __builtin_amdgcn_perm(b, a, 0x06020400u);      // {a0, b0, a2, b2}
+      w[j + D] = __builtin_amdgcn_perm(b, a, 0x07030501u);  // {a1, b1, a3, b3}
+    } else {
+      constexpr uint32_t m = S == 4 ? 0x0f0f0f0fu : S == 2 ? 0x33333333u : 0x55555555u;
+      w[j] = (a & m) | ((b << S) & ~m);
+      w[j + D] = ((a >> S) & m) | (b & ~m);
+    }
+  }
+}
+// words 32 g .. 32 g + 31 of w: raw key pairs -> complemented order-key planes
+template <int R>
+__device__ __forceinline__ void pk16_slice_planes_group(uint32_t (&w)[R], int g) {
+  uint32_t (&v)[32] = *reinterpret_cast<uint32_t (*)[32]>(&w[32 * g]);
+  slice_swap_stage<16, 16, 32>(v);
+  slice_swap_stage<8, 8, 32>(v);
+  slice_swap_stage<4, 4, 32>(v);
+  slice_swap_stage<2, 2, 32>(v);
+  slice_swap_stage<1, 1, 32>(v);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const uint32_t ns = ~v[16 * c + 15];  // 1: a non-negative value
+#pragma unroll
+    for (int b = 0; b < 15; ++b) v[16 * c + b] ^= ns;
+    // Z_15 = the sign plane itself
+  }
+}
+template <int P, int R>
+__device__ __forceinline__ uint32_t pk16_slice_select(const uint32_t (&w)[R]);
+// the two columns' lower medians as packed order keys (as pk16_count_median),
+// from this lane's R packed RAW words (column 0 in the low halves); w is
+// overwritten by the planes
+template <int P, int R>
+__device__ __forceinline__ uint32_t pk16_slice_median(uint32_t (&w)[R]) {
+  static_assert(R % 32 == 0, "whole 32-client groups per lane");
+#pragma unroll
+  for (int g = 0; g < R / 32; ++g) pk16_slice_planes_group<R>(w, g);
+  return pk16_slice_select<P, R>(w);
+}
+// the radix select over the planes of pk16_slice_planes_group
+template <int P, int R>
+__device__ __forceinline__ uint32_t pk16_slice_select(const uint32_t (&w)[R]) {
+  constexpr int G = R / 32;
+  uint32_t act[2][G];
+  uint32_t key[2] = {0u, 0u};
+  int rank[2] = {P * R / 2 - 1, P * R / 2 - 1};
+#pragma unroll
+  for (int b = 15; b >= 0; --b) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint32_t t[G];
+      uint32_t n = 0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const uint32_t z = w[32 * g + 16 * c + b];
+        t[g] = b == 15 ? z : (act[c][g] & z);
+        n = __builtin_popcount(t[g]) + n;
+      }
+      const int c0 = lanes_sum<P>(int(n));
+      const bool one = c0 <= rank[c];
+      rank[c] -= one ? c0 : 0;
+      key[c] = 2u * key[c] + (one ? 1u : 0u);
+      if (b > 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint32_t a = b == 15 ? ~0u : act[c][g];
+          act[c][g] = one ? (a ^ t[g]) : t[g];
+        }
+      }
+    }
+  }
+  return key[0] | (key[1] << 16);
+}
+
+template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256, int SEL = 0, int WPE = 2>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void median_pk16_lanes_kernel(
+    const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out, int64_t pair0) {
   static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column pair");
   static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
   constexpr int KMAX = P * R, PAD = 2;
@@ -962,33 +1066,50 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   // TAIL: `pairs` is the index of the pair holding the lone last column.
   // Otherwise a column group past the end recomputes the last pair and does
   // not store (every lane stays active through the DPP exchanges).
-  const int64_t e = TAIL ? pairs : (int64_t(blockIdx.x) * BS + t) / P;
+  const int64_t e = TAIL ? pairs : pair0 + (int64_t(blockIdx.x) * BS + t) / P;
   const uint64_t boff = uint64_t(TAIL || e < pairs ? e : pairs - 1) * 4u;
-  uint32_t raw[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if (j % 16 == 0 && j) __builtin_amdgcn_sched_barrier(0);
+  auto word = [&](int j) -> uint32_t {
     const int q = sub * (R + PAD) + j;
     const uint64_t off = FULL ? boff : (boff & offmask[q]);
     const auto row = reinterpret_cast<const char*>(rows[q]);
     if constexpr (TAIL)
-      raw[j] = uint32_t(*as_global(reinterpret_cast<const uint16_t*>(row + off))) * 0x10001u;
+      return uint32_t(*as_global(reinterpret_cast<const uint16_t*>(row + off))) * 0x10001u;
     else
-      raw[j] = lanes_load(as_global(reinterpret_cast<const uint32_t*>(row + off)));
+      return lanes_load(as_global(reinterpret_cast<const uint32_t*>(row + off)));
+  };
+  uint32_t raw[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (j % 16 == 0 && j) __builtin_amdgcn_sched_barrier(0);
+    raw[j] = word(j);
   }
   __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first test
   uint32_t nanacc = 0;  // per half, max of |x| bits
-#pragma unroll
-  for (int j = 0; j < R; ++j)
+  auto nan_max = [&](uint32_t x) {
     nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
-                                                                     __builtin_bit_cast(ushort2_t, raw[j] & 0x7fff7fffu)));
+                                                                    __builtin_bit_cast(ushort2_t, x & 0x7fff7fffu)));
+  };
+  if constexpr (SEL == 3) {
+    // planes group by group as the group's loads land (the swap stages pair
+    // words inside a 32-word group): the raw words are gone afterwards, so a
+    // wave holding a NaN reloads them below
+#pragma unroll
+    for (int g = 0; g < R / 32; ++g) {
+#pragma unroll
+      for (int j = 32 * g; j < 32 * g + 32; ++j) nan_max(raw[j]);
+      pk16_slice_planes_group<R>(raw, g);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; ++j) nan_max(raw[j]);
+  }
   // first NaN per half in client (= slot) order as (slot << 16 | bits), only
   // in waves holding a NaN column; KMAX << 16: none
   int first_lo = KMAX << 16, first_hi = KMAX << 16;
   if (__ballot((nanacc & 0xffffu) > E::kPosInf || (nanacc >> 16) > E::kPosInf)) {
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {  // predicated, walked backwards: the lowest slot wins
-      const uint32_t x = raw[j];
+      const uint32_t x = SEL == 3 ? word(j) : raw[j];
       const int s = (sub * R + j) << 16;
       if ((x & 0x7fffu) > E::kPosInf) first_lo = s | int(x & 0xffffu);
       if (((x >> 16) & 0x7fffu) > E::kPosInf) first_hi = s | int(x >> 16);
@@ -1000,7 +1121,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
     }
   }
   uint32_t bits;
-  if constexpr (COUNT) {
+  if constexpr (SEL == 3) {
+    bits = pk16_from_ukey(pk16_slice_select<P, R>(raw));
+  } else if constexpr (SEL == 2) {
+    bits = pk16_from_ukey(pk16_slice_median<P, R>(raw));
+  } else if constexpr (SEL == 1) {
 #pragma unroll
     for (int j = 0; j < R; ++j) raw[j] = pk16_ukey(raw[j]);
     bits = pk16_from_ukey(pk16_count_median<P, R>(raw));
@@ -1041,23 +1166,182 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void me
   }
 }
 
-template <int P, int R, class E, int BS = 256, bool COUNT = false>
-int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+template <int P, int R, class E, int BS = 256, int SEL = 0, int WPE = 2>
+int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st,
+                             int64_t pair0 = 0) {
   const int64_t pairs = N / 2;
-  const int64_t grid = (pairs * P + BS - 1) / BS;
+  const int64_t grid = ((pairs - pair0) * P + BS - 1) / BS;
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
-  if (pairs > 0) {
+  if (pairs > pair0) {
     if (K == P * R)
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS, COUNT>), dim3(unsigned(grid)), dim3(BS),
-                         0, st, src, K, pairs, out);
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS, SEL, WPE>), dim3(unsigned(grid)),
+                         dim3(BS), 0, st, src, K, pairs, out, pair0);
     else
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS, COUNT>), dim3(unsigned(grid)), dim3(BS),
-                         0, st, src, K, pairs, out);
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS, SEL, WPE>), dim3(unsigned(grid)),
+                         dim3(BS), 0, st, src, K, pairs, out, pair0);
   }
   if (N & 1)
-    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS, COUNT>), dim3(1), dim3(BS), 0, st, src, K,
-                       pairs, out);
+    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS, SEL, WPE>), dim3(1), dim3(BS), 0, st, src,
+                       K, pairs, out, int64_t(0));
   return check_launch("fedagg_median");
+}
+
+// ---------------------------------------------------------------------------
+// Streamed form of the bit-plane selection (128 < K <= 1024, 16-bit rows).
+// The register kernel above loads a wave's 32 KB, then selects: its waves
+// convoy (they start together, share the SIMD while selecting, and all wait
+// for memory again together), so it runs near the SUM of its memory time and
+// its selection time.  Here persistent blocks stage the NEXT column block in
+// LDS by LDS-DMA (global_load_lds_dwordx4, no registers) while their waves
+// select the current one, so memory and selection overlap by construction.
+//   - A block (4 waves, P lanes per column pair, R words per lane) owns a
+//     column block of 512 / P columns (1024 / P bytes of every row) and walks
+//     the column blocks with a grid stride; wave w selects the 128 / P
+//     columns [w * 128 / P, (w + 1) * 128 / P) of it.
+//   - The block's tile is KMAX = P R rows x 1024 / P bytes = R KB of LDS,
+//     filled by R DMA instructions (R / 4 per wave) of 64 lanes x 16 B, P
+//     whole rows each: full 128-B lines, whatever wave selects them.  Rows at
+//     or above K read a 16-B pad of -inf / +inf (the register kernel's
+//     padding, so the median stays at rank KMAX / 2 - 1).
+//   - Lane (p, s) = (lane / P, lane % P) of wave w takes rows P j + s, j < R,
+//     of its column pair p.  A row's 16-B chunks are stored XOR-swizzled
+//     (chunk c at c ^ swz(row), swz from the row's position among the P rows
+//     one ds_read_b32 covers), so the 64 lanes of a read hit 64 different
+//     banks; the DMA applies the inverse permutation to its SOURCE chunks
+//     (its LDS side is lane-linear).
+//   - Per column block: wait for the own DMA, barrier, read the lane's R
+//     words, barrier, issue the own share of the next column
+//     block's DMA into the same tile, then the NaN scan, the planes, the
+//     radix select (pk16_slice_planes_group / pk16_slice_select) and the store.
+// The columns past the last whole column block (and the odd last column) run
+// through median_pk16_lanes_kernel with a pair offset.
+template <class E>
+__device__ __attribute__((aligned(16))) uint32_t g_median_pad16[2][4] = {
+    {E::kNegInf * 0x10001u, E::kNegInf * 0x10001u, E::kNegInf * 0x10001u, E::kNegInf * 0x10001u},
+    {E::kPosInf * 0x10001u, E::kPosInf * 0x10001u, E::kPosInf * 0x10001u, E::kPosInf * 0x10001u}};
+
+// the 16-B chunk swizzle of tile row r (chunk c is stored at c ^ slice_swz(r))
+template <int P>
+__device__ __forceinline__ constexpr int slice_swz(int r) {
+  constexpr int Q = P < 4 ? P : 4, RPW = P / Q;  // rows per 256-B bank window: RPW
+  return (16 / P) * ((r / RPW) % Q);
+}
+
+template <int P, int R, bool FULL, class E>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 64 ? 2 : 1))) void median_pk16_stream_kernel(
+    const uint16_t* const* __restrict__ src, int K, int64_t nblk, uint16_t* __restrict__ out) {
+  static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2 to 16 lanes per column pair");
+  static_assert(R == 64 || R == 128, "64 or 128 words per lane");
+  constexpr int KMAX = P * R, RB = 1024 / P;  // tile rows, bytes per tile row (the column block's bytes)
+  constexpr int NC = RB / 16;                 // 16-B chunks per tile row = DMA lanes per row
+  constexpr int TILE = KMAX * RB;             // R KB
+  // ONE shared array (a second __shared__ object can make hipcc wait for
+  // every outstanding DMA before each LDS read): the tile, then the row table
+  __shared__ __attribute__((aligned(16))) unsigned char smem[TILE + KMAX * 8];
+  auto rows = reinterpret_cast<const char**>(smem + TILE);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if constexpr (FULL) K = KMAX;
+  const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
+  for (int i = t; i < KMAX; i += 256)
+    rows[i] = (FULL || i < K) ? reinterpret_cast<const char*>(src[i])
+                              : reinterpret_cast<const char*>(g_median_pad16<E>[i - K < below ? 0 : 1]);
+  __syncthreads();
+  // this wave's share of column block b's DMA: instructions i = 4 k + wave,
+  // lane -> tile row P i + lane / NC, stored chunk lane % NC, whose source is
+  // chunk (lane % NC) ^ swz(row) of the row's column block
+  auto dma = [&](int64_t b) {
+#pragma unroll
+    for (int k = 0; k < R / 4; ++k) {
+      const int i = 4 * k + wave;
+      const int r = P * i + lane / NC;
+      const int c = (lane % NC) ^ slice_swz<P>(r);
+      const uint64_t off = uint64_t(b) * RB + uint64_t(c) * 16u;
+      const char* g = (FULL || r < K) ? rows[r] + off : rows[r];
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(g),
+                                       (void __attribute__((address_space(3)))*)(smem + i * 1024), 16, 0, 0);
+    }
+  };
+  const int sub = lane & (P - 1), p = lane / P;
+  // word j of lane (p, sub): tile row P j + sub, chunk wave * 16 / P + p / 4
+  // (stored at chunk ^ swz), dword p % 4; the swizzle depends on sub only
+  const int chunk = (wave * (16 / P) + p / 4) ^ slice_swz<P>(sub);
+  const uint32_t* tw = reinterpret_cast<const uint32_t*>(smem + sub * RB + chunk * 16) + (p & 3);
+  int64_t b = blockIdx.x;
+  if (b < nblk) dma(b);
+  for (; b < nblk; b += gridDim.x) {
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's DMA has landed
+    __builtin_amdgcn_s_barrier();        // ... and every wave's
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t raw[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) raw[j] = tw[256 * j];
+    uint32_t nanacc = 0;  // per half, max of |x| bits
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
+                                                                       __builtin_bit_cast(ushort2_t, raw[j] & 0x7fff7fffu)));
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every word read ...
+    __builtin_amdgcn_s_barrier();        // ... by every wave before the tile is refilled
+    __builtin_amdgcn_sched_barrier(0);
+    if (b + gridDim.x < nblk) dma(b + gridDim.x);
+    // first NaN per half in client order as (client << 16 | bits), only in
+    // waves holding a NaN column; KMAX << 16: none
+    int first_lo = KMAX << 16, first_hi = KMAX << 16;
+    if (__ballot((nanacc & 0xffffu) > E::kPosInf || (nanacc >> 16) > E::kPosInf)) {
+#pragma unroll
+      for (int j = R - 1; j >= 0; --j) {  // predicated, walked backwards: the lowest client wins
+        const uint32_t x = raw[j];
+        const int s = (P * j + sub) << 16;
+        if ((x & 0x7fffu) > E::kPosInf) first_lo = s | int(x & 0xffffu);
+        if (((x >> 16) & 0x7fffu) > E::kPosInf) first_hi = s | int(x >> 16);
+      }
+#pragma unroll
+      for (int m = 1; m < P; m <<= 1) {
+        first_lo = min(first_lo, __shfl_xor(first_lo, m, 64));
+        first_hi = min(first_hi, __shfl_xor(first_hi, m, 64));
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < R / 32; ++g) pk16_slice_planes_group<R>(raw, g);
+    uint32_t bits = pk16_from_ukey(pk16_slice_select<P, R>(raw));
+    if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
+    if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
+    if (sub == 0) {
+      const int64_t e = b * (RB / 4) + wave * (64 / P) + p;  // column pair
+      *reinterpret_cast<uint32_t*>(out + 2 * e) = bits;
+    }
+  }
+}
+
+int device_cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+template <int P, int R, class E>
+int launch_median_pk16_stream(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  constexpr int COLS = 512 / P;  // columns per column block
+  const int64_t nblk = N / COLS;
+  if (nblk > 0) {
+    const int64_t cap = int64_t(device_cu_count()) * (R == 64 ? 2 : 1);  // resident blocks (LDS: R KB each)
+    const int64_t grid = nblk < cap ? nblk : cap;
+    if (K == P * R)
+      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K,
+                         nblk, out);
+    else
+      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K,
+                         nblk, out);
+    if (int rc = check_launch("fedagg_median")) return rc;
+  }
+  // the remaining columns (fewer than one column block) and the odd last one
+  return launch_median_pk16_lanes<P * R / 128, 128, E, 256, 3>(src, K, N, out, st, nblk * (COLS / 2));
 }
 
 // Any number of clients (the path above 1024, where the lane-group sort runs
