@@ -18,17 +18,6 @@
 constexpr int kPk16Mirror = 0;
 // reversed DPP reads issued per batch in lanes4_merge_median
 constexpr int kPk16Batch = 2;
-// Packed 16-bit lane groups (128 < K <= 1024): 1 selects the median by
-// counting (median_pk16_count: byte-wise bisection with v_sad_u8), 0 by the
-// sorting networks and cross-lane merges (the round-3 form, NOTES.md §5b)
-constexpr int kPk16Count = 1;
-// values per lane of the counting kernels (P = KMAX / R lanes per column pair;
-// 64 and 32, i.e. 8 and 16 rows per wave instruction, ran config 4 in 32 and
-// 66 ms against 21 ms at 128: profiles/r04/c/median_ab_variants.json)
-constexpr int kPk16CountR = 128;
-// independent v_sad_u8 accumulator chains per sum (4: 21.3 vs 22.5 ms at
-// config 4's 512 clients, profiles/r04/c/)
-constexpr int kSadChains = 4;
 // Loads of the lane-group kernels: a wave instruction reads 64 B of each of P
 // rows' 128-B lines and the block's next wave reads the other half, so plain
 // loads (0) keep the line in L2 for it; non-temporal ones (1) fetched 1.04-1.5x
@@ -819,36 +808,11 @@ template <class E>
 __device__ uint32_t g_median_pad2[2] = {E::kNegInf * 0x10001u, E::kPosInf * 0x10001u};
 
 // ---------------------------------------------------------------------------
-// Selection by counting (kPk16Count), for the packed lane groups: the
-// sorting networks above spend ~35 half-rate min/max per value at 512
-// clients (VALU-bound at 0.85 of the SIMDs' issue capacity).  Counting needs
-// far fewer operations per value:
-//   - every 16-bit float becomes its UNSIGNED order key (x ^ 0x8000 for a
-//     positive value, ~x for a negative one), so integer order = float order;
-//   - for integer keys x_i and a pivot p, S(p) = sum |x_i - p| is convex and
-//     S(p+1) - S(p) = #(x <= p) - #(x > p) = 2 c(p) - n, so the count c(p) of
-//     keys at or below p comes from two sums of absolute differences;
-//   - v_sad_u8 adds |a_b - p| over the 4 bytes b of a register into an
-//     accumulator: 4 keys per instruction.  So the keys are split into bytes
-//     and selected a byte at a time, most significant first: 8 bisection
-//     steps find the median's high byte h (the smallest h with #(hi <= h) at
-//     least the target rank + 1); then every key is clamped into
-//     [h << 8, h << 8 | 255] (a key below the range counts as low byte 0, one
-//     above as 255 and never counts for a pivot below 255, which is exactly
-//     its order relation to every candidate), and 8 more steps on the clamped
-//     low bytes find l.  The median's key is h << 8 | l, mapped back to the
-//     input's bits.
-// Padding stays the sorting kernels' (±inf slots that put the lower median at
-// slot KMAX/2 - 1 of KMAX), so the target count is KMAX/2 and the test per
-// step is D = S(p+1) - S(p) >= 0, summed over the column's P lanes (DPP adds).
-// Per lane at K = 512 (128 clients x 2 columns): 2 x 2 x 32 v_sad_u8 per step
-// x 16 steps = 2,048, plus 256 byte gathers (v_perm_b32), 256 clamps and the
-// key transform, against ~5,300 half-rate ops for the networks.
-[[maybe_unused]] __device__ __forceinline__ uint32_t pk16_ukey(uint32_t x) {
-  const uint32_t s = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, x) >> short(15));  // 0xffff: negative
-  return x ^ (s | 0x80008000u);
-}
-[[maybe_unused]] __device__ __forceinline__ uint32_t pk16_from_ukey(uint32_t k) {
+// 16-bit order keys: x ^ 0x8000 for a non-negative value, ~x for a negative
+// one, so that integer order is float order (-0 < +0; NaN above +inf or below
+// -inf, a NaN column's result is replaced by its first NaN anyway); the
+// inverse on a packed pair:
+__device__ __forceinline__ uint32_t pk16_from_ukey(uint32_t k) {
   const uint32_t s = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, k) >> short(15));  // 0xffff: positive
   return k ^ (~s | 0x80008000u);
 }
@@ -862,83 +826,8 @@ __device__ __forceinline__ int lanes_sum(int x) {
   if constexpr (P >= 32) x += __shfl_xor(x, 16, 64);
   return x;
 }
-// one byte of the two columns' medians: the smallest v in [0, 255] with
-// #(byte <= v) >= KMAX/2 over the column's P lanes, for column 0 (b0) and 1 (b1)
-template <int P, int NB>
-__device__ __forceinline__ void sad_bisect(const uint32_t (&b0)[NB], const uint32_t (&b1)[NB], uint32_t& v0,
-                                           uint32_t& v1) {
-  v0 = 0;
-  v1 = 0;
-#pragma unroll
-  for (int bit = 7; bit >= 0; --bit) {
-    const uint32_t p0 = (v0 + (1u << bit) - 1u) * 0x01010101u, p1 = (v1 + (1u << bit) - 1u) * 0x01010101u;
-    const uint32_t q0 = p0 + 0x01010101u, q1 = p1 + 0x01010101u;
-    constexpr int C = kSadChains < NB ? kSadChains : NB;
-    uint32_t s0[C], t0[C], s1[C], t1[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) s0[c] = t0[c] = s1[c] = t1[c] = 0;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      s0[j % C] = __builtin_amdgcn_sad_u8(b0[j], p0, s0[j % C]);
-      t0[j % C] = __builtin_amdgcn_sad_u8(b0[j], q0, t0[j % C]);
-      s1[j % C] = __builtin_amdgcn_sad_u8(b1[j], p1, s1[j % C]);
-      t1[j % C] = __builtin_amdgcn_sad_u8(b1[j], q1, t1[j % C]);
-    }
-#pragma unroll
-    for (int c = 1; c < C; ++c) {
-      s0[0] += s0[c];
-      t0[0] += t0[c];
-      s1[0] += s1[c];
-      t1[0] += t1[c];
-    }
-    const int d0 = lanes_sum<P>(int(t0[0]) - int(s0[0]));
-    const int d1 = lanes_sum<P>(int(t1[0]) - int(s1[0]));
-    if (d0 < 0) v0 += 1u << bit;  // fewer than KMAX/2 keys at or below the pivot: the median is above it
-    if (d1 < 0) v1 += 1u << bit;
-  }
-}
-// bytes `lo` and `lo + 2` (the two columns' byte of one key pair) of four
-// registers, gathered per column: c0 = {k0, k1, k2, k3}.byte lo, c1 = .byte lo+2
-template <int LO>
-__device__ __forceinline__ void gather_bytes(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t& c0,
-                                             uint32_t& c1) {
-  constexpr uint32_t sel = LO == 0 ? 0x06040200u : 0x07050301u;  // {S1.b, S1.b+2, S0.b, S0.b+2}
-  const uint32_t t01 = __builtin_amdgcn_perm(k1, k0, sel), t23 = __builtin_amdgcn_perm(k3, k2, sel);
-  c0 = __builtin_amdgcn_perm(t23, t01, 0x06040200u);
-  c1 = __builtin_amdgcn_perm(t23, t01, 0x07050301u);
-}
-// the two columns' lower medians as packed order keys, from this lane's R
-// packed key registers (column 0 in the low halves)
-template <int P, int R>
-__device__ __forceinline__ uint32_t pk16_count_median(uint32_t (&k)[R]) {
-  constexpr int NB = R / 4;
-  uint32_t h0, h1, l0, l1;
-  {
-    uint32_t b0[NB], b1[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) gather_bytes<1>(k[4 * j], k[4 * j + 1], k[4 * j + 2], k[4 * j + 3], b0[j], b1[j]);
-    sad_bisect<P, NB>(b0, b1, h0, h1);
-  }
-  const uint32_t lo = (h0 << 8) | (h1 << 24), hi = lo | 0x00ff00ffu;
-  uint32_t b0[NB], b1[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    uint32_t c[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const ushort2_t x = __builtin_bit_cast(ushort2_t, k[4 * j + u]);
-      c[u] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
-                                              __builtin_elementwise_max(x, __builtin_bit_cast(ushort2_t, lo)),
-                                              __builtin_bit_cast(ushort2_t, hi)));
-    }
-    gather_bytes<0>(c[0], c[1], c[2], c[3], b0[j], b1[j]);
-  }
-  sad_bisect<P, NB>(b0, b1, l0, l1);
-  return lo | l0 | (l1 << 16);
-}
-
 // ---------------------------------------------------------------------------
-// Selection on bit planes (SEL == 2).  Counting with v_sad_u8 costs two
+// Selection on bit planes.  Counting with v_sad_u8 (rounds 4-5) cost two
 // instructions per 4 keys per bit; on bit planes a 32-bit register holds one
 // bit of 32 keys, so a most-significant-first radix select costs 4
 // instructions per 32 keys per bit (and, popcount, xor, select):
@@ -956,8 +845,9 @@ __device__ __forceinline__ uint32_t pk16_count_median(uint32_t (&k)[R]) {
 //     bit is 0) summed over the column's P lanes (DPP); the median (rank
 //     KMAX/2 - 1, the padding's fixed slot) has bit 0 if rank < c0 (active &=
 //     Z_b), else bit 1 (rank -= c0, active &= ~Z_b).
-// Per lane at K = 512: 512 transpose + 128 key-map + ~700 select instructions
-// for the two columns' 256 keys, against ~3,600 (2,048 v_sad_u8) above.
+// Per lane at K = 512 (two columns of 128 clients): 1,024 transpose, 128
+// key-map and ~700 select instructions for 256 keys, where the byte-wise
+// counting took ~3,600 (2,048 v_sad_u8; NOTES.md §5b).
 template <int S, int D, int R>
 __device__ __forceinline__ void slice_swap_stage(uint32_t (&w)[R]) {
 #pragma unroll
@@ -994,18 +884,6 @@ __device__ __forceinline__ void pk16_slice_planes_group(uint32_t (&w)[R], int g)
     // Z_15 = the sign plane itself
   }
 }
-template <int P, int R>
-__device__ __forceinline__ uint32_t pk16_slice_select(const uint32_t (&w)[R]);
-// the two columns' lower medians as packed order keys (as pk16_count_median),
-// from this lane's R packed RAW words (column 0 in the low halves); w is
-// overwritten by the planes
-template <int P, int R>
-__device__ __forceinline__ uint32_t pk16_slice_median(uint32_t (&w)[R]) {
-  static_assert(R % 32 == 0, "whole 32-client groups per lane");
-#pragma unroll
-  for (int g = 0; g < R / 32; ++g) pk16_slice_planes_group<R>(w, g);
-  return pk16_slice_select<P, R>(w);
-}
 // the radix select over the planes of pk16_slice_planes_group
 template <int P, int R>
 __device__ __forceinline__ uint32_t pk16_slice_select(const uint32_t (&w)[R]) {
@@ -1041,8 +919,11 @@ __device__ __forceinline__ uint32_t pk16_slice_select(const uint32_t (&w)[R]) {
   return key[0] | (key[1] << 16);
 }
 
-template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256, int SEL = 0, int WPE = 2>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void median_pk16_lanes_kernel(
+// PLANES: the median by the bit-plane radix select, planes built group by
+// group as the loads land (a wave holding a NaN re-reads its words for the
+// first NaN); otherwise by the sorting networks and cross-lane merges
+template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256, bool PLANES = false>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
     const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out, int64_t pair0) {
   static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column pair");
   static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
@@ -1089,7 +970,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
                                                                     __builtin_bit_cast(ushort2_t, x & 0x7fff7fffu)));
   };
-  if constexpr (SEL == 3) {
+  if constexpr (PLANES) {
     // planes group by group as the group's loads land (the swap stages pair
     // words inside a 32-word group): the raw words are gone afterwards, so a
     // wave holding a NaN reloads them below
@@ -1109,7 +990,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (__ballot((nanacc & 0xffffu) > E::kPosInf || (nanacc >> 16) > E::kPosInf)) {
 #pragma unroll
     for (int j = R - 1; j >= 0; --j) {  // predicated, walked backwards: the lowest slot wins
-      const uint32_t x = SEL == 3 ? word(j) : raw[j];
+      const uint32_t x = PLANES ? word(j) : raw[j];
       const int s = (sub * R + j) << 16;
       if ((x & 0x7fffu) > E::kPosInf) first_lo = s | int(x & 0xffffu);
       if (((x >> 16) & 0x7fffu) > E::kPosInf) first_hi = s | int(x >> 16);
@@ -1121,14 +1002,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
   }
   uint32_t bits;
-  if constexpr (SEL == 3) {
+  if constexpr (PLANES) {
     bits = pk16_from_ukey(pk16_slice_select<P, R>(raw));
-  } else if constexpr (SEL == 2) {
-    bits = pk16_from_ukey(pk16_slice_median<P, R>(raw));
-  } else if constexpr (SEL == 1) {
-#pragma unroll
-    for (int j = 0; j < R; ++j) raw[j] = pk16_ukey(raw[j]);
-    bits = pk16_from_ukey(pk16_count_median<P, R>(raw));
   } else {
   short2_t v[R];
 #pragma unroll
@@ -1166,7 +1041,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
 }
 
-template <int P, int R, class E, int BS = 256, int SEL = 0, int WPE = 2>
+template <int P, int R, class E, int BS = 256, bool PLANES = false>
 int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st,
                              int64_t pair0 = 0) {
   const int64_t pairs = N / 2;
@@ -1174,14 +1049,14 @@ int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint1
   if (grid > 0x7fffffffLL) return set_error(FEDAGG_EINVAL, "fedagg_median: N too large");
   if (pairs > pair0) {
     if (K == P * R)
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS, SEL, WPE>), dim3(unsigned(grid)),
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, true, false, E, BS, PLANES>), dim3(unsigned(grid)),
                          dim3(BS), 0, st, src, K, pairs, out, pair0);
     else
-      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS, SEL, WPE>), dim3(unsigned(grid)),
+      hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, false, E, BS, PLANES>), dim3(unsigned(grid)),
                          dim3(BS), 0, st, src, K, pairs, out, pair0);
   }
   if (N & 1)
-    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS, SEL, WPE>), dim3(1), dim3(BS), 0, st, src,
+    hipLaunchKernelGGL((median_pk16_lanes_kernel<P, R, false, true, E, BS, PLANES>), dim3(1), dim3(BS), 0, st, src,
                        K, pairs, out, int64_t(0));
   return check_launch("fedagg_median");
 }
@@ -1195,12 +1070,17 @@ int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint1
 // LDS by LDS-DMA (global_load_lds_dwordx4, no registers) while their waves
 // select the current one, so memory and selection overlap by construction.
 //   - A block (4 waves, P lanes per column pair, R words per lane) owns a
-//     column block of 512 / P columns (1024 / P bytes of every row) and walks
-//     the column blocks with a grid stride; wave w selects the 128 / P
-//     columns [w * 128 / P, (w + 1) * 128 / P) of it.
+//     column block of 512 / P columns (1024 / P bytes of every row) at a
+//     time, and walks a contiguous range of column blocks (each block its
+//     own share of the row, read front to back: the loads ran at 0.80 of HBM
+//     this way against 0.69 with a grid stride, whose blocks all work in the
+//     same 64-KB window of every row); wave w selects the 128 / P columns
+//     [w * 128 / P, (w + 1) * 128 / P) of it.
 //   - The block's tile is KMAX = P R rows x 1024 / P bytes = R KB of LDS,
 //     filled by R DMA instructions (R / 4 per wave) of 64 lanes x 16 B, P
-//     whole rows each: full 128-B lines, whatever wave selects them.  Rows at
+//     whole rows each: full 128-B lines, whatever wave selects them;
+//     non-temporal, every byte is read once (0.80 against 0.74 of HBM for the
+//     loads alone, NOTES.md §5b).  Rows at
 //     or above K read a 16-B pad of -inf / +inf (the register kernel's
 //     padding, so the median stays at rank KMAX / 2 - 1).
 //   - Lane (p, s) = (lane / P, lane % P) of wave w takes rows P j + s, j < R,
@@ -1219,6 +1099,33 @@ template <class E>
 __device__ __attribute__((aligned(16))) uint32_t g_median_pad16[2][4] = {
     {E::kNegInf * 0x10001u, E::kNegInf * 0x10001u, E::kNegInf * 0x10001u, E::kNegInf * 0x10001u},
     {E::kPosInf * 0x10001u, E::kPosInf * 0x10001u, E::kPosInf * 0x10001u, E::kPosInf * 0x10001u}};
+
+// A wave's share of a streamed tile's LDS-DMA: NK instructions of 64 lanes x
+// 16 B (1 KB each, instruction k at LDS base + 4 k KB: the block's 4 waves
+// interleave), non-temporal.  The per-lane source pointers live in registers
+// and step one column block per next(); pad rows do not step.
+template <int NK>
+struct TileDma {
+  const char* src[NK];
+  uint32_t step[NK];
+  __device__ __forceinline__ void issue(unsigned char* lds) const {
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[k]),
+                                       (void __attribute__((address_space(3)))*)(lds + k * 4096), 16, 0, 2);
+  }
+  __device__ __forceinline__ void next() {
+#pragma unroll
+    for (int k = 0; k < NK; ++k) src[k] += step[k];
+  }
+};
+
+// this block's contiguous range [b, b_end) of the nblk column blocks
+__device__ __forceinline__ void block_range(int64_t nblk, int64_t& b, int64_t& b_end) {
+  const int64_t per = (nblk + gridDim.x - 1) / gridDim.x;
+  b = int64_t(blockIdx.x) * per;
+  b_end = b + per < nblk ? b + per : nblk;
+}
 
 // the 16-B chunk swizzle of tile row r (chunk c is stored at c ^ slice_swz(r))
 template <int P>
@@ -1246,29 +1153,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 64 ? 2
     rows[i] = (FULL || i < K) ? reinterpret_cast<const char*>(src[i])
                               : reinterpret_cast<const char*>(g_median_pad16<E>[i - K < below ? 0 : 1]);
   __syncthreads();
-  // this wave's share of column block b's DMA: instructions i = 4 k + wave,
+  int64_t b, b_end;
+  block_range(nblk, b, b_end);
+  // this wave's share of a column block's DMA: instructions i = 4 k + wave,
   // lane -> tile row P i + lane / NC, stored chunk lane % NC, whose source is
   // chunk (lane % NC) ^ swz(row) of the row's column block
-  auto dma = [&](int64_t b) {
+  unsigned char* const tile_w = smem + __builtin_amdgcn_readfirstlane(wave) * 1024;
+  TileDma<R / 4> dma;
 #pragma unroll
-    for (int k = 0; k < R / 4; ++k) {
-      const int i = 4 * k + wave;
-      const int r = P * i + lane / NC;
-      const int c = (lane % NC) ^ slice_swz<P>(r);
-      const uint64_t off = uint64_t(b) * RB + uint64_t(c) * 16u;
-      const char* g = (FULL || r < K) ? rows[r] + off : rows[r];
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(g),
-                                       (void __attribute__((address_space(3)))*)(smem + i * 1024), 16, 0, 0);
-    }
-  };
+  for (int k = 0; k < R / 4; ++k) {
+    const int r = P * (4 * k + wave) + lane / NC;
+    const int c = (lane % NC) ^ slice_swz<P>(r);
+    const bool real = FULL || r < K;
+    dma.src[k] = real ? rows[r] + (uint64_t(b) * RB + uint64_t(c) * 16u) : rows[r];
+    dma.step[k] = real ? uint32_t(RB) : 0u;
+  }
   const int sub = lane & (P - 1), p = lane / P;
   // word j of lane (p, sub): tile row P j + sub, chunk wave * 16 / P + p / 4
   // (stored at chunk ^ swz), dword p % 4; the swizzle depends on sub only
   const int chunk = (wave * (16 / P) + p / 4) ^ slice_swz<P>(sub);
   const uint32_t* tw = reinterpret_cast<const uint32_t*>(smem + sub * RB + chunk * 16) + (p & 3);
-  int64_t b = blockIdx.x;
-  if (b < nblk) dma(b);
-  for (; b < nblk; b += gridDim.x) {
+  if (b < b_end) dma.issue(tile_w);
+  for (; b < b_end; ++b) {
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's DMA has landed
     __builtin_amdgcn_s_barrier();        // ... and every wave's
     __builtin_amdgcn_sched_barrier(0);
@@ -1283,7 +1189,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 64 ? 2
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every word read ...
     __builtin_amdgcn_s_barrier();        // ... by every wave before the tile is refilled
     __builtin_amdgcn_sched_barrier(0);
-    if (b + gridDim.x < nblk) dma(b + gridDim.x);
+    if (b + 1 < b_end) {
+      dma.next();
+      dma.issue(tile_w);
+    }
     // first NaN per half in client order as (client << 16 | bits), only in
     // waves holding a NaN column; KMAX << 16: none
     int first_lo = KMAX << 16, first_hi = KMAX << 16;
@@ -1313,6 +1222,180 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 64 ? 2
   }
 }
 
+// ---------------------------------------------------------------------------
+// One column per lane (the streamed form for K <= 512).  The pair kernels
+// above give a lane two columns of R clients and spend a v_perm_b32 per word
+// separating the columns (swap stage 16) and, per bit, the P-lane count
+// reduction for two columns.  Here a lane's word j holds ONE column of two
+// clients, 2 (P j + s) in the low half and the next client in the high half,
+// assembled from the LDS tile by two 16-bit reads and a v_perm_b32; the half
+// bit is a client bit, so four swap
+// stages (8, 4, 2, 1) on groups of 16 words make the planes: word 16 g + b is
+// plane b of clients 32 g .. 32 g + 31 of the lane (the lane's client
+// 2 (P (16 g + i) + s) + h at position 2 i + h).  A lane holds 2 R clients of
+// its column, P = KMAX / (2 R) lanes per column.
+//   - Block: 4 waves x 64 / P columns = 256 / P columns = 512 / P bytes of
+//     every row per column block (P = 4: one 128-B line); tile KMAX x 512 / P
+//     bytes = R KB, R DMA instructions of 2 P rows each; a contiguous range
+//     of column blocks per block, as median_pk16_stream_kernel.
+//   - Per lane at K = 512: ~900 VALU instructions for its 128 keys (the pair
+//     form: ~1,500); config 4's median 15.0 ms against 16.7 ms for the pair
+//     form and 21.7 ms for the byte-wise counting (NOTES.md §5b).
+//   - Chunk swizzle: row r's 16-B chunk c is stored at c ^ ((8 / P) * ((r / 2)
+//     % P)), so the P row pairs one read covers land in different banks.
+//   - NaN: found on the raw planes (all exponent planes set and a mantissa
+//     plane set); a wave holding one re-reads its columns from memory for the
+//     first NaN in client order (the tile is being refilled by then).
+template <int P>
+__device__ __forceinline__ constexpr int colswz(int r) {
+  return (8 / P) * ((r / 2) % P);
+}
+
+template <int P, int R, bool FULL, class E>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_colstream_kernel(
+    const uint16_t* const* __restrict__ src, int K, int64_t nblk, uint16_t* __restrict__ out) {
+  static_assert(P == 2 || P == 4, "2 or 4 lanes per column");
+  static_assert(R == 64, "64 words (128 clients) per lane");
+  constexpr int KMAX = 2 * P * R, RB = 512 / P;  // tile rows, bytes per tile row
+  constexpr int NC = RB / 16;                    // 16-B chunks per tile row = DMA lanes per row
+  constexpr int TILE = KMAX * RB;                // R KB
+  constexpr int WB = 128 / P;                    // a wave's bytes of a tile row
+  __shared__ __attribute__((aligned(16))) unsigned char smem[TILE + KMAX * 8];
+  auto rows = reinterpret_cast<const char**>(smem + TILE);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if constexpr (FULL) K = KMAX;
+  const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
+  for (int i = t; i < KMAX; i += 256)
+    rows[i] = (FULL || i < K) ? reinterpret_cast<const char*>(src[i])
+                              : reinterpret_cast<const char*>(g_median_pad16<E>[i - K < below ? 0 : 1]);
+  __syncthreads();
+  int64_t b, b_end;
+  block_range(nblk, b, b_end);
+  // DMA share of this wave: instructions i = 4 k + wave, lane -> tile row
+  // 2 P i + lane / NC, stored chunk lane % NC = source chunk ^ swz(row)
+  unsigned char* const tile_w = smem + __builtin_amdgcn_readfirstlane(wave) * 1024;
+  TileDma<R / 4> dma;
+#pragma unroll
+  for (int k = 0; k < R / 4; ++k) {
+    const int r = 2 * P * (4 * k + wave) + lane / NC;
+    const int c = (lane % NC) ^ colswz<P>(r);
+    const bool real = FULL || r < K;
+    dma.src[k] = real ? rows[r] + (uint64_t(b) * RB + uint64_t(c) * 16u) : rows[r];
+    dma.step[k] = real ? uint32_t(RB) : 0u;
+  }
+  const int sub = lane & (P - 1), p = lane / P;
+  // word j: rows 2 (P j + sub) and + 1, column byte cb = wave * WB + 2 p,
+  // chunk cb / 16 stored at ^ swz (the same for both rows and every j)
+  const int cb = wave * WB + 2 * p;
+  const int pos = (cb / 16) ^ colswz<P>(2 * sub);
+  const uint16_t* tlo = reinterpret_cast<const uint16_t*>(smem + 2 * sub * RB + pos * 16 + (cb & 15));
+  constexpr int JS = P * RB;  // 16-bit elements between words j and j + 1 (2 P rows)
+  if (b < b_end) dma.issue(tile_w);
+  for (; b < b_end; ++b) {
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's DMA has landed
+    __builtin_amdgcn_s_barrier();        // ... and every wave's
+    __builtin_amdgcn_sched_barrier(0);
+    // each word from two 16-bit reads (gfx950's d16 reads, which would merge
+    // the halves in the register file, zero the other half under SRAM ECC:
+    // hipcc merges them with a v_perm_b32 per word)
+    uint32_t w[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      ushort2_t v;
+      v.x = tlo[j * JS];
+      v.y = tlo[j * JS + RB / 2];
+      w[j] = __builtin_bit_cast(uint32_t, v);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every word read ...
+    __builtin_amdgcn_s_barrier();        // ... by every wave before the tile is refilled
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t bcur = b;
+    if (b + 1 < b_end) {
+      dma.next();
+      dma.issue(tile_w);
+    }
+    // planes: four swap stages per 16-word group
+    constexpr int MB = __builtin_ctz(E::kPosInf);  // mantissa bits
+    uint32_t nan = 0;
+#pragma unroll
+    for (int g = 0; g < R / 16; ++g) {
+      uint32_t (&v)[16] = *reinterpret_cast<uint32_t (*)[16]>(&w[16 * g]);
+      slice_swap_stage<8, 8, 16>(v);
+      slice_swap_stage<4, 4, 16>(v);
+      slice_swap_stage<2, 2, 16>(v);
+      slice_swap_stage<1, 1, 16>(v);
+      uint32_t e = v[14], m = v[0];
+#pragma unroll
+      for (int q = MB; q < 14; ++q) e &= v[q];
+#pragma unroll
+      for (int q = 1; q < MB; ++q) m |= v[q];
+      nan |= e & m;
+      const uint32_t ns = ~v[15];  // 1: a non-negative value
+#pragma unroll
+      for (int q = 0; q < 15; ++q) v[q] ^= ns;  // complemented order-key planes; Z_15 = the sign plane
+    }
+    // the select: rank KMAX / 2 - 1 over the column's P lanes
+    constexpr int G = R / 16;
+    uint32_t act[G];
+    uint32_t key = 0;
+    int rank = KMAX / 2 - 1;
+#pragma unroll
+    for (int q = 15; q >= 0; --q) {
+      uint32_t tq[G];
+      uint32_t n = 0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const uint32_t z = w[16 * g + q];
+        tq[g] = q == 15 ? z : (act[g] & z);
+        n = __builtin_popcount(tq[g]) + n;
+      }
+      const int c0 = lanes_sum<P>(int(n));
+      const bool one = c0 <= rank;
+      rank -= one ? c0 : 0;
+      key = 2u * key + (one ? 1u : 0u);
+      if (q > 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint32_t a = q == 15 ? ~0u : act[g];
+          act[g] = one ? (a ^ tq[g]) : tq[g];
+        }
+      }
+    }
+    // order key -> bits (the 16-bit form of pk16_from_ukey)
+    uint32_t bits = (key & 0x8000u) ? (key ^ 0x8000u) : (~key & 0xffffu);
+    if (__ballot(nan != 0)) {
+      // first NaN of the column in client order, from memory
+      int first = KMAX;
+      uint32_t fb = 0;
+      const uint64_t off = uint64_t(bcur) * RB + uint64_t(cb);
+      for (int j = R - 1; j >= 0; --j) {
+#pragma unroll
+        for (int h = 1; h >= 0; --h) {
+          const int r = 2 * (P * j + sub) + h;
+          if (r < K) {
+            const uint32_t x = *as_global(reinterpret_cast<const uint16_t*>(rows[r] + off));
+            if ((x & 0x7fffu) > E::kPosInf) {
+              first = r;
+              fb = x;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int m2 = 1; m2 < P; m2 <<= 1) {
+        const int of = __shfl_xor(first, m2, 64);
+        const uint32_t ob = __shfl_xor(fb, m2, 64);
+        if (of < first) {
+          first = of;
+          fb = ob;
+        }
+      }
+      if (first < KMAX) bits = fb;
+    }
+    if (sub == 0) out[bcur * (RB / 2) + wave * (64 / P) + p] = uint16_t(bits);
+  }
+}
+
 int device_cu_count() {
   static int cus[64] = {0};
   int dev = 0;
@@ -1333,15 +1416,34 @@ int launch_median_pk16_stream(const uint16_t* const* src, int K, int64_t N, uint
     const int64_t cap = int64_t(device_cu_count()) * (R == 64 ? 2 : 1);  // resident blocks (LDS: R KB each)
     const int64_t grid = nblk < cap ? nblk : cap;
     if (K == P * R)
-      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K,
-                         nblk, out);
+      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st,
+                         src, K, nblk, out);
     else
-      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0, st, src, K,
-                         nblk, out);
+      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0,
+                         st, src, K, nblk, out);
     if (int rc = check_launch("fedagg_median")) return rc;
   }
   // the remaining columns (fewer than one column block) and the odd last one
-  return launch_median_pk16_lanes<P * R / 128, 128, E, 256, 3>(src, K, N, out, st, nblk * (COLS / 2));
+  return launch_median_pk16_lanes<P * R / 128, 128, E, 256, true>(src, K, N, out, st, nblk * (COLS / 2));
+}
+
+template <int P, int R, class E>
+int launch_median_pk16_colstream(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  constexpr int COLS = 256 / P;  // columns per column block
+  const int64_t nblk = N / COLS;
+  if (nblk > 0) {
+    const int64_t cap = int64_t(device_cu_count()) * 2;  // resident blocks (LDS: R KB each)
+    const int64_t grid = nblk < cap ? nblk : cap;
+    if (K == 2 * P * R)
+      hipLaunchKernelGGL((median_pk16_colstream_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st,
+                         src, K, nblk, out);
+    else
+      hipLaunchKernelGGL((median_pk16_colstream_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0,
+                         st, src, K, nblk, out);
+    if (int rc = check_launch("fedagg_median")) return rc;
+  }
+  // the remaining columns (fewer than one column block) and the odd last one
+  return launch_median_pk16_lanes<2 * P * R / 128, 128, E, 256, true>(src, K, N, out, st, nblk * (COLS / 2));
 }
 
 // Any number of clients (the path above 1024, where the lane-group sort runs
@@ -1446,15 +1548,11 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
     if constexpr (sizeof(typename E::S) == 2) {
       if (aligned && K <= 4096) {  // two columns per lane on packed int16 keys
-        if constexpr (kPk16Count) {  // selection by counting: R values per lane, 256 / R .. 1024 / R lanes
-          constexpr int RC = kPk16CountR;
-          if (K <= 256) return launch_median_pk16_lanes<256 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
-          if (K <= 512) return launch_median_pk16_lanes<512 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
-          if (K <= 1024) return launch_median_pk16_lanes<1024 / RC, RC, E, 256, true>(d_src, K, N, d_out, st);
-        }
-        if (K <= 256) return launch_median_pk16_lanes<4, 64, E>(d_src, K, N, d_out, st);
-        if (K <= 512) return launch_median_pk16_lanes<4, 128, E>(d_src, K, N, d_out, st);
-        if (K <= 1024) return launch_median_pk16_lanes<8, 128, E>(d_src, K, N, d_out, st);
+        // the bit-plane radix select, streamed through LDS: one column per
+        // lane up to 512 clients, column pairs up to 1024
+        if (K <= 256) return launch_median_pk16_colstream<2, 64, E>(d_src, K, N, d_out, st);
+        if (K <= 512) return launch_median_pk16_colstream<4, 64, E>(d_src, K, N, d_out, st);
+        if (K <= 1024) return launch_median_pk16_stream<8, 128, E>(d_src, K, N, d_out, st);
         if (K <= 2048) return launch_median_pk16_lanes<16, 128, E>(d_src, K, N, d_out, st);
         return launch_median_pk16_lanes<32, 128, E>(d_src, K, N, d_out, st);
       }

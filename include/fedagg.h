@@ -341,10 +341,12 @@ int fedagg_median_f32(const float* const* d_src, int32_t K, int64_t N,
  * d_out of that dtype): a bf16 / f16 model's stack, torch.median over it
  * (torch.cat keeps the 16-bit dtype).  Values are widened to fp32 exactly,
  * selected, and the selected input narrowed back exactly; a NaN column
- * returns a NaN.  With FEDAGG_ALIGNED16 (4-byte aligned rows and output)
- * 16-bit rows up to K = 4096 take the packed kernels instead: two columns per
- * register as order-preserving int16 keys, the same networks on
- * v_pk_min_i16 / v_pk_max_i16. */
+ * returns a NaN.  With FEDAGG_ALIGNED16 (16-byte aligned rows and output)
+ * 16-bit rows up to K = 4096 take the packed kernels instead: up to 128
+ * clients two columns per register as order-preserving int16 keys on the same
+ * networks (v_pk_min_i16 / v_pk_max_i16); 129 to 1024 clients a radix select
+ * on bit planes of the order keys, the rows streamed through LDS by LDS-DMA;
+ * above that sorting networks over lane groups. */
 int fedagg_median(int32_t dtype, const void* const* d_src, int32_t K,
                   int64_t N, void* d_out, uint32_t flags,
                   fedagg_stream_t stream);

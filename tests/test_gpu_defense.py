@@ -210,6 +210,44 @@ def test_median_16bit_rows_vs_oracle(aligned, dtype, K, cuda_device):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K", [129, 256, 300, 512, 513, 1000])
+def test_median_16bit_streamed_many_column_blocks(dtype, K, cuda_device):
+    """The streamed bit-plane kernels (aligned 16-bit rows, 128 < K <= 1024)
+    over far more column blocks than resident blocks, so every block walks a
+    range of them with its next tile's DMA in flight: sampled columns at the
+    range seams, NaN columns (first NaN in client order, payload included) in
+    many column blocks, infinities, -0.0 and the ragged end vs the oracle."""
+    N = 400_003
+    g = torch.Generator(device=cuda_device).manual_seed(K + 11)
+    rows = torch.empty((K, (N + 127) // 128 * 128), dtype=dtype, device=cuda_device)[:, :N]
+    rows.copy_((torch.randint(-300, 300, (K, N), generator=g, device=cuda_device).float() * 0.01).to(dtype))
+    r16 = rows.view(torch.int16)
+    nan = 0x7f80 if dtype == torch.bfloat16 else 0x7c00
+    nan_cols = torch.arange(5, N, 9_973, device=cuda_device)
+    late, early = K - 2, K // 2 + 1
+    r16[late, nan_cols] = nan | 0x11
+    r16[early, nan_cols[::2]] = ((nan | 0x23) | 0x8000) - 0x10000
+    inf_cols = torch.arange(17, N, 7_919, device=cuda_device)
+    rows[: K // 2 + 1, inf_cols] = float("inf")
+    rows[:, inf_cols + 1] = -0.0
+    d_ptrs = kn.upload_i64([rows[i].data_ptr() for i in range(K)], cuda_device)
+    out = torch.empty(N, dtype=dtype, device=cuda_device)
+    dfn.median_rows(d_ptrs, K, N, out, aligned=True)
+    seams = torch.arange(0, N, 64 * ((N // 64 + 511) // 512), device=cuda_device)
+    idx = torch.cat([seams, seams + 1, seams + 63, nan_cols, inf_cols, inf_cols + 1,
+                     torch.arange(N - 300, N, device=cuda_device),
+                     torch.randint(0, N, (8_000,), generator=g, device=cuda_device)]).clamp(max=N - 1).unique()
+    exp = torch.from_numpy(orc.lower_median_cols(rows[:, idx].float().cpu().numpy())).to(dtype)
+    gu.assert_same(out[idx].cpu(), exp, f"median {dtype} K={K} streamed")
+    o16 = out.view(torch.int16)[nan_cols].cpu()
+    want = torch.tensor([((nan | 0x23) | 0x8000) - 0x10000 if i % 2 == 0 else nan | 0x11
+                         for i in range(len(nan_cols))], dtype=torch.int16)
+    assert torch.equal(o16, want)
+    del rows, out
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("K,N", [(256, 1_000), (512, 999), (700, 65), (1024, 1), (2048, 77), (4096, 33)])
 def test_median_16bit_lanes_first_nan_payload(dtype, K, N, cuda_device):
     """The packed lane-group kernel (16-bit rows, 128 < K <= 4096): a NaN

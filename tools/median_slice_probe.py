@@ -1,19 +1,21 @@
-"""The packed 16-bit median's two selections side by side (tool only;
-tests/test_gpu_defense.py is the parity check of what ships).
+"""The packed 16-bit median above 128 clients, as shipped and beside its
+register forms (tool only; tests/test_gpu_defense.py is the parity check).
 
     python tools/median_slice_probe.py [out.json]   # default gpurun_out/median_slice_probe.json
 
-Variants (median_slice_probe.hip: slice_probe_name): SEL 1 counts with
-v_sad_u8 (byte-wise bisection), SEL 2 is the radix select on bit planes
-(median.hip, pk16_slice_median), SEL 3 builds the planes group by group as the
-loads land; at 2 or 3 waves per SIMD.  All run on the same rows and must agree
-bit for bit with variant 1:
+Variants (median_slice_probe.hip: slice_probe_name): 1 the product dispatch
+(LDS-DMA streamed bit-plane select), 2 the register form of the bit-plane
+select, 3 the sorting networks.  All run on the same rows and must agree bit
+for bit with the first variant listed:
   - edge shapes first (K = 129 .. 1024 incl. padding, odd N for the tail
     launch, f16 and bf16, NaN / +-inf / +-0 / denormal columns, all-equal and
-    two-valued columns);
+    two-valued columns), each also against torch.median's value;
   - then the timed shapes, interleaved in one process: 3 warm-ups, then
     PROBE_REPS launches of each (HIP events on the launch stream, median),
-    bf16 K = 512 over config 4's 86,567,656 columns (88.8 GB) last.
+    bf16 K = 512 over config 4's 86,567,656 columns (88.8 GB) last;
+    one_row: every table entry points at row 0 (the selection's cost alone).
+PROBE_VARIANTS picks variants (default 1,2); PROBE_QUICK=1 skips the edge
+shapes and keeps K = 512 over 8M columns, =2 adds config 4's full shape.
 """
 from __future__ import annotations
 
@@ -73,7 +75,7 @@ def main():
     P = ctypes.c_void_p
     lib.slice_probe_launch.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int64, P, P]
     lib.slice_probe_name.restype = ctypes.c_char_p
-    variants = [int(v) for v in os.environ.get("PROBE_VARIANTS", "1,2,3,4,5").split(",")]
+    variants = [int(v) for v in os.environ.get("PROBE_VARIANTS", "1,2").split(",")]
     names = {v: lib.slice_probe_name(v).decode() for v in variants}
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -97,7 +99,7 @@ def main():
             b1 = outs[variants[0]].view(torch.int16)
             diffs = {names[v]: int((b1 != outs[v].view(torch.int16)).sum()) for v in variants[1:]}
             ref = rows[:, :N].float().median(dim=0).values.to(dtype)
-            o2 = outs[variants[-1]]
+            o2 = outs[variants[0]]
             same_val = (ref.view(torch.int16) == o2.view(torch.int16)) | ((ref == 0) & (o2 == 0)) | (
                 ref.isnan() & o2.isnan())
             r = {"dtype": str(dtype)[6:], "K": K, "N": N, "diff_vs_first": diffs,
@@ -113,7 +115,7 @@ def main():
               (torch.bfloat16, 1024, 4_000_000, False), (torch.float16, 512, 8_000_000, False),
               (torch.bfloat16, 512, 8_000_000, True), (torch.bfloat16, 512, 86_567_656, False)]
     if os.environ.get("PROBE_QUICK"):
-        shapes = shapes[1:2] + shapes[4:5]
+        shapes = shapes[1:2] + shapes[4:5] + (shapes[5:6] if os.environ.get("PROBE_QUICK") == "2" else [])
     for dtype, K, N, one_row in shapes:
         f16 = int(dtype == torch.float16)
         # one_row: every table entry points at row 0 (served from the caches): the selection's cost alone
