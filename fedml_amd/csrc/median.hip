@@ -1101,10 +1101,10 @@ __device__ __attribute__((aligned(16))) uint32_t g_median_pad16[2][4] = {
     {E::kPosInf * 0x10001u, E::kPosInf * 0x10001u, E::kPosInf * 0x10001u, E::kPosInf * 0x10001u}};
 
 // A wave's share of a streamed tile's LDS-DMA: NK instructions of 64 lanes x
-// 16 B (1 KB each, instruction k at LDS base + 4 k KB: the block's 4 waves
+// 16 B (1 KB each, instruction k at LDS base + WAVES k KB: the block's waves
 // interleave), non-temporal.  The per-lane source pointers live in registers
 // and step one column block per next(); pad rows do not step.
-template <int NK>
+template <int NK, int WAVES = 4>
 struct TileDma {
   const char* src[NK];
   uint32_t step[NK];
@@ -1112,7 +1112,7 @@ struct TileDma {
 #pragma unroll
     for (int k = 0; k < NK; ++k)
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[k]),
-                                       (void __attribute__((address_space(3)))*)(lds + k * 4096), 16, 0, 2);
+                                       (void __attribute__((address_space(3)))*)(lds + k * WAVES * 1024), 16, 0, 2);
   }
   __device__ __forceinline__ void next() {
 #pragma unroll
@@ -1251,33 +1251,41 @@ __device__ __forceinline__ constexpr int colswz(int r) {
   return (8 / P) * ((r / 2) % P);
 }
 
-template <int P, int R, bool FULL, class E>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_colstream_kernel(
-    const uint16_t* const* __restrict__ src, int K, int64_t nblk, uint16_t* __restrict__ out) {
-  static_assert(P == 2 || P == 4, "2 or 4 lanes per column");
-  static_assert(R == 64, "64 words (128 clients) per lane");
-  constexpr int KMAX = 2 * P * R, RB = 512 / P;  // tile rows, bytes per tile row
+// blocks of the column kernel that fit a CU's 160 KB of LDS
+template <int P, int R, int WAVES>
+constexpr int colstream_blocks_per_cu() {
+  return 163840 / (2 * P * R * WAVES * 128 / P + 2 * P * R * 8);
+}
+template <int P, int R, int WAVES, bool FULL, class E>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(
+    colstream_blocks_per_cu<P, R, WAVES>() * WAVES / 4))) void
+median_pk16_colstream_kernel(const uint16_t* const* __restrict__ src, int K, int64_t nblk,
+                             uint16_t* __restrict__ out) {
+  static_assert(P == 2 || P == 4 || P == 8, "2, 4 or 8 lanes per column");
+  static_assert(R == 32 || R == 64, "32 or 64 words (64 or 128 clients) per lane");
+  constexpr int KMAX = 2 * P * R, WB = 128 / P;  // tile rows, a wave's bytes of a tile row
+  constexpr int RB = WAVES * WB;                 // bytes per tile row (the column block's bytes)
   constexpr int NC = RB / 16;                    // 16-B chunks per tile row = DMA lanes per row
-  constexpr int TILE = KMAX * RB;                // R KB
-  constexpr int WB = 128 / P;                    // a wave's bytes of a tile row
+  constexpr int TILE = KMAX * RB;                // R * WAVES / 4 KB
+  static_assert(8 * (P - 1) / P < NC, "the chunk swizzle stays inside a row");
   __shared__ __attribute__((aligned(16))) unsigned char smem[TILE + KMAX * 8];
   auto rows = reinterpret_cast<const char**>(smem + TILE);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   if constexpr (FULL) K = KMAX;
   const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
-  for (int i = t; i < KMAX; i += 256)
+  for (int i = t; i < KMAX; i += 64 * WAVES)
     rows[i] = (FULL || i < K) ? reinterpret_cast<const char*>(src[i])
                               : reinterpret_cast<const char*>(g_median_pad16<E>[i - K < below ? 0 : 1]);
   __syncthreads();
   int64_t b, b_end;
   block_range(nblk, b, b_end);
-  // DMA share of this wave: instructions i = 4 k + wave, lane -> tile row
-  // 2 P i + lane / NC, stored chunk lane % NC = source chunk ^ swz(row)
+  // DMA share of this wave: instructions i = WAVES k + wave, lane -> tile row
+  // (1024 / RB) i + lane / NC, stored chunk lane % NC = source chunk ^ swz(row)
   unsigned char* const tile_w = smem + __builtin_amdgcn_readfirstlane(wave) * 1024;
-  TileDma<R / 4> dma;
+  TileDma<R / 4, WAVES> dma;
 #pragma unroll
   for (int k = 0; k < R / 4; ++k) {
-    const int r = 2 * P * (4 * k + wave) + lane / NC;
+    const int r = (1024 / RB) * (WAVES * k + wave) + lane / NC;
     const int c = (lane % NC) ^ colswz<P>(r);
     const bool real = FULL || r < K;
     dma.src[k] = real ? rows[r] + (uint64_t(b) * RB + uint64_t(c) * 16u) : rows[r];
@@ -1427,19 +1435,19 @@ int launch_median_pk16_stream(const uint16_t* const* src, int K, int64_t N, uint
   return launch_median_pk16_lanes<P * R / 128, 128, E, 256, true>(src, K, N, out, st, nblk * (COLS / 2));
 }
 
-template <int P, int R, class E>
+template <int P, int R, int WAVES, class E>
 int launch_median_pk16_colstream(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
-  constexpr int COLS = 256 / P;  // columns per column block
+  constexpr int COLS = WAVES * 64 / P;  // columns per column block
   const int64_t nblk = N / COLS;
   if (nblk > 0) {
-    const int64_t cap = int64_t(device_cu_count()) * 2;  // resident blocks (LDS: R KB each)
+    const int64_t cap = int64_t(device_cu_count()) * colstream_blocks_per_cu<P, R, WAVES>();  // resident
     const int64_t grid = nblk < cap ? nblk : cap;
     if (K == 2 * P * R)
-      hipLaunchKernelGGL((median_pk16_colstream_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st,
-                         src, K, nblk, out);
+      hipLaunchKernelGGL((median_pk16_colstream_kernel<P, R, WAVES, true, E>), dim3(unsigned(grid)),
+                         dim3(64 * WAVES), 0, st, src, K, nblk, out);
     else
-      hipLaunchKernelGGL((median_pk16_colstream_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0,
-                         st, src, K, nblk, out);
+      hipLaunchKernelGGL((median_pk16_colstream_kernel<P, R, WAVES, false, E>), dim3(unsigned(grid)),
+                         dim3(64 * WAVES), 0, st, src, K, nblk, out);
     if (int rc = check_launch("fedagg_median")) return rc;
   }
   // the remaining columns (fewer than one column block) and the odd last one
@@ -1550,8 +1558,8 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
       if (aligned && K <= 4096) {  // two columns per lane on packed int16 keys
         // the bit-plane radix select, streamed through LDS: one column per
         // lane up to 512 clients, column pairs up to 1024
-        if (K <= 256) return launch_median_pk16_colstream<2, 64, E>(d_src, K, N, d_out, st);
-        if (K <= 512) return launch_median_pk16_colstream<4, 64, E>(d_src, K, N, d_out, st);
+        if (K <= 256) return launch_median_pk16_colstream<2, 64, 4, E>(d_src, K, N, d_out, st);
+        if (K <= 512) return launch_median_pk16_colstream<4, 64, 4, E>(d_src, K, N, d_out, st);
         if (K <= 1024) return launch_median_pk16_stream<8, 128, E>(d_src, K, N, d_out, st);
         if (K <= 2048) return launch_median_pk16_lanes<16, 128, E>(d_src, K, N, d_out, st);
         return launch_median_pk16_lanes<32, 128, E>(d_src, K, N, d_out, st);

@@ -28,7 +28,10 @@ def test_median_valu_issue_fraction_formula():
         bench.SIMDS * bench.CLOCK_GHZ * 1e9) * 1e3
     # one wave64 half-rate instruction per 4 cycles per SIMD, 1,024 SIMDs at 2.4 GHz
     assert bench.SIMDS == 1024 and bench.VALU_HALF_RATE_CYCLES == 4
-    assert 15.0 < issue_ms < 30.0  # config 4 at 512 clients: ~5,300 instructions x 2.7M waves
+    # config 4 at 512 clients, the streamed bit-plane select (round 6): ~2.45M instructions per
+    # persistent wave x 1,026 waves = ~4.1 ms of issue in a ~15-ms kernel (the counting kernel
+    # before it: 3,619 x 2.7M waves = 16.3 ms in 21.3)
+    assert 3.0 < issue_ms < 8.0
 
 
 def test_traffic_table_keys():

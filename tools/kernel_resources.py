@@ -65,7 +65,10 @@ def kernels(co: bytes):
     for k, d in zip(out, names):
         d = d.replace("(anonymous namespace)::", "")
         k["kernel"] = re.sub(r"\(.*$", "", d).replace("void ", "")
-        regs = int(k["vgpr_count"] or 0) + int(k["agpr_count"] or 0)
+        # gfx950's metadata .vgpr_count is the unified file's count (arch VGPRs
+        # rounded up, then the AGPRs): 423 for 256 arch + 167 AGPRs
+        v, a = int(k["vgpr_count"] or 0), int(k["agpr_count"] or 0)
+        regs = v if v > 256 or a == 0 else (v + 3) // 4 * 4 + a
         regs = (regs + 7) // 8 * 8
         k["occupancy"] = min(8, 512 // max(regs, 1))
     return out

@@ -2,7 +2,8 @@
 // median above 128 clients (K <= 1024) as fedagg_median dispatches it (the
 // LDS-DMA streamed bit-plane kernels, median.hip) beside the register form of
 // the same selection (median_pk16_lanes_kernel<PLANES>) and the sorting
-// networks (median_pk16_lanes_kernel, K > 1024 in the product), timed and
+// networks (median_pk16_lanes_kernel, K > 1024 in the product) and the column
+// kernel at 32 words per lane in 8-wave blocks (4 waves per SIMD), timed and
 // compared bit for bit by tools/median_slice_probe.py.  The forms measured
 // and dropped in round 6 (byte-wise counting, the per-wave and grid-stride
 // streams, R = 64 pair tiles) are in NOTES.md §5b with their numbers.
@@ -19,19 +20,26 @@ int probe_lanes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hip
   return 1;
 }
 template <class E>
+int probe_col32(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  if (K <= 256) return launch_median_pk16_colstream<4, 32, 8, E>(src, K, N, out, st);
+  if (K <= 512) return launch_median_pk16_colstream<8, 32, 8, E>(src, K, N, out, st);
+  return median_dispatch<E>(src, K, N, out, true, st);
+}
+template <class E>
 int probe_variant(int v, const uint16_t* const* s, int K, int64_t N, uint16_t* o, hipStream_t st) {
   switch (v) {
     case 1: return median_dispatch<E>(s, K, N, o, true, st);
     case 2: return probe_lanes<true, E>(s, K, N, o, st);
     case 3: return probe_lanes<false, E>(s, K, N, o, st);
+    case 4: return probe_col32<E>(s, K, N, o, st);
   }
   return 1;
 }
 }  // namespace
 
 extern "C" const char* slice_probe_name(int v) {
-  static const char* n[] = {"", "shipped", "planes_regs", "networks_regs"};
-  return (v >= 1 && v <= 3) ? n[v] : "";
+  static const char* n[] = {"", "shipped", "planes_regs", "networks_regs", "col_r32_w8"};
+  return (v >= 1 && v <= 4) ? n[v] : "";
 }
 
 // v: variant (slice_probe_name); f16: 0 bf16 rows, 1 f16 rows

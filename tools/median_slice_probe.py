@@ -5,7 +5,8 @@ register forms (tool only; tests/test_gpu_defense.py is the parity check).
 
 Variants (median_slice_probe.hip: slice_probe_name): 1 the product dispatch
 (LDS-DMA streamed bit-plane select), 2 the register form of the bit-plane
-select, 3 the sorting networks.  All run on the same rows and must agree bit
+select, 3 the sorting networks, 4 the column kernel at 32 words per lane in
+8-wave blocks.  All run on the same rows and must agree bit
 for bit with the first variant listed:
   - edge shapes first (K = 129 .. 1024 incl. padding, odd N for the tail
     launch, f16 and bf16, NaN / +-inf / +-0 / denormal columns, all-equal and
