@@ -636,6 +636,8 @@ def median_kernel_name(K: int, dt) -> str:
     (median_dispatch in csrc/median.hip)."""
     name = str(dt).replace("torch.", "")
     packed = dt in (torch.bfloat16, torch.float16)
+    if packed and 96 < K <= 128:  # bit-plane select, one lane per column pair
+        return f"median_pk16_lanes_kernel<1, 128, planes> ({name})"
     if K <= 128:
         kmax = next(m for m in ((32, 64, 96, 128) if packed else (8, 16, 24, 32, 48, 64, 96, 128)) if K <= m)
         return f"median_{'pk16_' if packed else ''}kernel<{kmax}> ({name})"

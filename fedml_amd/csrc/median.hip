@@ -819,7 +819,7 @@ __device__ __forceinline__ uint32_t pk16_from_ukey(uint32_t k) {
 // sum of x over the P adjacent lanes of a column group (every lane gets it)
 template <int P>
 __device__ __forceinline__ int lanes_sum(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, dpp_xor_ctrl<1>(), 0xf, 0xf, false);
+  if constexpr (P >= 2) x += __builtin_amdgcn_update_dpp(0, x, dpp_xor_ctrl<1>(), 0xf, 0xf, false);
   if constexpr (P >= 4) x += __builtin_amdgcn_update_dpp(0, x, dpp_xor_ctrl<2>(), 0xf, 0xf, false);
   if constexpr (P >= 8) x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xf, 0xf, false);  // row_half_mirror: quads
   if constexpr (P >= 16) x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xf, 0xf, false);  // row_mirror: halves
@@ -925,7 +925,8 @@ __device__ __forceinline__ uint32_t pk16_slice_select(const uint32_t (&w)[R]) {
 template <int P, int R, bool FULL, bool TAIL, class E, int BS = 256, bool PLANES = false>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(2))) void median_pk16_lanes_kernel(
     const uint16_t* const* __restrict__ src, int K, int64_t pairs, uint16_t* __restrict__ out, int64_t pair0) {
-  static_assert(P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "2 to 32 lanes per column pair");
+  static_assert((PLANES && P == 1) || P == 2 || P == 4 || P == 8 || P == 16 || P == 32,
+                "2 to 32 lanes per column pair (1 for the bit-plane select)");
   static_assert(R == 32 || R == 64 || R == 128, "32, 64 or 128 values per lane");
   constexpr int KMAX = P * R, PAD = 2;
   __shared__ const uint16_t* rows[KMAX + PAD * P];
@@ -1580,7 +1581,11 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
       if (K <= 32) return launch_median_pk16<32, E>(d_src, K, N, d_out, st);
       if (K <= 64) return launch_median_pk16<64, E>(d_src, K, N, d_out, st);
       if (K <= 96) return launch_median_pk16<96, E>(d_src, K, N, d_out, st);
-      return launch_median_pk16<128, E>(d_src, K, N, d_out, st);
+      // 97..128: the bit-plane select, one lane per column pair holding all
+      // 128 slots (the 128-slot network padded K = 100 to 0.42 ms per 8M
+      // columns against 0.33; 3.79 vs 3.70 ms at config 4's 128 clients;
+      // below 97 the networks' smaller tiers win: NOTES.md §5b, round 6)
+      return launch_median_pk16_lanes<1, 128, E, 256, true>(d_src, K, N, d_out, st);
     }
   }
   if (K <= 8) return launch_median<8, E>(d_src, K, N, d_out, st);

@@ -248,7 +248,8 @@ def test_median_16bit_streamed_many_column_blocks(dtype, K, cuda_device):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K,N", [(256, 1_000), (512, 999), (700, 65), (1024, 1), (2048, 77), (4096, 33)])
+@pytest.mark.parametrize("K,N", [(100, 1_001), (128, 998), (256, 1_000), (512, 999), (700, 65), (1024, 1),
+                                 (2048, 77), (4096, 33)])
 def test_median_16bit_lanes_first_nan_payload(dtype, K, N, cuda_device):
     """The packed lane-group kernel (16-bit rows, 128 < K <= 4096): a NaN
     column returns ITS FIRST NaN in client order, payload included, per half of

@@ -25,6 +25,19 @@ int probe_col32(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hip
   if (K <= 512) return launch_median_pk16_colstream<8, 32, 8, E>(src, K, N, out, st);
   return median_dispatch<E>(src, K, N, out, true, st);
 }
+// K <= 128: one lane per column pair holding all 128 clients, bit planes
+template <class E>
+int probe_k128_planes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  if (K <= 128) return launch_median_pk16_lanes<1, 128, E, 256, true>(src, K, N, out, st);
+  return median_dispatch<E>(src, K, N, out, true, st);
+}
+template <class E>
+int probe_small_planes(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  if (K <= 32) return launch_median_pk16_lanes<1, 32, E, 256, true>(src, K, N, out, st);
+  if (K <= 64) return launch_median_pk16_lanes<1, 64, E, 256, true>(src, K, N, out, st);
+  if (K <= 128) return launch_median_pk16_lanes<1, 128, E, 256, true>(src, K, N, out, st);
+  return median_dispatch<E>(src, K, N, out, true, st);
+}
 template <class E>
 int probe_variant(int v, const uint16_t* const* s, int K, int64_t N, uint16_t* o, hipStream_t st) {
   switch (v) {
@@ -32,14 +45,17 @@ int probe_variant(int v, const uint16_t* const* s, int K, int64_t N, uint16_t* o
     case 2: return probe_lanes<true, E>(s, K, N, o, st);
     case 3: return probe_lanes<false, E>(s, K, N, o, st);
     case 4: return probe_col32<E>(s, K, N, o, st);
+    case 5: return probe_k128_planes<E>(s, K, N, o, st);
+    case 6: return probe_small_planes<E>(s, K, N, o, st);
   }
   return 1;
 }
 }  // namespace
 
 extern "C" const char* slice_probe_name(int v) {
-  static const char* n[] = {"", "shipped", "planes_regs", "networks_regs", "col_r32_w8"};
-  return (v >= 1 && v <= 4) ? n[v] : "";
+  static const char* n[] = {"", "shipped", "planes_regs", "networks_regs", "col_r32_w8", "k128_planes",
+                           "small_planes"};
+  return (v >= 1 && v <= 6) ? n[v] : "";
 }
 
 // v: variant (slice_probe_name); f16: 0 bf16 rows, 1 f16 rows

@@ -89,7 +89,8 @@ def main():
     # edge shapes: bit-exact agreement, and torch.median's value on every column (sign of a zero aside)
     for dtype in (() if os.environ.get("PROBE_QUICK") else (torch.bfloat16, torch.float16)):
         f16 = int(dtype == torch.float16)
-        for K, N in ((129, 5001), (200, 4096), (256, 4097), (300, 3333), (511, 4096), (512, 4099), (513, 2049),
+        for K, N in (((1, 999), (2, 1000), (5, 1001), (31, 3000), (33, 3001), (64, 2048), (65, 2049), (100, 4097),
+                      (127, 2049), (128, 4098)) if os.environ.get("PROBE_SMALLK") else ()) + ((129, 5001), (200, 4096), (256, 4097), (300, 3333), (511, 4096), (512, 4099), (513, 2049),
                      (700, 4097), (1024, 4096)):
             rows = rows_for(K, N, dtype, dev, seed=K + 17 * f16, specials=True)
             tab = kn.upload_i64([rows[i].data_ptr() for i in range(K)], dev)
@@ -115,7 +116,11 @@ def main():
     shapes = [(torch.bfloat16, 256, 8_000_000, False), (torch.bfloat16, 512, 8_000_000, False),
               (torch.bfloat16, 1024, 4_000_000, False), (torch.float16, 512, 8_000_000, False),
               (torch.bfloat16, 512, 8_000_000, True), (torch.bfloat16, 512, 86_567_656, False)]
-    if os.environ.get("PROBE_QUICK"):
+    if os.environ.get("PROBE_SMALLK"):
+        shapes = [(torch.bfloat16, k, 8_000_000, False) for k in (16, 32, 48, 64, 96, 100, 128)]
+        shapes += [(torch.bfloat16, 128, 8_000_000, True), (torch.bfloat16, 64, 86_567_656, False),
+                   (torch.bfloat16, 128, 86_567_656, False)]
+    elif os.environ.get("PROBE_QUICK"):
         shapes = shapes[1:2] + shapes[4:5] + (shapes[5:6] if os.environ.get("PROBE_QUICK") == "2" else [])
     for dtype, K, N, one_row in shapes:
         f16 = int(dtype == torch.float16)
