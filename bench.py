@@ -643,10 +643,9 @@ def median_kernel_name(K: int, dt) -> str:
         return f"median_{'pk16_' if packed else ''}kernel<{kmax}> ({name})"
     if K > 4096 or (not packed and 2048 < K <= 2560):
         return f"median_radix_stream_kernel ({name})"
-    if packed and K <= 512:  # streamed bit-plane select, one column per lane (+ the register form for the tail)
-        return f"median_pk16_colstream_kernel<{2 if K <= 256 else 4}, 64> ({name})"
-    if packed and K <= 1024:  # streamed bit-plane select, column pairs
-        return f"median_pk16_stream_kernel<8, 128> ({name})"
+    if packed and K <= 1024:  # streamed bit-plane select, one column per lane (+ the register form for the tail)
+        p, w = (2, 4) if K <= 256 else (4, 4) if K <= 512 else (8, 8)
+        return f"median_pk16_colstream_kernel<{p}, 64, {w}> ({name})"
     p, r = (4, 64) if K <= 256 else (4, 128) if K <= 512 else (8, 128) if K <= 1024 else \
         (16, 128) if K <= 2048 else (32, 128)
     return f"median_{'pk16_' if packed else ''}lanes_kernel<{p}, {r}> ({name})"

@@ -1069,31 +1069,22 @@ int launch_median_pk16_lanes(const uint16_t* const* src, int K, int64_t N, uint1
 // for memory again together), so it runs near the SUM of its memory time and
 // its selection time.  Here persistent blocks stage the NEXT column block in
 // LDS by LDS-DMA (global_load_lds_dwordx4, no registers) while their waves
-// select the current one, so memory and selection overlap by construction.
-//   - A block (4 waves, P lanes per column pair, R words per lane) owns a
-//     column block of 512 / P columns (1024 / P bytes of every row) at a
-//     time, and walks a contiguous range of column blocks (each block its
-//     own share of the row, read front to back: the loads ran at 0.80 of HBM
-//     this way against 0.69 with a grid stride, whose blocks all work in the
-//     same 64-KB window of every row); wave w selects the 128 / P columns
-//     [w * 128 / P, (w + 1) * 128 / P) of it.
-//   - The block's tile is KMAX = P R rows x 1024 / P bytes = R KB of LDS,
-//     filled by R DMA instructions (R / 4 per wave) of 64 lanes x 16 B, P
-//     whole rows each: full 128-B lines, whatever wave selects them;
-//     non-temporal, every byte is read once (0.80 against 0.74 of HBM for the
-//     loads alone, NOTES.md §5b).  Rows at
-//     or above K read a 16-B pad of -inf / +inf (the register kernel's
-//     padding, so the median stays at rank KMAX / 2 - 1).
-//   - Lane (p, s) = (lane / P, lane % P) of wave w takes rows P j + s, j < R,
-//     of its column pair p.  A row's 16-B chunks are stored XOR-swizzled
-//     (chunk c at c ^ swz(row), swz from the row's position among the P rows
-//     one ds_read_b32 covers), so the 64 lanes of a read hit 64 different
-//     banks; the DMA applies the inverse permutation to its SOURCE chunks
-//     (its LDS side is lane-linear).
-//   - Per column block: wait for the own DMA, barrier, read the lane's R
-//     words, barrier, issue the own share of the next column
-//     block's DMA into the same tile, then the NaN scan, the planes, the
-//     radix select (pk16_slice_planes_group / pk16_slice_select) and the store.
+// select the current one:
+//   - each block walks a contiguous range of column blocks (its own share of
+//     every row, read front to back: the loads ran at 0.80 of HBM this way
+//     against 0.69 with a grid stride, whose blocks all work in the same
+//     64-KB window of every row);
+//   - the tile's DMA instructions read whole 128-B lines of the rows,
+//     non-temporal (every byte is read once: 0.80 against 0.74 of HBM for
+//     the loads alone, NOTES.md §5b); rows at or above K read a 16-B pad of
+//     -inf / +inf (the register kernel's padding, so the median stays at rank
+//     KMAX / 2 - 1);
+//   - a row's 16-B chunks are stored XOR-swizzled so that the 64 lanes of a
+//     ds_read hit 64 banks; the DMA applies the inverse permutation to its
+//     SOURCE chunks (its LDS side is lane-linear);
+//   - per column block: wait for the own DMA, barrier, read the lane's
+//     words, barrier, issue the own share of the next column block's DMA into
+//     the same tile, then the planes, the radix select and the store.
 // The columns past the last whole column block (and the odd last column) run
 // through median_pk16_lanes_kernel with a pair offset.
 template <class E>
@@ -1128,106 +1119,12 @@ __device__ __forceinline__ void block_range(int64_t nblk, int64_t& b, int64_t& b
   b_end = b + per < nblk ? b + per : nblk;
 }
 
-// the 16-B chunk swizzle of tile row r (chunk c is stored at c ^ slice_swz(r))
-template <int P>
-__device__ __forceinline__ constexpr int slice_swz(int r) {
-  constexpr int Q = P < 4 ? P : 4, RPW = P / Q;  // rows per 256-B bank window: RPW
-  return (16 / P) * ((r / RPW) % Q);
-}
-
-template <int P, int R, bool FULL, class E>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 64 ? 2 : 1))) void median_pk16_stream_kernel(
-    const uint16_t* const* __restrict__ src, int K, int64_t nblk, uint16_t* __restrict__ out) {
-  static_assert(P == 2 || P == 4 || P == 8 || P == 16, "2 to 16 lanes per column pair");
-  static_assert(R == 64 || R == 128, "64 or 128 words per lane");
-  constexpr int KMAX = P * R, RB = 1024 / P;  // tile rows, bytes per tile row (the column block's bytes)
-  constexpr int NC = RB / 16;                 // 16-B chunks per tile row = DMA lanes per row
-  constexpr int TILE = KMAX * RB;             // R KB
-  // ONE shared array (a second __shared__ object can make hipcc wait for
-  // every outstanding DMA before each LDS read): the tile, then the row table
-  __shared__ __attribute__((aligned(16))) unsigned char smem[TILE + KMAX * 8];
-  auto rows = reinterpret_cast<const char**>(smem + TILE);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  if constexpr (FULL) K = KMAX;
-  const int below = KMAX / 2 - 1 - (K - 1) / 2;  // -inf pads; the rest of the padding is +inf
-  for (int i = t; i < KMAX; i += 256)
-    rows[i] = (FULL || i < K) ? reinterpret_cast<const char*>(src[i])
-                              : reinterpret_cast<const char*>(g_median_pad16<E>[i - K < below ? 0 : 1]);
-  __syncthreads();
-  int64_t b, b_end;
-  block_range(nblk, b, b_end);
-  // this wave's share of a column block's DMA: instructions i = 4 k + wave,
-  // lane -> tile row P i + lane / NC, stored chunk lane % NC, whose source is
-  // chunk (lane % NC) ^ swz(row) of the row's column block
-  unsigned char* const tile_w = smem + __builtin_amdgcn_readfirstlane(wave) * 1024;
-  TileDma<R / 4> dma;
-#pragma unroll
-  for (int k = 0; k < R / 4; ++k) {
-    const int r = P * (4 * k + wave) + lane / NC;
-    const int c = (lane % NC) ^ slice_swz<P>(r);
-    const bool real = FULL || r < K;
-    dma.src[k] = real ? rows[r] + (uint64_t(b) * RB + uint64_t(c) * 16u) : rows[r];
-    dma.step[k] = real ? uint32_t(RB) : 0u;
-  }
-  const int sub = lane & (P - 1), p = lane / P;
-  // word j of lane (p, sub): tile row P j + sub, chunk wave * 16 / P + p / 4
-  // (stored at chunk ^ swz), dword p % 4; the swizzle depends on sub only
-  const int chunk = (wave * (16 / P) + p / 4) ^ slice_swz<P>(sub);
-  const uint32_t* tw = reinterpret_cast<const uint32_t*>(smem + sub * RB + chunk * 16) + (p & 3);
-  if (b < b_end) dma.issue(tile_w);
-  for (; b < b_end; ++b) {
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's DMA has landed
-    __builtin_amdgcn_s_barrier();        // ... and every wave's
-    __builtin_amdgcn_sched_barrier(0);
-    uint32_t raw[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) raw[j] = tw[256 * j];
-    uint32_t nanacc = 0;  // per half, max of |x| bits
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-      nanacc = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(ushort2_t, nanacc),
-                                                                       __builtin_bit_cast(ushort2_t, raw[j] & 0x7fff7fffu)));
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every word read ...
-    __builtin_amdgcn_s_barrier();        // ... by every wave before the tile is refilled
-    __builtin_amdgcn_sched_barrier(0);
-    if (b + 1 < b_end) {
-      dma.next();
-      dma.issue(tile_w);
-    }
-    // first NaN per half in client order as (client << 16 | bits), only in
-    // waves holding a NaN column; KMAX << 16: none
-    int first_lo = KMAX << 16, first_hi = KMAX << 16;
-    if (__ballot((nanacc & 0xffffu) > E::kPosInf || (nanacc >> 16) > E::kPosInf)) {
-#pragma unroll
-      for (int j = R - 1; j >= 0; --j) {  // predicated, walked backwards: the lowest client wins
-        const uint32_t x = raw[j];
-        const int s = (P * j + sub) << 16;
-        if ((x & 0x7fffu) > E::kPosInf) first_lo = s | int(x & 0xffffu);
-        if (((x >> 16) & 0x7fffu) > E::kPosInf) first_hi = s | int(x >> 16);
-      }
-#pragma unroll
-      for (int m = 1; m < P; m <<= 1) {
-        first_lo = min(first_lo, __shfl_xor(first_lo, m, 64));
-        first_hi = min(first_hi, __shfl_xor(first_hi, m, 64));
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < R / 32; ++g) pk16_slice_planes_group<R>(raw, g);
-    uint32_t bits = pk16_from_ukey(pk16_slice_select<P, R>(raw));
-    if (first_lo < (KMAX << 16)) bits = (bits & 0xffff0000u) | (uint32_t(first_lo) & 0xffffu);
-    if (first_hi < (KMAX << 16)) bits = (bits & 0xffffu) | (uint32_t(first_hi) << 16);
-    if (sub == 0) {
-      const int64_t e = b * (RB / 4) + wave * (64 / P) + p;  // column pair
-      *reinterpret_cast<uint32_t*>(out + 2 * e) = bits;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// One column per lane (the streamed form for K <= 512).  The pair kernels
-// above give a lane two columns of R clients and spend a v_perm_b32 per word
-// separating the columns (swap stage 16) and, per bit, the P-lane count
-// reduction for two columns.  Here a lane's word j holds ONE column of two
+// One column per lane.  The register kernel above gives a lane two columns
+// of R clients and spends a v_perm_b32 per word separating the columns (swap
+// stage 16) and, per bit, the P-lane count reduction for two columns (a
+// streamed form of it, measured in round 6, ran config 4 in 16.7 ms against
+// 15.0-15.6 for this one).  Here a lane's word j holds ONE column of two
 // clients, 2 (P j + s) in the low half and the next client in the high half,
 // assembled from the LDS tile by two 16-bit reads and a v_perm_b32; the half
 // bit is a client bit, so four swap
@@ -1235,10 +1132,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R == 64 ? 2
 // plane b of clients 32 g .. 32 g + 31 of the lane (the lane's client
 // 2 (P (16 g + i) + s) + h at position 2 i + h).  A lane holds 2 R clients of
 // its column, P = KMAX / (2 R) lanes per column.
-//   - Block: 4 waves x 64 / P columns = 256 / P columns = 512 / P bytes of
-//     every row per column block (P = 4: one 128-B line); tile KMAX x 512 / P
-//     bytes = R KB, R DMA instructions of 2 P rows each; a contiguous range
-//     of column blocks per block, as median_pk16_stream_kernel.
+//   - Block: WAVES waves x 64 / P columns = WAVES * 128 / P bytes of every
+//     row per column block (one 128-B line for (P, WAVES) = (4, 4) and
+//     (8, 8)); tile KMAX x that, R DMA instructions per wave-quarter; up to
+//     512 clients (4, 64, 4): 2 blocks per CU; up to 1024 (8, 64, 8): one
+//     block of 8 waves per CU (K = 1024 over 4M columns 1.43 ms against 1.85
+//     for the streamed pair form; profiles/r06/q/).
 //   - Per lane at K = 512: ~900 VALU instructions for its 128 keys (the pair
 //     form: ~1,500); config 4's median 15.0 ms against 16.7 ms for the pair
 //     form and 21.7 ms for the byte-wise counting (NOTES.md §5b).
@@ -1417,25 +1316,6 @@ int device_cu_count() {
   return cus[dev];
 }
 
-template <int P, int R, class E>
-int launch_median_pk16_stream(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
-  constexpr int COLS = 512 / P;  // columns per column block
-  const int64_t nblk = N / COLS;
-  if (nblk > 0) {
-    const int64_t cap = int64_t(device_cu_count()) * (R == 64 ? 2 : 1);  // resident blocks (LDS: R KB each)
-    const int64_t grid = nblk < cap ? nblk : cap;
-    if (K == P * R)
-      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, true, E>), dim3(unsigned(grid)), dim3(256), 0, st,
-                         src, K, nblk, out);
-    else
-      hipLaunchKernelGGL((median_pk16_stream_kernel<P, R, false, E>), dim3(unsigned(grid)), dim3(256), 0,
-                         st, src, K, nblk, out);
-    if (int rc = check_launch("fedagg_median")) return rc;
-  }
-  // the remaining columns (fewer than one column block) and the odd last one
-  return launch_median_pk16_lanes<P * R / 128, 128, E, 256, true>(src, K, N, out, st, nblk * (COLS / 2));
-}
-
 template <int P, int R, int WAVES, class E>
 int launch_median_pk16_colstream(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
   constexpr int COLS = WAVES * 64 / P;  // columns per column block
@@ -1557,11 +1437,10 @@ int median_dispatch(const typename E::S* const* d_src, int32_t K, int64_t N, typ
   if (K > 128) {  // 4 or 8 lanes per column, register sorts + cross-lane merges
     if constexpr (sizeof(typename E::S) == 2) {
       if (aligned && K <= 4096) {  // two columns per lane on packed int16 keys
-        // the bit-plane radix select, streamed through LDS: one column per
-        // lane up to 512 clients, column pairs up to 1024
+        // the bit-plane radix select streamed through LDS, one column per lane
         if (K <= 256) return launch_median_pk16_colstream<2, 64, 4, E>(d_src, K, N, d_out, st);
         if (K <= 512) return launch_median_pk16_colstream<4, 64, 4, E>(d_src, K, N, d_out, st);
-        if (K <= 1024) return launch_median_pk16_stream<8, 128, E>(d_src, K, N, d_out, st);
+        if (K <= 1024) return launch_median_pk16_colstream<8, 64, 8, E>(d_src, K, N, d_out, st);
         if (K <= 2048) return launch_median_pk16_lanes<16, 128, E>(d_src, K, N, d_out, st);
         return launch_median_pk16_lanes<32, 128, E>(d_src, K, N, d_out, st);
       }

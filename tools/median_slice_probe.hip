@@ -38,6 +38,12 @@ int probe_small_planes(const uint16_t* const* src, int K, int64_t N, uint16_t* o
   if (K <= 128) return launch_median_pk16_lanes<1, 128, E, 256, true>(src, K, N, out, st);
   return median_dispatch<E>(src, K, N, out, true, st);
 }
+// 513..1024 clients through the column kernel (8 lanes per column, 8-wave blocks, one per CU)
+template <class E>
+int probe_col1024(const uint16_t* const* src, int K, int64_t N, uint16_t* out, hipStream_t st) {
+  if (K > 512 && K <= 1024) return launch_median_pk16_colstream<8, 64, 8, E>(src, K, N, out, st);
+  return median_dispatch<E>(src, K, N, out, true, st);
+}
 template <class E>
 int probe_variant(int v, const uint16_t* const* s, int K, int64_t N, uint16_t* o, hipStream_t st) {
   switch (v) {
@@ -47,6 +53,7 @@ int probe_variant(int v, const uint16_t* const* s, int K, int64_t N, uint16_t* o
     case 4: return probe_col32<E>(s, K, N, o, st);
     case 5: return probe_k128_planes<E>(s, K, N, o, st);
     case 6: return probe_small_planes<E>(s, K, N, o, st);
+    case 7: return probe_col1024<E>(s, K, N, o, st);
   }
   return 1;
 }
@@ -54,8 +61,8 @@ int probe_variant(int v, const uint16_t* const* s, int K, int64_t N, uint16_t* o
 
 extern "C" const char* slice_probe_name(int v) {
   static const char* n[] = {"", "shipped", "planes_regs", "networks_regs", "col_r32_w8", "k128_planes",
-                           "small_planes"};
-  return (v >= 1 && v <= 6) ? n[v] : "";
+                           "small_planes", "col_k1024"};
+  return (v >= 1 && v <= 7) ? n[v] : "";
 }
 
 // v: variant (slice_probe_name); f16: 0 bf16 rows, 1 f16 rows

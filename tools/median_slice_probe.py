@@ -116,7 +116,11 @@ def main():
     shapes = [(torch.bfloat16, 256, 8_000_000, False), (torch.bfloat16, 512, 8_000_000, False),
               (torch.bfloat16, 1024, 4_000_000, False), (torch.float16, 512, 8_000_000, False),
               (torch.bfloat16, 512, 8_000_000, True), (torch.bfloat16, 512, 86_567_656, False)]
-    if os.environ.get("PROBE_SMALLK"):
+    if os.environ.get("PROBE_BIGK"):
+        shapes = [(torch.bfloat16, 1024, 4_000_000, False), (torch.bfloat16, 700, 4_000_000, False),
+                  (torch.float16, 1024, 4_000_000, False), (torch.bfloat16, 1024, 4_000_000, True),
+                  (torch.bfloat16, 1024, 43_283_828, False)]
+    elif os.environ.get("PROBE_SMALLK"):
         shapes = [(torch.bfloat16, k, 8_000_000, False) for k in (16, 32, 48, 64, 96, 100, 128)]
         shapes += [(torch.bfloat16, 128, 8_000_000, True), (torch.bfloat16, 64, 86_567_656, False),
                    (torch.bfloat16, 128, 86_567_656, False)]
