@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <string>
 #include <type_traits>
 #include <utility>
@@ -1304,16 +1305,19 @@ median_pk16_colstream_kernel(const uint16_t* const* __restrict__ src, int K, int
   }
 }
 
+// CUs of the current device (the persistent kernels' resident grid), cached
+// per device; callers on several threads may race to fill an entry with the
+// same value, hence the relaxed atomics
 int device_cu_count() {
-  static int cus[64] = {0};
+  static std::atomic<int> cus[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cus[dev]) {
-    int n = 0;
+  int n = cus[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
+    cus[dev].store(n, std::memory_order_relaxed);
   }
-  return cus[dev];
+  return n;
 }
 
 template <int P, int R, int WAVES, class E>
